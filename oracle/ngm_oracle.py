@@ -1,0 +1,456 @@
+"""CPU restatement of ``Net.forward`` (reference ``src/model/ngm.py:205-491``) — TEST ORACLE ONLY.
+
+See ``oracle/__init__.py`` for the rules (never imported by the product path).  Every function
+cites the reference file:line (or the pinned third-party algorithm) it restates.  All arithmetic
+is PyTorch CPU in ``dtype`` (fp32 by default, like the reference; fp64 for sensitivity studies).
+"""
+import math
+
+import numpy as np
+import scipy.optimize as opt
+import torch
+import torch.nn.functional as F
+
+TAU = 0.01               # ngm.py:45
+SK_ITER = 10             # ngm.py:53
+GNN_SK_ITER = 20         # gnn.py:182 (PYGNNLayer default sk_iter)
+UNIV = 600               # ngm.py:52
+K_FACTOR = 50.0          # ngm.py:55
+SPLINE = "message_pass_node_features.mp_network.convs"
+
+__all__ = [
+    "spline_basis", "spline_conv", "siamese_sconv", "edge_diff", "global_weights", "affinity",
+    "kron_pattern", "pattern_mean_explicit", "pattern_mean_factorized", "pygm_sinkhorn",
+    "gnn_layer", "afau_encoder", "afau_ks", "sinkhorn_m", "soft_topk", "hungarian",
+    "greedy_perm", "match_classifier", "gconv", "forward",
+]
+
+
+# ----------------------------------------------------------------------------------------------
+# SplineConv (PyG 1.6.3 SplineConv(768, 768, dim=2, kernel_size=5, aggr='max'),
+# torch-spline-conv 1.2.0 open B-spline degree 1) — restated, parity unpinned.
+# Call sites: src/model/spline_conv.py:17,35,38.
+# ----------------------------------------------------------------------------------------------
+def spline_basis(pseudo, kernel_size=5):
+    """torch_spline_conv ``spline_basis`` (degree 1, open): (E,2) -> basis (E,4), weight_index (E,4)."""
+    pseudo = pseudo.float()
+    v = pseudo * float(kernel_size - 1)            # open spline: kernel_size - degree
+    fl = torch.floor(v)
+    frac = v - fl
+    fi = fl.long()
+    basis = torch.ones(pseudo.shape[0], 4, dtype=torch.float32)
+    wi = torch.zeros(pseudo.shape[0], 4, dtype=torch.long)
+    for s in range(4):
+        off = 1
+        b = torch.ones(pseudo.shape[0], dtype=torch.float32)
+        w = torch.zeros(pseudo.shape[0], dtype=torch.long)
+        for d in range(2):
+            km = (s >> d) & 1
+            w = w + ((fi[:, d] + km) % kernel_size) * off
+            off *= kernel_size
+            b = b * (frac[:, d] if km else 1.0 - frac[:, d])
+        basis[:, s] = b
+        wi[:, s] = w
+    return basis, wi
+
+
+def spline_conv(x, edge_index, pseudo, weight, root, bias):
+    """One SplineConv layer with max aggregation (messages src->dst, empty segment -> 0).
+
+    out_i = max_{e: dst_e = i} sum_s B_s(u_e) x_{src_e} W[k_s(u_e)]   (+ x_i R) (+ beta)
+    """
+    dt = x.dtype
+    n, d = x.shape
+    basis, wi = spline_basis(pseudo)
+    basis = basis.to(dt)
+    K = weight.shape[0]
+    Y = (x @ weight.to(dt).permute(1, 0, 2).reshape(d, -1)).view(n, K, -1)   # node-GEMM form
+    src, dst = edge_index[0].long(), edge_index[1].long()
+    msg = None
+    for s in range(4):
+        t = basis[:, s:s + 1] * Y[src, wi[:, s]]
+        msg = t if msg is None else msg + t
+    out = torch.zeros(n, Y.shape[-1], dtype=dt)
+    if src.numel():
+        out = out.scatter_reduce(0, dst[:, None].expand(-1, Y.shape[-1]), msg, reduce="amax",
+                                 include_self=False)
+    out = out + x @ root.to(dt)
+    out = out + bias.to(dt)
+    return out
+
+
+def siamese_sconv(x, edge_index, pseudo, sd, prefix=SPLINE):
+    """SiameseSConvOnNodes (spline_conv.py:51-57) over SConv (spline_conv.py:28-41)."""
+    h = F.relu(spline_conv(x, edge_index, pseudo, sd[prefix + ".0.weight"], sd[prefix + ".0.root"],
+                           sd[prefix + ".0.bias"]))
+    o = spline_conv(h, edge_index, pseudo, sd[prefix + ".1.weight"], sd[prefix + ".1.root"],
+                    sd[prefix + ".1.bias"])
+    return x + 0.1 * o
+
+
+def edge_diff(x, edge_index):
+    """vertex_attr_to_edge_attr (spline_conv.py:73-81): Xe[e] = x[src] - x[dst]."""
+    return x[edge_index[0].long()] - x[edge_index[1].long()]
+
+
+# ----------------------------------------------------------------------------------------------
+# Affinities (ngm.py:262-287, affinity_layer.py:11-19)
+# ----------------------------------------------------------------------------------------------
+def global_weights(w1, w2):
+    """ngm.py:262-268: normalize_over_channels(cat(g_src, g_tgt)) per pair, (B,1024)."""
+    g = torch.cat([w1, w2], dim=-1)
+    return g / torch.norm(g, dim=1, keepdim=True)
+
+
+def affinity(X, Y, w, A_weight, A_bias):
+    """InnerProductWithWeightsAffinity._forward (affinity_layer.py:11-19), use_global=True."""
+    c = torch.tanh(F.linear(w, A_weight.to(X.dtype), A_bias.to(X.dtype)))
+    res = torch.matmul(X * c, Y.transpose(0, 1))
+    return F.softplus(res) - 0.5
+
+
+# ----------------------------------------------------------------------------------------------
+# Association graph pattern (gmdataset.py:614-642, factorize_graph_matching.py:90-95,
+# ngm.py:339-344) and SAGEConv mean aggregation over it (gnn.py:208; PyG 1.6.3
+# SAGEConv.message_and_aggregate + torch_sparse matmul(reduce='mean'): values are dropped).
+# ----------------------------------------------------------------------------------------------
+def kron_pattern(ei1, ei2, n1max, n2max, n1b, n2b):
+    """Explicit (row, col) index lists of one pair's sparse affinity pattern.
+
+    Kronecker entries: for edge a->c in g1 (index e1) and b->d in g2 (e2), ordered column-major
+    over edge pairs (e2 outer, e1 inner): row = p(a,b), col = p(c,d) with p(i,j) = j*n1max + i.
+    Diagonal: (q, q) for q < n1b*n2b in padded p-space (quirk A.10(ii)).
+    """
+    s1, d1 = ei1[0].long(), ei1[1].long()
+    s2, d2 = ei2[0].long(), ei2[1].long()
+    E1, E2 = s1.numel(), s2.numel()
+    e1 = torch.arange(E1).repeat(E2)
+    e2 = torch.arange(E2).repeat_interleave(E1)
+    row = s2[e2] * n1max + s1[e1]
+    col = d2[e2] * n1max + d1[e1]
+    q = torch.arange(n1b * n2b)
+    return torch.cat([row, q]), torch.cat([col, q])
+
+
+def pattern_mean_explicit(x, row, col, N):
+    """agg[p] = mean_{k: col_k = p} x[row_k]  (count clamped to >= 1)."""
+    agg = torch.zeros(N, x.shape[1], dtype=x.dtype)
+    agg.index_add_(0, col, x[row])
+    cnt = torch.zeros(N, dtype=x.dtype)
+    cnt.index_add_(0, col, torch.ones(col.numel(), dtype=x.dtype))
+    return agg / cnt.clamp(min=1)[:, None]
+
+
+def pattern_mean_factorized(x, ei1, ei2, n1max, n2max, n1b, n2b):
+    """Same aggregation without materialising the pattern:
+    (A1 X A2^T + D o X) / (deg1 deg2^T + D), D[p] = [p < n1b*n2b], X[i,j] = x[p(i,j)]."""
+    C = x.shape[1]
+    Xm = x.view(n2max, n1max, C).permute(1, 0, 2)           # [i][j][c]
+    A1 = torch.zeros(n1max, n1max, dtype=x.dtype)
+    A1[ei1[1].long(), ei1[0].long()] = 1.0                  # A1[c, a] for edge a->c
+    A2 = torch.zeros(n2max, n2max, dtype=x.dtype)
+    A2[ei2[1].long(), ei2[0].long()] = 1.0
+    T = torch.einsum("ca,abk->cbk", A1, Xm)
+    T = torch.einsum("db,cbk->cdk", A2, T)
+    dmask = (torch.arange(n2max * n1max) < n1b * n2b).to(x.dtype).view(n2max, n1max).t()
+    num = T + dmask[:, :, None] * Xm
+    den = A1.sum(1)[:, None] * A2.sum(1)[None, :] + dmask
+    agg = num / den.clamp(min=1)[:, :, None]
+    return agg.permute(1, 0, 2).reshape(n2max * n1max, C)
+
+
+# ----------------------------------------------------------------------------------------------
+# pygmtools 0.5.3 pytorch ``sinkhorn`` (called at sinkhorn.py:87 with batched_operation=False)
+# — restated, parity unpinned (its log-domain step is the one Sinkhorn_m runs, pinned via soft_topk).
+# ----------------------------------------------------------------------------------------------
+def pygm_sinkhorn(s, n1, n2, dummy_row=False, max_iter=10, tau=1.0):
+    B = s.shape[0]
+    out = torch.zeros_like(s)
+    for b in range(B):
+        r, c = int(n1[b]), int(n2[b])
+        L = s[b, :r, :c] / tau
+        transposed = r > c
+        if transposed:
+            L = L.t()
+            r, c = c, r
+        if dummy_row and c > r:
+            L = torch.cat([L, torch.full((c - r, c), -100.0, dtype=L.dtype)], 0)
+        for i in range(max_iter):
+            if i % 2 == 0:
+                L = L - torch.logsumexp(L, 1, keepdim=True)
+            else:
+                L = L - torch.logsumexp(L, 0, keepdim=True)
+            L[torch.isnan(L)] = -float("inf")
+        P = torch.exp(L[:r])
+        if transposed:
+            P = P.t()
+        out[b, :P.shape[0], :P.shape[1]] = P
+    return out
+
+
+def gnn_layer(x, sd, l, agg_fn, n1max, n2max, n1b, n2b, tau=TAU, sk_iter=GNN_SK_ITER):
+    """PYGNNLayer.forward (gnn.py:207-226) for one pair: x (N, C_in) -> (N, 17)."""
+    p = "gnn_layer_%d" % l
+    dt = x.dtype
+    g = lambda k: sd[p + k].to(dt)
+    agg = agg_fn(x)
+    x1 = F.linear(agg, g(".conv2.lin_l.weight"), g(".conv2.lin_l.bias")) + \
+        F.linear(x, g(".conv2.lin_r.weight"))
+    h = F.relu(F.linear(x, g(".n_self_func.0.weight"), g(".n_self_func.0.bias")))
+    x1 = x1 + F.relu(F.linear(h, g(".n_self_func.2.weight"), g(".n_self_func.2.bias")))
+    z = F.linear(x1, g(".classifier.weight"), g(".classifier.bias"))        # (N, 1)
+    Z = z.t().reshape(1, n2max, n1max).transpose(1, 2)
+    S = pygm_sinkhorn(Z, [n1b], [n2b], dummy_row=True, max_iter=sk_iter, tau=tau)
+    x5 = S.transpose(2, 1).contiguous().reshape(1, 1, n1max * n2max).permute(0, 2, 1)[0]
+    return torch.cat([x1, x5], dim=-1)
+
+
+# ----------------------------------------------------------------------------------------------
+# AFA-U k regressor (ngm.py:386-412; afau.py:54-300)
+# ----------------------------------------------------------------------------------------------
+def _instnorm(x, w, b, eps=1e-5):
+    """AddAndInstanceNormalization (afau.py:154-176): InstanceNorm1d over positions."""
+    return F.instance_norm(x.transpose(1, 2), weight=w, bias=b, eps=eps).transpose(1, 2)
+
+
+def _encoding_block(a, bemb, cost, sd, p):
+    dt = a.dtype
+    g = lambda k: sd[p + k].to(dt)
+    B, R, _ = a.shape
+    Cn = bemb.shape[1]
+    H, D = 16, 16
+    q = F.linear(a, g(".Wq.weight")).reshape(B, R, H, D).transpose(1, 2)
+    k = F.linear(bemb, g(".Wk.weight")).reshape(B, Cn, H, D).transpose(1, 2)
+    v = F.linear(bemb, g(".Wv.weight")).reshape(B, Cn, H, D).transpose(1, 2)
+    dot = torch.matmul(q, k.transpose(2, 3)) / math.sqrt(16)
+    cs = cost[:, None, :, :].expand(B, H, R, Cn)
+    two = torch.stack((dot, cs), dim=4).transpose(1, 2)                 # (B, R, H, Cn, 2)
+    ms1 = torch.matmul(two, g(".mixed_score_MHA.mix1_weight"))
+    ms1 = ms1 + g(".mixed_score_MHA.mix1_bias")[None, None, :, None, :]
+    ms2 = torch.matmul(F.relu(ms1), g(".mixed_score_MHA.mix2_weight"))
+    ms2 = ms2 + g(".mixed_score_MHA.mix2_bias")[None, None, :, None, :]
+    mixed = ms2.transpose(1, 2).squeeze(4)                              # (B, H, R, Cn)
+    w = torch.softmax(mixed, dim=3)
+    out = torch.matmul(w, v).transpose(1, 2).reshape(B, R, H * D)
+    mh = F.linear(out, g(".multi_head_combine.weight"), g(".multi_head_combine.bias"))
+    o1 = _instnorm(a + mh, g(".add_n_normalization_1.norm.weight"), g(".add_n_normalization_1.norm.bias"))
+    ff = F.linear(F.relu(F.linear(o1, g(".feed_forward.W1.weight"), g(".feed_forward.W1.bias"))),
+                  g(".feed_forward.W2.weight"), g(".feed_forward.W2.bias"))
+    return _instnorm(o1 + ff, g(".add_n_normalization_2.norm.weight"), g(".add_n_normalization_2.norm.bias"))
+
+
+def afau_encoder(row_emb, col_emb, cost, sd):
+    """Encoder -> EncoderLayer (afau.py:54-57, 82-83)."""
+    p = "encoder_k.layers.0."
+    r = _encoding_block(row_emb, col_emb, cost, sd, p + "row_encoding_block")
+    c = _encoding_block(col_emb, row_emb, cost.transpose(1, 2), sd, p + "col_encoding_block")
+    return r, c
+
+
+def afau_ks(ss, n1, n2, sd):
+    """ngm.py:386-412: predicted k ratio ``ks`` (B,)."""
+    dt = ss.dtype
+    B = ss.shape[0]
+    n1max, n2max = int(max(n1)), int(max(n2))
+    row0 = torch.zeros(B, n1max, UNIV, dtype=dt)
+    col0 = torch.zeros(B, n2max, UNIV, dtype=dt)
+    for b in range(B):
+        nb = int(n2[b])
+        col0[b, torch.arange(nb), torch.arange(nb)] = 1.0
+    r, c = afau_encoder(row0, col0, ss, sd)
+    gr = r.max(dim=1).values            # pad to 600 with -inf then MaxPool1d(600)
+    gc = c.max(dim=1).values
+    g = lambda k: sd[k].to(dt)
+    kr = F.linear(F.relu(F.linear(gr, g("final_row.0.weight"), g("final_row.0.bias"))),
+                  g("final_row.2.weight"), g("final_row.2.bias")).squeeze(-1)
+    kc = F.linear(F.relu(F.linear(gc, g("final_col.0.weight"), g("final_col.0.bias"))),
+                  g("final_col.2.weight"), g("final_col.2.bias")).squeeze(-1)
+    return torch.sigmoid((kr + kc) / 2)
+
+
+# ----------------------------------------------------------------------------------------------
+# Soft top-k (soft_topk.py:8-53, Sinkhorn_m.forward_log soft_topk.py:166-255)
+# ----------------------------------------------------------------------------------------------
+def sinkhorn_m(dist_list, row_prob, col_prob, nrows, ncols, max_iter=10, tau=TAU):
+    """Sinkhorn_m.forward_log, batched_operation=False branch incl. the while loop (:214-255)."""
+    B = len(dist_list)
+    dt = dist_list[0].dtype
+    s = [d / tau for d in dist_list]
+    lrp = torch.log(row_prob).unsqueeze(2)
+    lcp = torch.log(col_prob).unsqueeze(1)
+    N = int(max(nrows)) * int(max(ncols))
+    ret = torch.full((B, N, 2), -float("inf"), dtype=dt)
+    for b in range(B):
+        L = s[b]
+        nn_ = int(nrows[b]) * int(ncols[b])
+
+        def step(L, i):
+            if i % 2 == 0:
+                L = L - torch.logsumexp(L, 1, keepdim=True) + lrp[b, 0:nn_]
+            else:
+                L = L - torch.logsumexp(L, 0, keepdim=True) + lcp[b]
+            L[torch.isnan(L)] = -float("inf")
+            return L
+        for i in range(max_iter):
+            L = step(L, i)
+        st = max_iter
+        while torch.any(L > 0):
+            L = step(L, st)
+            st += 1
+        ret[b, 0:nn_] = L
+    return torch.exp(ret)
+
+
+def soft_topk(scores, ks, nrows, ncols, max_iter=10, tau=TAU):
+    """soft_topk(..., return_prob=True)[1] — the soft top-k matrix ``ds_mat`` (soft_topk.py:23-45)."""
+    B = scores.shape[0]
+    dt = scores.dtype
+    dist = []
+    for b in range(B):
+        n1, n2 = int(nrows[b]), int(ncols[b])
+        blk = scores[b, 0:n1, 0:n2]
+        anchors = torch.stack([blk.min(), blk.max()])
+        dist.append(-torch.abs(blk.reshape(-1).unsqueeze(-1) - anchors.unsqueeze(0)))
+    row_prob = torch.ones(B, scores.shape[1] * scores.shape[2], dtype=dt)
+    col_prob = torch.zeros(B, 2, dtype=dt)
+    col_prob[:, 1] += ks
+    col_prob[:, 0] += torch.as_tensor(nrows) * torch.as_tensor(ncols) - ks
+    out = sinkhorn_m(dist, row_prob, col_prob, nrows, ncols, max_iter, tau)
+    ds = torch.zeros_like(scores)
+    for b in range(B):
+        n1, n2 = int(nrows[b]), int(ncols[b])
+        ds[b, 0:n1, 0:n2] = out[b, 0:n1 * n2, 1].view(n1, -1)
+    return ds
+
+
+def hungarian(s, n1, n2):
+    """utils/hungarian.py:8-66: scipy LSA on -s (nproc=1)."""
+    pm = s.detach().cpu().float().numpy() * -1
+    res = []
+    for b in range(pm.shape[0]):
+        r, c = opt.linear_sum_assignment(pm[b][:int(n1[b]), :int(n2[b])])
+        m = np.zeros_like(pm[b])
+        m[r, c] = 1
+        res.append(m)
+    return torch.from_numpy(np.stack(res))
+
+
+def greedy_perm(x, top_indices, ks):
+    """soft_topk.py:56-77 (round() is Python's half-to-even)."""
+    x = x.clone()
+    for b in range(x.shape[0]):
+        matched = 0
+        cur = 0
+        ref = round(float(ks[b]))
+        while matched < ref and cur < top_indices.shape[1]:
+            idx = int(top_indices[b][cur])
+            row, col = idx // x.shape[2], idx % x.shape[2]
+            if x[b, :, col].sum() < 1 and x[b, row, :].sum() < 1:
+                x[b, row, col] = 1
+                matched += 1
+            cur += 1
+    return x
+
+
+# ----------------------------------------------------------------------------------------------
+# MatchClassifier (ngm.py:75-106), eval-mode BatchNorm (running stats)
+# ----------------------------------------------------------------------------------------------
+def match_classifier(m, sd, eps=1e-5):
+    dt = m.dtype
+    g = lambda k: sd[k].to(dt)
+    x = m.unsqueeze(1)
+    for ci, bi in ((0, 2), (4, 6)):
+        x = F.conv2d(x, g("match_cls.conv.%d.weight" % ci), g("match_cls.conv.%d.bias" % ci), padding=1)
+        x = F.relu(x)
+        x = F.batch_norm(x, g("match_cls.conv.%d.running_mean" % bi), g("match_cls.conv.%d.running_var" % bi),
+                         g("match_cls.conv.%d.weight" % bi), g("match_cls.conv.%d.bias" % bi), False, 0.0, eps)
+        x = F.max_pool2d(x, 2)
+    x = F.adaptive_avg_pool2d(x, 1).view(x.shape[0], -1)
+    return F.linear(x, g("match_cls.fc.weight"), g("match_cls.fc.bias")).squeeze(-1)
+
+
+def gconv(A, x, a_w, a_b, u_w, u_b, norm=True):
+    """Gconv.forward (src/model/gcn.py:24-38)."""
+    if norm:
+        A = F.normalize(A, p=1, dim=-2)
+    return torch.bmm(A, F.relu(F.linear(x, a_w, a_b))) + F.relu(F.linear(x, u_w, u_b))
+
+
+# ----------------------------------------------------------------------------------------------
+# Net.forward (ngm.py:205-491) from node features (synthetic bypass of backbone+feature_align)
+# ----------------------------------------------------------------------------------------------
+def forward(pairs, sd, regression=True, training=False, gt_perm=None, labels=None,
+            dtype=torch.float32, explicit_pattern=False, stages=None):
+    """pairs: list of (g0, g1) dicts as produced by ``fpm.synth.make_graph`` (keys x, w,
+    edge_index, pseudo, n).  Returns the data_dict keys written at ngm.py:479-487 plus the
+    intermediates ``s``, ``ss``, ``Kp`` used by the parity tests."""
+    B = len(pairs)
+    n1 = torch.tensor([p[0]["n"] for p in pairs])
+    n2 = torch.tensor([p[1]["n"] for p in pairs])
+    n1max, n2max = int(n1.max()), int(n2.max())
+    N = n1max * n2max
+    T = lambda a: torch.as_tensor(a)
+    feats = [[], []]
+    for side in range(2):
+        for p in pairs:
+            g = p[side]
+            x = T(g["x"]).to(dtype)
+            feats[side].append(siamese_sconv(x, T(g["edge_index"]), T(g["pseudo"]), sd))
+    w1 = torch.stack([T(p[0]["w"]) for p in pairs]).to(dtype)
+    w2 = torch.stack([T(p[1]["w"]) for p in pairs]).to(dtype)
+    gw = global_weights(w1, w2)
+    Kp = torch.zeros(B, n1max, n2max, dtype=dtype)
+    for b in range(B):
+        kp = affinity(feats[0][b], feats[1][b], gw[b], sd["vertex_affinity.A.weight"],
+                      sd["vertex_affinity.A.bias"])
+        Kp[b, :kp.shape[0], :kp.shape[1]] = kp
+    emb = Kp.transpose(1, 2).contiguous().view(B, -1, 1)
+    qap = []
+    for b in range(B):
+        ei1, ei2 = T(pairs[b][0]["edge_index"]), T(pairs[b][1]["edge_index"])
+        n1b, n2b = int(n1[b]), int(n2[b])
+        if explicit_pattern:
+            row, col = kron_pattern(ei1, ei2, n1max, n2max, n1b, n2b)
+            agg_fn = lambda x, row=row, col=col: pattern_mean_explicit(x, row, col, N)
+        else:
+            agg_fn = lambda x, ei1=ei1, ei2=ei2, n1b=n1b, n2b=n2b: pattern_mean_factorized(
+                x, ei1, ei2, n1max, n2max, n1b, n2b)
+        x = emb[b]
+        for l in range(3):
+            x = gnn_layer(x, sd, l, agg_fn, n1max, n2max, n1b, n2b)
+        qap.append(x)
+    emb = torch.stack(qap)
+    v = F.linear(emb, sd["classifier.weight"].to(dtype), sd["classifier.bias"].to(dtype))
+    s = v.view(B, n2max, -1).transpose(1, 2)
+    ss = pygm_sinkhorn(s, n1, n2, dummy_row=True, max_iter=SK_ITER, tau=TAU)
+    min_pt = torch.minimum(n1, n2).to(dtype)
+    if gt_perm is None:
+        gt_perm = torch.zeros(B, n1max, n2max, dtype=dtype)
+        for b in range(B):
+            m = min(int(n1[b]), int(n2[b]))
+            gt_perm[b, torch.arange(m), torch.arange(m)] = 1
+    gt_ks = gt_perm.reshape(B, -1).sum(-1).to(dtype)
+    if regression:
+        ks = afau_ks(ss, n1, n2, sd)
+    else:
+        ks = gt_ks / min_pt
+    k_used = gt_ks.view(-1) if training else ks.view(-1) * min_pt
+    ds = soft_topk(ss, k_used, n1, n2, SK_ITER, TAU)
+    x = hungarian(ds, n1, n2).to(dtype)
+    top = torch.argsort(x.mul(ds).reshape(B, -1), descending=True, dim=-1)
+    perm = greedy_perm(torch.zeros_like(ds), top, ks.view(-1) * min_pt)
+    logits = match_classifier(s * perm, sd)
+    cls_prob = torch.sigmoid(logits)
+    out = dict(ds_mat=ds, perm_mat=perm, k_prob=ks, cls_prob=cls_prob, cls_logits=logits,
+               s=s, ss=ss, Kp=Kp, lsa=x)
+    if labels is not None:
+        out["cls_loss"] = F.binary_cross_entropy_with_logits(logits, T(labels).to(dtype).view(-1))
+    else:
+        out["cls_loss"] = torch.tensor(0.0, dtype=dtype)
+    if regression:
+        out["ks_loss"] = F.mse_loss(ks, gt_ks / min_pt) * K_FACTOR
+        out["ks_error"] = F.l1_loss(ks * min_pt, gt_ks)
+    else:
+        out["ks_loss"] = 0.0
+        out["ks_error"] = 0.0
+    return out

@@ -1,0 +1,172 @@
+"""Generate golden vectors from the reference's own importable modules.
+
+Run ONLY in the build container (the reference tree does not exist on the GPU box):
+
+    cd /tmp && PYTHONDONTWRITEBYTECODE=1 SPHINX=1 PYTHONPATH=/root/reference:/root/repo \
+        python /root/repo/tests/golden/make_golden.py
+
+``SPHINX=1`` is the reference's own switch that skips the nvcc JIT of ``src/extension``
+(``src/sparse_torch/csx_matrix.py:7``, ``src/sparse.py:10``).  Only inputs and outputs are
+written (``tests/golden/*.npz``); no reference source is copied.  Modules used:
+``src.model.soft_topk`` (soft_topk -> Sinkhorn_m, greedy_perm), ``src.model.afau.Encoder``,
+``src.model.affinity_layer``, ``src.model.gcn.Gconv``, ``utils.hungarian``,
+``utils.build_graphs``, ``utils.factorize_graph_matching`` + ``src.sparse_torch``.
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+import fpm  # noqa: E402  (seeded params + synthetic graphs; no reference code)
+from fpm import params, synth  # noqa: E402
+
+from src.model.soft_topk import soft_topk, greedy_perm  # noqa: E402
+from src.model.afau import Encoder  # noqa: E402
+from src.model.affinity_layer import InnerProductWithWeightsAffinity  # noqa: E402
+from src.model.gcn import Gconv  # noqa: E402
+from utils.hungarian import hungarian  # noqa: E402
+from utils.build_graphs import build_graphs  # noqa: E402
+from utils.factorize_graph_matching import kronecker_sparse, construct_sparse_aff_mat  # noqa: E402
+from src.sparse_torch import CSCMatrix3d  # noqa: E402
+
+
+def save(name, **arrs):
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **{k: np.asarray(v) for k, v in arrs.items()})
+    print("wrote", path, sorted(arrs))
+
+
+def gen_soft_topk():
+    g = torch.Generator().manual_seed(11)
+    cases = []
+    # (n1, n2) per pair; B=3 incl. a ragged pair; scores shaped like Sinkhorn outputs in [0,1]
+    for ci, (ns1, ns2) in enumerate([((8, 8, 8), (8, 8, 8)), ((6, 8, 7), (8, 8, 5)), ((16, 12), (16, 14))]):
+        B = len(ns1)
+        n1m, n2m = max(ns1), max(ns2)
+        sc = torch.zeros(B, n1m, n2m)
+        for b in range(B):
+            sc[b, :ns1[b], :ns2[b]] = torch.rand(ns1[b], ns2[b], generator=g) ** 3
+        ks = torch.tensor([min(a, b) * f for a, b, f in list(zip(ns1, ns2, (0.37, 0.62, 0.81)))[:B]],
+                          dtype=torch.float32)
+        nr, nc = torch.tensor(ns1), torch.tensor(ns2)
+        x, ss = soft_topk(sc, ks, 10, 0.01, nr, nc, True)
+        cases.append(dict(scores=sc.numpy(), ks=ks.numpy(), n1=nr.numpy(), n2=nc.numpy(),
+                          ss_out=ss.numpy(), x=x.numpy()))
+    save("soft_topk", **{"c%d_%s" % (i, k): v for i, c in enumerate(cases) for k, v in c.items()},
+         ncases=len(cases))
+
+
+def gen_hungarian_greedy():
+    g = torch.Generator().manual_seed(12)
+    B, n1, n2 = 3, 9, 10
+    s = torch.rand(B, n1, n2, generator=g)
+    s[1, :, 7] = 0.0                       # ties
+    nr = torch.tensor([9, 7, 9])
+    nc = torch.tensor([10, 10, 6])
+    x = hungarian(s, nr, nc)
+    ks = torch.tensor([4.5, 5.5, 3.2])     # .5 -> half-to-even rounding
+    top = torch.argsort(x.mul(s).reshape(B, -1), descending=True, dim=-1)
+    perm = greedy_perm(torch.zeros(s.shape), top, ks)
+    save("hungarian_greedy", s=s.numpy(), n1=nr.numpy(), n2=nc.numpy(), x=x.numpy(), ks=ks.numpy(),
+         top=top.numpy(), perm=perm.numpy())
+
+
+def gen_encoder():
+    sd = params.init_params(5)
+    enc = Encoder()
+    esd = {k[len("encoder_k."):]: v for k, v in sd.items() if k.startswith("encoder_k.")}
+    enc.load_state_dict(esd)
+    enc.eval()
+    g = torch.Generator().manual_seed(14)
+    B, n1m, n2m = 2, 10, 12
+    ns2 = [12, 9]
+    row = torch.zeros(B, n1m, 600)
+    col = torch.zeros(B, n2m, 600)
+    for b in range(B):
+        col[b, torch.arange(ns2[b]), torch.arange(ns2[b])] = 1
+    cost = torch.rand(B, n1m, n2m, generator=g)
+    cost[1, :, 9:] = 0
+    with torch.no_grad():
+        r, c = enc(row, col, cost)
+        # general (non-zero) row embedding exercises the q/k path too
+        row2 = torch.randn(B, n1m, 600, generator=g) * 0.1
+        r2, c2 = enc(row2, col, cost)
+    save("afau_encoder", seed=5, row=row.numpy(), col=col.numpy(), cost=cost.numpy(), r=r.numpy(),
+         c=c.numpy(), row2=row2.numpy(), r2=r2.numpy(), c2=c2.numpy())
+
+
+def gen_affinity():
+    sd = params.init_params(6)
+    aff = InnerProductWithWeightsAffinity(1024, 768)
+    aff.A.weight.data.copy_(sd["vertex_affinity.A.weight"])
+    aff.A.bias.data.copy_(sd["vertex_affinity.A.bias"])
+    g = torch.Generator().manual_seed(15)
+    X = [torch.randn(7, 768, generator=g) * 0.05, torch.randn(5, 768, generator=g) * 0.05]
+    Y = [torch.randn(9, 768, generator=g) * 0.05, torch.randn(5, 768, generator=g) * 0.05]
+    W = torch.rand(2, 1024, generator=g)
+    W = W / W.norm(dim=1, keepdim=True)
+    with torch.no_grad():
+        out = aff(X, Y, W)
+    save("affinity", seed=6, X0=X[0].numpy(), X1=X[1].numpy(), Y0=Y[0].numpy(), Y1=Y[1].numpy(),
+         W=W.numpy(), K0=out[0].numpy(), K1=out[1].numpy())
+
+
+def gen_graphs_and_pattern():
+    rng = np.random.default_rng(16)
+    P1 = np.stack([rng.uniform(0, 320, 9), rng.uniform(0, 240, 9)], 1)
+    P2 = np.stack([rng.uniform(0, 320, 7), rng.uniform(0, 240, 7)], 1)
+    A1, G1, H1, e1 = build_graphs(P1, 9, stg="tri", sym=True)
+    A2, G2, H2, e2 = build_graphs(P2, 7, stg="tri", sym=True)
+    # collate (src/gmdataset.py:623-634): per-pair K1G = kron(G2, G1) in CSC, K1H = kron(H2, H1)^T
+    n1max = 9
+    K1G = [kronecker_sparse(G2, G1).astype(np.float32)]
+    K1H = [kronecker_sparse(H2, H1).astype(np.float32)]
+    kro_G = CSCMatrix3d(K1G).indices
+    kro_H = CSCMatrix3d(K1H).transpose().indices
+    Ke = torch.arange(e1 * e2, dtype=torch.float32).view(e1, e2) + 1000
+    Kp = torch.arange(9 * 7, dtype=torch.float32).view(9, 7)
+    val, row, col = construct_sparse_aff_mat(Ke, Kp, kro_G.float(), kro_H.float())
+    save("graphs_pattern", P1=P1, P2=P2, A1=A1, G1=G1, H1=H1, A2=A2, G2=G2, H2=H2, n1max=n1max,
+         kro_G=kro_G.numpy(), kro_H=kro_H.numpy(), val=val.numpy(), row=row.numpy(), col=col.numpy())
+
+
+def gen_pyg_edges():
+    """Edge list/pseudo built the way GMDataset.to_pyg_graph does (gmdataset.py:170-189):
+    restated in fpm.synth; pin the Delaunay adjacency against build_graphs('tri')."""
+    out = {}
+    for i, n in enumerate((12, 40)):
+        g = synth.make_graph(77, i, 0, n)
+        A, G, H, e = build_graphs(g["P"].astype(np.float64), n, stg="tri", sym=True)
+        out["c%d_P" % i] = g["P"]
+        out["c%d_A" % i] = A
+        out["c%d_G" % i] = G
+        out["c%d_H" % i] = H
+    save("delaunay", ncases=2, **out)
+
+
+def gen_gconv():
+    g = torch.Generator().manual_seed(17)
+    torch.manual_seed(17)
+    gc = Gconv(6, 5)
+    A = (torch.rand(2, 8, 8, generator=g) > 0.6).float()
+    x = torch.randn(2, 8, 6, generator=g)
+    with torch.no_grad():
+        y = gc(A, x)
+    save("gconv", A=A.numpy(), x=x.numpy(), a_w=gc.a_fc.weight.detach().numpy(),
+         a_b=gc.a_fc.bias.detach().numpy(), u_w=gc.u_fc.weight.detach().numpy(),
+         u_b=gc.u_fc.bias.detach().numpy(), y=y.numpy())
+
+
+if __name__ == "__main__":
+    gen_soft_topk()
+    gen_hungarian_greedy()
+    gen_encoder()
+    gen_affinity()
+    gen_graphs_and_pattern()
+    gen_pyg_edges()
+    gen_gconv()

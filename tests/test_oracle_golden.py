@@ -1,0 +1,172 @@
+"""Pin the CPU oracle against golden vectors produced by the reference's own modules
+(tests/golden/make_golden.py).  CPU only."""
+import os
+
+import numpy as np
+import torch
+
+import fpm  # noqa: F401
+from fpm import params, synth
+import oracle as O
+
+from conftest import GOLDEN
+
+
+def _load(name):
+    return np.load(os.path.join(GOLDEN, name + ".npz"))
+
+
+def test_soft_topk_golden():
+    z = _load("soft_topk")
+    for i in range(int(z["ncases"])):
+        g = lambda k: torch.from_numpy(z["c%d_%s" % (i, k)])
+        ds = O.soft_topk(g("scores"), g("ks"), g("n1"), g("n2"), 10, 0.01)
+        np.testing.assert_allclose(ds.numpy(), z["c%d_ss_out" % i], atol=1e-6, rtol=0)
+
+
+def test_soft_topk_while_loop_exercised():
+    """At least one golden case must need the data-dependent extra step (soft_topk.py:232-241)."""
+    z = _load("soft_topk")
+    hit = 0
+    for i in range(int(z["ncases"])):
+        sc, ks = torch.from_numpy(z["c%d_scores" % i]), torch.from_numpy(z["c%d_ks" % i])
+        n1, n2 = z["c%d_n1" % i], z["c%d_n2" % i]
+        for b in range(sc.shape[0]):
+            blk = sc[b, :n1[b], :n2[b]]
+            an = torch.stack([blk.min(), blk.max()])
+            d = -torch.abs(blk.reshape(-1, 1) - an[None])
+            rp = torch.ones(1, d.shape[0])
+            cp = torch.tensor([[float(n1[b] * n2[b]) - float(ks[b]), float(ks[b])]])
+            L = d / 0.01
+            for it in range(10):
+                L = L - torch.logsumexp(L, 1 if it % 2 == 0 else 0, keepdim=True) + \
+                    (torch.log(rp).t() if it % 2 == 0 else torch.log(cp))
+            hit += int(bool((L > 0).any()))
+    assert hit > 0
+
+
+def test_hungarian_greedy_golden():
+    z = _load("hungarian_greedy")
+    s = torch.from_numpy(z["s"])
+    x = O.hungarian(s, z["n1"], z["n2"])
+    np.testing.assert_array_equal(x.numpy(), z["x"])
+    perm = O.greedy_perm(torch.zeros(s.shape), torch.from_numpy(z["top"]), torch.from_numpy(z["ks"]))
+    np.testing.assert_array_equal(perm.numpy(), z["perm"])
+
+
+def test_afau_encoder_golden():
+    z = _load("afau_encoder")
+    sd = params.init_params(int(z["seed"]))
+    with torch.no_grad():
+        r, c = O.afau_encoder(torch.from_numpy(z["row"]), torch.from_numpy(z["col"]),
+                              torch.from_numpy(z["cost"]), sd)
+        r2, c2 = O.afau_encoder(torch.from_numpy(z["row2"]), torch.from_numpy(z["col"]),
+                                torch.from_numpy(z["cost"]), sd)
+    for a, k in ((r, "r"), (c, "c"), (r2, "r2"), (c2, "c2")):
+        np.testing.assert_allclose(a.numpy(), z[k], atol=2e-5, rtol=0)
+
+
+def test_affinity_golden():
+    z = _load("affinity")
+    sd = params.init_params(int(z["seed"]))
+    for i in range(2):
+        K = O.affinity(torch.from_numpy(z["X%d" % i]), torch.from_numpy(z["Y%d" % i]),
+                       torch.from_numpy(z["W"][i]), sd["vertex_affinity.A.weight"],
+                       sd["vertex_affinity.A.bias"])
+        np.testing.assert_allclose(K.numpy(), z["K%d" % i], atol=1e-6, rtol=0)
+
+
+def test_kron_pattern_golden():
+    """Oracle pattern (row/col incl. diagonal, column-major edge-pair order) equals the
+    reference collate + construct_sparse_aff_mat indices; value order quirk A.10(i)."""
+    z = _load("graphs_pattern")
+    ei1 = torch.from_numpy(np.stack(np.nonzero(z["A1"]))).long()
+    ei2 = torch.from_numpy(np.stack(np.nonzero(z["A2"]))).long()
+    n1, n2 = z["A1"].shape[0], z["A2"].shape[0]
+    row, col = O.kron_pattern(ei1, ei2, int(z["n1max"]), n2, n1, n2)
+    np.testing.assert_array_equal(row.numpy(), z["row"].astype(np.int64))
+    np.testing.assert_array_equal(col.numpy(), z["col"].astype(np.int64))
+    # values: flatten(Ke) is row-major (e1 outer) while the indices are e2-outer (quirk A.10(i))
+    e1, e2 = ei1.shape[1], ei2.shape[1]
+    assert np.array_equal(z["val"][:e1 * e2], (np.arange(e1 * e2) + 1000).astype(np.float32))
+
+
+def test_pattern_mean_factorized_equals_explicit():
+    """SAGE-mean over the explicit Kronecker pattern == factorised (A1 X A2^T + X)/(d1 d2^T + 1),
+    incl. a ragged pair (diagonal in padded p-space, quirk A.10(ii))."""
+    torch.manual_seed(0)
+    for (na, nb, n1max, n2max) in ((9, 7, 9, 7), (6, 8, 9, 8), (10, 10, 10, 10)):
+        g1 = synth.make_graph(3, na, 0, na)
+        g2 = synth.make_graph(3, nb, 1, nb)
+        ei1, ei2 = torch.from_numpy(g1["edge_index"]), torch.from_numpy(g2["edge_index"])
+        N = n1max * n2max
+        x = torch.randn(N, 5, dtype=torch.float64)
+        row, col = O.kron_pattern(ei1, ei2, n1max, n2max, na, nb)
+        a = O.pattern_mean_explicit(x, row, col, N)
+        b = O.pattern_mean_factorized(x, ei1, ei2, n1max, n2max, na, nb)
+        np.testing.assert_allclose(a.numpy(), b.numpy(), atol=1e-12)
+
+
+def test_delaunay_edges_golden():
+    z = _load("delaunay")
+    for i in range(int(z["ncases"])):
+        P = z["c%d_P" % i].astype(np.float64)
+        A = synth.delaunay_adjacency(P)
+        np.testing.assert_array_equal(A, z["c%d_A" % i])
+        # G/H column order == np.nonzero(A) row-major edge list (build_graphs.py:62-72)
+        src, dst = np.nonzero(A)
+        G, H = z["c%d_G" % i], z["c%d_H" % i]
+        np.testing.assert_array_equal(np.argmax(G, 0), src)
+        np.testing.assert_array_equal(np.argmax(H, 0), dst)
+
+
+def test_gconv_golden():
+    z = _load("gconv")
+    t = lambda k: torch.from_numpy(z[k])
+    y = O.gconv(t("A"), t("x"), t("a_w"), t("a_b"), t("u_w"), t("u_b"))
+    np.testing.assert_allclose(y.numpy(), z["y"], atol=1e-6)
+
+
+def test_spline_basis_known_answer():
+    """Open B-spline degree 1, kernel 5 (torch-spline-conv 1.2.0): hand-derived values."""
+    ps = torch.tensor([[0.0, 0.0], [1.0, 1.0], [0.3, 0.6], [0.125, 0.9]])
+    basis, wi = O.spline_basis(ps)
+    # u=0.3 -> v=1.2 (f=1,t=.2); u=0.6 -> v=2.4 (f=2,t=.4)
+    np.testing.assert_allclose(basis[2].numpy(), [0.8 * 0.6, 0.2 * 0.6, 0.8 * 0.4, 0.2 * 0.4], atol=1e-6)
+    assert wi[2].tolist() == [1 + 5 * 2, 2 + 5 * 2, 1 + 5 * 3, 2 + 5 * 3]
+    assert wi[0].tolist() == [0, 1, 5, 6] and basis[0].tolist() == [1.0, 0.0, 0.0, 0.0]
+    # u=1 -> v=4 (f=4, t=0): indices wrap modulo 5
+    assert wi[1].tolist() == [24, 20, 4, 0] and basis[1].tolist() == [1.0, 0.0, 0.0, 0.0]
+
+
+def test_spline_conv_literal_loop():
+    """GEMM-form SplineConv == a literal per-edge loop of the documented weighting."""
+    torch.manual_seed(1)
+    n, d, E = 6, 5, 10
+    x = torch.randn(n, d, dtype=torch.float64)
+    ei = torch.randint(0, n, (2, E))
+    ei[1, :] = torch.tensor([0, 0, 1, 2, 2, 2, 3, 4, 4, 0])       # node 5 has no in-edge
+    ps = torch.rand(E, 2)
+    W = torch.randn(25, d, d, dtype=torch.float64)
+    R = torch.randn(d, d, dtype=torch.float64)
+    bias = torch.randn(d, dtype=torch.float64)
+    out = O.spline_conv(x, ei, ps, W, R, bias)
+    basis, wi = O.spline_basis(ps)
+    ref = torch.full((n, d), -float("inf"), dtype=torch.float64)
+    for e in range(E):
+        m = sum(float(basis[e, s]) * (x[ei[0, e]] @ W[wi[e, s]]) for s in range(4))
+        ref[ei[1, e]] = torch.maximum(ref[ei[1, e]], m)
+    ref[torch.isinf(ref)] = 0.0
+    ref = ref + x @ R + bias
+    np.testing.assert_allclose(out.numpy(), ref.numpy(), atol=1e-10)
+
+
+def test_oracle_forward_c1_smoke():
+    """Config 1: single pair, 32 keypoints, CPU forward end to end."""
+    sd = params.init_params(1)
+    pairs = synth.make_batch(1, 1, 32)
+    out = O.forward(pairs, sd)
+    ds = out["ds_mat"]
+    assert ds.shape == (1, 32, 32) and torch.isfinite(ds).all()
+    assert out["perm_mat"].sum() == round(float(out["k_prob"][0]) * 32)
+    assert 0 < float(out["cls_prob"][0]) < 1
