@@ -1,0 +1,170 @@
+"""Benchmark: graph-match pairs/sec of the matcher's forward (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 1024] [--n 256] [--dtype bf16]
+
+One step = one full ``Net.forward`` (eval, AFA-U regression, soft top-k, host Hungarian + greedy,
+match classifier) over a batch of ``--batch`` synthetic pairs of ``--n``-keypoint Delaunay graphs
+per GPU, inputs resident in HBM (graph generation is outside the timed region).  Multi-GPU:
+launched by torch.distributed.run, one process per GPU, pairs sharded (no data-path collective;
+gloo barrier + max-over-ranks timing only), ``value`` = pairs of all ranks / max rank time.
+Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+
+def _gen(args):
+    seed, p, n = args
+    from fpm import synth
+    return (synth.make_graph(seed, p, 0, n), synth.make_graph(seed, p, 1, n))
+
+
+def make_pairs(seed, first, B, n, workers):
+    ids = [(seed, first + b, n) for b in range(B)]
+    if workers <= 1 or B < 8:
+        return [_gen(a) for a in ids]
+    import multiprocessing as mp
+    with mp.get_context("fork").Pool(workers) as pool:
+        return pool.map(_gen, ids, chunksize=max(1, B // (workers * 4)))
+
+
+def cpu_baseline(n, npairs, seed, sd):
+    """The CPU oracle (PyTorch CPU restatement of the same forward) on a bounded sample."""
+    import torch
+    import oracle as O
+    cores = len(os.sched_getaffinity(0))
+    torch.set_num_threads(cores)
+    pairs = make_pairs(seed + 7919, 0, npairs, n, 1)
+    O.forward(pairs[:1], sd)                   # warm-up
+    t = time.perf_counter()
+    O.forward(pairs, sd)
+    dt = time.perf_counter() - t
+    return {"value": npairs / dt, "unit": "pairs/s", "cores": cores, "kind": "port",
+            "sample": "%d pairs, n=%d, fp32 oracle forward incl. scipy Hungarian (1 process)" % (npairs, n)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=1024, help="pairs per GPU")
+    ap.add_argument("--n", type=int, default=256, help="keypoints per graph")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu-pairs", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--lsa-threads", type=int, default=0)
+    ap.add_argument("--gen-workers", type=int, default=16)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print("note: WORLD_SIZE=%d, --gpus=%d" % (world, args.gpus), file=sys.stderr)
+
+    # inputs first (forked workers must not inherit a GPU context)
+    t_gen = time.perf_counter()
+    pairs = make_pairs(args.seed, rank * args.batch, args.batch, args.n, args.gen_workers)
+    t_gen = time.perf_counter() - t_gen
+
+    import torch
+    import torch.distributed as dist
+    import fpm
+    from fpm import _lib, params
+    from fpm.batch import DeviceBatch
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    sd = params.init_params(args.seed)
+    net = fpm.Net(regression=True, dtype=args.dtype, lsa_threads=args.lsa_threads or None)
+    net.load_state_dict(sd)
+    bt = DeviceBatch.from_pairs(pairs, dev)
+    E_tot = bt.E[0] + bt.E[1]
+    del pairs
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        net.run(bt)
+    torch.cuda.synchronize()
+    lib = _lib.load()
+    import ctypes
+    lib.fpm_profile_read(None, None, None)     # drop warm-up records
+    lib.fpm_profile_enable(1)
+    gpu_s = lsa_s = 0.0
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        net.run(bt)
+        gpu_s += net.last_timing["gpu_stage_s"]
+        lsa_s += net.last_timing["lsa_s"]
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    lib.fpm_profile_enable(0)
+    ms = ctypes.c_double()
+    fl = ctypes.c_double()
+    cnt = ctypes.c_int()
+    _lib.call("fpm_profile_read", ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(cnt))
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed, gpu_s, lsa_s], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, gpu_s, lsa_s = t.tolist()
+    pairs_total = args.batch * world * args.steps
+    value = pairs_total / elapsed
+    peak = 2500.0 if args.dtype == "bf16" else 157.3
+    achieved = (fl.value / (ms.value / 1e3)) / 1e12 if ms.value > 0 else 0.0
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args.n, args.cpu_pairs, args.seed, sd)
+        res = {
+            "metric": "graph-match pairs/sec @ n=256 kpts, batch=1024, 1 & 8 GPU",
+            "value": value,
+            "unit": "pairs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic (seeded Delaunay keypoint graphs, random node/global features, random-init weights)",
+            "config": {"workload": "batch=%d pairs/GPU, n=%d keypoints, Delaunay edges, factorized Kronecker "
+                                   "affinity, %s MFMA; full Net.forward incl. AFA-U, soft top-k, host Hungarian, "
+                                   "greedy top-k, MatchClassifier" % (args.batch, args.n, args.dtype),
+                       "global_batch": args.batch * world, "n_keypoints": args.n,
+                       "edges_per_graph": E_tot / (2.0 * args.batch), "parallelism": "pair-sharded x%d" % world},
+            "gpu_stage_pairs_per_s": args.batch * world * args.steps / gpu_s,
+            "host_lsa_ms_per_step": lsa_s / args.steps * 1e3,
+            "roofline": {"kernel": "spline edge-message GEMM (gemm_kernel<%s,SEGSCALE>)" % args.dtype,
+                         "bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                         "frac": achieved / peak, "traffic": None,
+                         "launches": cnt.value, "avg_launch_ms": ms.value / max(cnt.value, 1),
+                         "algorithmic_flops_per_launch": fl.value / max(cnt.value, 1)},
+            "cpu_baseline": cpu,
+            "input_gen_s": t_gen,
+        }
+        print(json.dumps(res))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

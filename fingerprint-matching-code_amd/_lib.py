@@ -1,0 +1,77 @@
+"""ctypes binding of ``libfpm_hip.so`` (C-ABI declared in ``include/fpm.h``).
+
+The library is loaded from this package directory (built in-tree by ``build.py``).  There is no
+fallback: if the library is missing every op raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfpm_hip.so")
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+L = ctypes.c_long
+F = ctypes.c_float
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "fpm_last_error": (ctypes.c_char_p, []),
+    "fpm_version": (I, []),
+    "fpm_device_sync": (I, []),
+    "fpm_sinkhorn_log_fwd": (I, [P, L, L, L, P, L, L, L, P, P, I, I, I, I, F, I, P]),
+    "fpm_soft_topk_fwd": (I, [P, L, L, P, P, P, I, I, I, I, F, P, L, L, P, P]),
+    "fpm_topk_select": (I, [P, L, L, P, L, P, I, I, I, P, L, L, P, L, L, P]),
+    "fpm_gemm": (I, [I, P, L, L, P, P, L, L, I, I, I, I, I, P, P, P, L, L, P, P, P]),
+    "fpm_cast_bf16": (I, [P, P, L, P]),
+    "fpm_spline_plan_bytes": (L, [L, L]),
+    "fpm_spline_plan": (I, [P, P, P, L, L, I, P, L, P]),
+    "fpm_spline_plan_csr": (I, [P, L, L, ctypes.POINTER(P), ctypes.POINTER(P)]),
+    "fpm_spline_conv_fwd": (I, [I, P, P, L, L, I, P, P, P, P, P, P, I, P, P, P, P, P]),
+    "fpm_edge_diff": (I, [P, P, P, L, I, P, P]),
+    "fpm_kron_gnn_layer_fwd": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, P, P]),
+    "fpm_gnn_param_count": (I, [I]),
+    "fpm_node_classifier": (I, [P, I, I, I, P, P, P, P]),
+    "fpm_crossset_attn_fwd": (I, [I, P, L, L, I, I, I, P, P, I, P, P, P, P, P, P]),
+    "fpm_instnorm": (I, [I, P, P, I, I, I, P, P, P, P, F, P, P, P, P]),
+    "fpm_afau_head": (I, [P, P, I, I, P, P, P, P, P, P, P, P, P, P]),
+    "fpm_match_cls_ws_floats": (L, [I, I, I]),
+    "fpm_match_cls_fwd": (I, [P, P, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),
+    "fpm_lsa_batch_host": (I, [P, L, L, P, P, I, I, P, I]),
+    "fpm_profile_enable": (I, [I]),
+    "fpm_profile_read": (I, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                             ctypes.POINTER(I)]),
+}
+
+_lib = None
+
+
+class FpmError(RuntimeError):
+    pass
+
+
+def load():
+    """Load the HIP library once; raise loudly if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FpmError("libfpm_hip.so not found at %s — build it with "
+                       "`python fingerprint-matching-code_amd/build.py` (no CPU fallback exists)" % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def call(name, *args):
+    """Invoke a status-returning C-ABI function; raise FpmError with fpm_last_error() on failure."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.fpm_last_error().decode(errors="replace")
+        raise FpmError("%s failed (status %d): %s" % (name, rc, msg))
+    return rc

@@ -1,0 +1,113 @@
+"""Device-side batch layout for the matcher's forward.
+
+Per side g (0 = source graphs ``idx1``, 1 = target graphs ``idx2``):
+  * x[g]      (B*nmax_g, 768) fp32   node features, graph b at rows [b*nmax_g, b*nmax_g + n_b),
+                                     zero rows in the padding (the reference concatenates unpadded
+                                     graphs in a PyG Batch, ngm.py:246-251; padding is inert here);
+  * src/dst[g] (E_g,) int32          edges with padded global node ids (PyG message flow src -> dst);
+  * pseudo[g] (E_g, 2) fp32          edge_attr pseudo-coordinates (GMDataset.to_pyg_graph);
+  * w[g]      (B, 512) fp32          global feature (ngm.py:238).
+n1/n2 are per-pair node counts (int32, device + host copies); n1max/n2max the batch maxima.
+"""
+import numpy as np
+import torch
+
+from . import config as C
+
+
+class DeviceBatch:
+    def __init__(self, B, n1, n2, x, w, src, dst, pseudo, device):
+        self.B = B
+        self.device = device
+        self.n_host = [torch.as_tensor(n1, dtype=torch.int32), torch.as_tensor(n2, dtype=torch.int32)]
+        self.n = [t.to(device) for t in self.n_host]
+        self.nmax = [int(self.n_host[0].max()), int(self.n_host[1].max())]
+        self.x, self.w, self.src, self.dst, self.pseudo = x, w, src, dst, pseudo
+        self.E = [int(s.numel()) for s in src]
+
+    @property
+    def n1(self):
+        return self.n[0]
+
+    @property
+    def n2(self):
+        return self.n[1]
+
+    @property
+    def n1max(self):
+        return self.nmax[0]
+
+    @property
+    def n2max(self):
+        return self.nmax[1]
+
+    @staticmethod
+    def from_pairs(pairs, device):
+        """From ``fpm.synth`` pairs (list of (g0, g1) dicts)."""
+        B = len(pairs)
+        xs, ws, srcs, dsts, pss = [], [], [], [], []
+        ns = []
+        for side in range(2):
+            n = np.array([p[side]["n"] for p in pairs], dtype=np.int32)
+            nmax = int(n.max())
+            X = np.zeros((B, nmax, C.NODE_FEATURE_DIM), np.float32)
+            s_l, d_l, p_l = [], [], []
+            for b, p in enumerate(pairs):
+                g = p[side]
+                X[b, :g["n"]] = g["x"]
+                ei = g["edge_index"]
+                s_l.append(ei[0] + b * nmax)
+                d_l.append(ei[1] + b * nmax)
+                p_l.append(g["pseudo"])
+            ns.append(n)
+            xs.append(torch.from_numpy(X.reshape(B * nmax, -1)).to(device))
+            ws.append(torch.from_numpy(np.stack([p[side]["w"] for p in pairs]).astype(np.float32)).to(device))
+            srcs.append(torch.from_numpy(np.concatenate(s_l).astype(np.int32)).to(device))
+            dsts.append(torch.from_numpy(np.concatenate(d_l).astype(np.int32)).to(device))
+            pss.append(torch.from_numpy(np.concatenate(p_l).astype(np.float32)).to(device).contiguous())
+        return DeviceBatch(B, ns[0], ns[1], xs, ws, srcs, dsts, pss, device)
+
+    @staticmethod
+    def from_data_dict(data_dict, device):
+        """From a reference-shaped data_dict with the synthetic bypass keys.
+
+        Reads ``ns`` (2 x (B,)), ``pyg_graphs`` (2 duck-typed PyG batches: edge_index (2, sumE) with
+        unpadded batch-global node ids, edge_attr (sumE, 2), and ``ptr`` or ``batch``),
+        ``node_features`` (2 x (B, nmax, 768) padded or (sum n, 768) concatenated) and
+        ``global_features`` (2 x (B, 512)).  Backbone features from ``images`` are out of scope.
+        """
+        if "node_features" not in data_dict:
+            raise NotImplementedError(
+                "fpm.Net starts after the ResNet-18 backbone + feature_align (out of scope, see DESIGN.md): "
+                "pass data_dict['node_features'] and data_dict['global_features']")
+        ns = [torch.as_tensor(t).view(-1).to(torch.int32).cpu() for t in data_dict["ns"]]
+        B = int(ns[0].numel())
+        xs, ws, srcs, dsts, pss = [], [], [], [], []
+        for side in range(2):
+            n = ns[side]
+            nmax = int(n.max())
+            g = data_dict["pyg_graphs"][side]
+            ptr = getattr(g, "ptr", None)
+            if ptr is None:
+                counts = torch.bincount(torch.as_tensor(g.batch).cpu(), minlength=B)
+                ptr = torch.cat([torch.zeros(1, dtype=torch.long), counts.cumsum(0)])
+            ptr = torch.as_tensor(ptr).cpu().long()
+            ei = torch.as_tensor(g.edge_index).cpu().long()
+            gidx = torch.searchsorted(ptr, ei[0], right=True) - 1
+            off = gidx * nmax - ptr[gidx]
+            srcs.append((ei[0] + off).to(torch.int32).to(device))
+            dsts.append((ei[1] + off).to(torch.int32).to(device))
+            pss.append(torch.as_tensor(g.edge_attr).to(torch.float32).to(device).contiguous())
+            nf = torch.as_tensor(data_dict["node_features"][side]).to(torch.float32)
+            if nf.dim() == 3:
+                X = torch.zeros(B, nmax, nf.shape[-1], dtype=torch.float32, device=nf.device)
+                X[:, :nf.shape[1]] = nf[:, :nmax]
+                for b in range(B):
+                    X[b, int(n[b]):] = 0
+            else:
+                X = torch.zeros(B, nmax, nf.shape[-1], dtype=torch.float32, device=nf.device)
+                for b in range(B):
+                    X[b, :int(n[b])] = nf[int(ptr[b]):int(ptr[b + 1])]
+            xs.append(X.reshape(B * nmax, -1).to(device).contiguous())
+            ws.append(torch.as_tensor(data_dict["global_features"][side]).to(torch.float32).to(device).contiguous())
+        return DeviceBatch(B, ns[0], ns[1], xs, ws, srcs, dsts, pss, device)

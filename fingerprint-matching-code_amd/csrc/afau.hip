@@ -1,0 +1,204 @@
+// AFA-U k regressor (reference ngm.py:386-412 over src/model/afau.py:54-300).
+//
+// With the reference's inputs R0 = 0 and C0 = one-hot (ngm.py:392-399):
+//   row block: q = Wq R0 = 0, so the mixed score depends on the cost only:
+//     score_h[i,j] = mix2_h . relu(mix1_h[1] * cost[i,j] + mix1_bias_h) + mix2_bias_h
+//     out[i, h*16+d] = sum_j softmax_j(score_h[i,:]) * Wv[h*16+d, j]   (v = Wv C0, zero for j >= n2b)
+//   col block: v = Wv R0 = 0, so the attention output is exactly 0 and o1 = IN(C0 + combine.bias).
+// Kernels: the row-block cross-set attention, instance norm (optionally + residual, optionally
+// fused with the max-pool over positions), and the 600->8->1 heads + sigmoid.
+// The projections/FFN are MFMA GEMMs through fpm_gemm.
+#include "fpm_common.h"
+
+namespace {
+
+// one workgroup per (pair, 16-row tile); 4 waves x 4 rows; heads looped
+template <typename T>
+__global__ __launch_bounds__(256) void afau_row_attn_kernel(const float* __restrict__ cost, long c_sb, long c_ld,
+                                                            int n1max, int n2max, const int* __restrict__ n2,
+                                                            const float* __restrict__ Wv, int emb,
+                                                            const float* __restrict__ mix1w,
+                                                            const float* __restrict__ mix1b,
+                                                            const float* __restrict__ mix2w,
+                                                            const float* __restrict__ mix2b, T* __restrict__ out) {
+    extern __shared__ float sh[];
+    float* V = sh;                        // [n2max][16]
+    float* Pm = sh + n2max * 16;          // [16 rows][n2max]
+    const int b = blockIdx.x, i0 = blockIdx.y * 16, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int n2b = n2[b];
+    const float* Cb = cost + (long)b * c_sb;
+    for (int h = 0; h < 16; ++h) {
+        __syncthreads();
+        for (int k = tid; k < n2max * 16; k += 256) {
+            int j = k >> 4, dd = k & 15;
+            V[k] = j < n2b ? Wv[(long)(h * 16 + dd) * emb + j] : 0.f;
+        }
+        float w1[16], b1[16], w2[16];
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            w1[m] = mix1w[(h * 2 + 1) * 16 + m];
+            b1[m] = mix1b[h * 16 + m];
+            w2[m] = mix2w[h * 16 + m];
+        }
+        const float b2 = mix2b[h];
+        for (int rr = 0; rr < 4; ++rr) {
+            const int lr = wv * 4 + rr, i = i0 + lr;
+            if (i >= n1max) break;
+            float mx = -INFINITY;
+            for (int j = lane; j < n2max; j += 64) {
+                float c = Cb[(long)i * c_ld + j];
+                float s = 0.f;
+#pragma unroll
+                for (int m = 0; m < 16; ++m) s += fmaxf(c * w1[m] + b1[m], 0.f) * w2[m];
+                s += b2;
+                Pm[lr * n2max + j] = s;
+                mx = fmaxf(mx, s);
+            }
+            mx = fpm::warp_max(mx);
+            float sum = 0.f;
+            for (int j = lane; j < n2max; j += 64) {
+                float e = expf(Pm[lr * n2max + j] - mx);
+                Pm[lr * n2max + j] = e;
+                sum += e;
+            }
+            sum = fpm::warp_sum(sum);
+            float inv = 1.f / sum;
+            for (int j = lane; j < n2max; j += 64) Pm[lr * n2max + j] *= inv;
+        }
+        __syncthreads();
+        // out[i][h*16 + d] for the 16 rows: thread = (row, d)
+        {
+            const int lr = tid >> 4, dd = tid & 15, i = i0 + lr;
+            if (i < n1max) {
+                float acc = 0.f;
+                for (int j = 0; j < n2max; ++j) acc += Pm[lr * n2max + j] * V[j * 16 + dd];
+                out[((long)b * n1max + i) * 256 + h * 16 + dd] = fpm::from_f<T>(acc);
+            }
+        }
+    }
+}
+
+// InstanceNorm1d over positions (afau.py:145-176) of x = in1 (+ in2), or of the synthesised col
+// input C0 + bias (onehot mode).  Writes out_f / out_t, or (gmax != null) only the max over
+// positions of the normalised values (MaxPool1d over the -inf padded 600 positions, ngm.py:402-405).
+template <typename T>
+__global__ __launch_bounds__(256) void instnorm_kernel(const float* __restrict__ in1, const float* __restrict__ in2,
+                                                       int P, int Cn, const int* __restrict__ nvalid,
+                                                       const float* __restrict__ onehot_bias, const float* __restrict__ w,
+                                                       const float* __restrict__ bb, float eps, float* __restrict__ out_f,
+                                                       T* __restrict__ out_t, float* __restrict__ gmax) {
+    __shared__ float ps[4][64], pq[4][64];
+    const int b = blockIdx.x, c = blockIdx.y * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
+    const bool cv = c < Cn;
+    const int nb = onehot_bias ? nvalid[b] : 0;
+    auto val = [&](int p) -> float {
+        if (onehot_bias) return ((p == c && p < nb) ? 1.f : 0.f) + onehot_bias[c];
+        long o = ((long)b * P + p) * Cn + c;
+        return in2 ? in1[o] + in2[o] : in1[o];
+    };
+    float s = 0.f;
+    if (cv)
+        for (int p = g; p < P; p += 4) s += val(p);
+    ps[g][threadIdx.x & 63] = s;
+    __syncthreads();
+    const float mean = (ps[0][threadIdx.x & 63] + ps[1][threadIdx.x & 63] + ps[2][threadIdx.x & 63] +
+                        ps[3][threadIdx.x & 63]) / (float)P;
+    float q = 0.f;
+    if (cv)
+        for (int p = g; p < P; p += 4) {
+            float d = val(p) - mean;
+            q += d * d;
+        }
+    pq[g][threadIdx.x & 63] = q;
+    __syncthreads();
+    const float var = (pq[0][threadIdx.x & 63] + pq[1][threadIdx.x & 63] + pq[2][threadIdx.x & 63] +
+                       pq[3][threadIdx.x & 63]) / (float)P;
+    const float rstd = 1.f / sqrtf(var + eps);
+    const float ww = cv ? w[c] : 0.f, bv = cv ? bb[c] : 0.f;
+    float mx = -INFINITY;
+    for (int p = g; cv && p < P; p += 4) {
+        float y = (val(p) - mean) * rstd * ww + bv;
+        if (gmax) mx = fmaxf(mx, y);
+        else {
+            long o = ((long)b * P + p) * Cn + c;
+            if (out_f) out_f[o] = y;
+            if (out_t) out_t[o] = fpm::from_f<T>(y);
+        }
+    }
+    if (gmax) {
+        __syncthreads();
+        ps[g][threadIdx.x & 63] = mx;
+        __syncthreads();
+        if (g == 0 && cv)
+            gmax[(long)b * Cn + c] = fmaxf(fmaxf(ps[0][threadIdx.x & 63], ps[1][threadIdx.x & 63]),
+                                           fmaxf(ps[2][threadIdx.x & 63], ps[3][threadIdx.x & 63]));
+    }
+}
+
+// ks = sigmoid((final_row(gr) + final_col(gc)) / 2)   (ngm.py:406-412, mean_k = True)
+__global__ __launch_bounds__(64) void afau_head_kernel(const float* __restrict__ gr, const float* __restrict__ gc,
+                                                       int E, const float* __restrict__ r0w, const float* __restrict__ r0b,
+                                                       const float* __restrict__ r2w, const float* __restrict__ r2b,
+                                                       const float* __restrict__ c0w, const float* __restrict__ c0b,
+                                                       const float* __restrict__ c2w, const float* __restrict__ c2b,
+                                                       float* __restrict__ ks) {
+    const int b = blockIdx.x, lane = threadIdx.x;
+    float kr = 0.f, kc = 0.f;
+    for (int m = 0; m < 8; ++m) {
+        float sr = 0.f, sc = 0.f;
+        for (int k = lane; k < E; k += 64) {
+            sr += r0w[m * E + k] * gr[(long)b * E + k];
+            sc += c0w[m * E + k] * gc[(long)b * E + k];
+        }
+        sr = fpm::warp_sum(sr) + r0b[m];
+        sc = fpm::warp_sum(sc) + c0b[m];
+        kr += r2w[m] * fmaxf(sr, 0.f);
+        kc += c2w[m] * fmaxf(sc, 0.f);
+    }
+    kr += r2b[0];
+    kc += c2b[0];
+    if (lane == 0) ks[b] = 1.f / (1.f + expf(-((kr + kc) / 2.f)));
+}
+
+}  // namespace
+
+extern "C" int fpm_crossset_attn_fwd(int dtype, const float* cost, long c_sb, long c_ld, int B, int n1max, int n2max,
+                                     const int* n2, const float* Wv, int emb, const float* mix1w, const float* mix1b,
+                                     const float* mix2w, const float* mix2b, void* out, void* stream) {
+    FPM_CHECK_ARG(n2max <= emb, "crossset_attn: n2max > embedding dim");
+    if (B == 0) return 0;
+    dim3 grid(B, (n1max + 15) / 16);
+    size_t sh = (size_t)(n2max * 16 + 16 * n2max) * 4;
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == 0)
+        hipLaunchKernelGGL((afau_row_attn_kernel<float>), grid, dim3(256), sh, st, cost, c_sb, c_ld, n1max, n2max, n2,
+                           Wv, emb, mix1w, mix1b, mix2w, mix2b, (float*)out);
+    else
+        hipLaunchKernelGGL((afau_row_attn_kernel<bf16_t>), grid, dim3(256), sh, st, cost, c_sb, c_ld, n1max, n2max,
+                           n2, Wv, emb, mix1w, mix1b, mix2w, mix2b, (bf16_t*)out);
+    return fpm::check_launch("fpm_crossset_attn_fwd");
+}
+
+extern "C" int fpm_instnorm(int dtype, const float* in1, const float* in2, int B, int P, int Cn, const int* nvalid,
+                            const float* onehot_bias, const float* w, const float* bias, float eps, float* out_f,
+                            void* out_t, float* gmax, void* stream) {
+    if (B == 0) return 0;
+    dim3 grid(B, (Cn + 63) / 64);
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == 0)
+        hipLaunchKernelGGL((instnorm_kernel<float>), grid, dim3(256), 0, st, in1, in2, P, Cn, nvalid, onehot_bias, w,
+                           bias, eps, out_f, (float*)out_t, gmax);
+    else
+        hipLaunchKernelGGL((instnorm_kernel<bf16_t>), grid, dim3(256), 0, st, in1, in2, P, Cn, nvalid, onehot_bias, w,
+                           bias, eps, out_f, (bf16_t*)out_t, gmax);
+    return fpm::check_launch("fpm_instnorm");
+}
+
+extern "C" int fpm_afau_head(const float* gr, const float* gc, int B, int E, const float* r0w, const float* r0b,
+                             const float* r2w, const float* r2b, const float* c0w, const float* c0b, const float* c2w,
+                             const float* c2b, float* ks, void* stream) {
+    if (B == 0) return 0;
+    hipLaunchKernelGGL(afau_head_kernel, dim3(B), dim3(64), 0, (hipStream_t)stream, gr, gc, E, r0w, r0b, r2w, r2b, c0w,
+                       c0b, c2w, c2b, ks);
+    return fpm::check_launch("fpm_afau_head");
+}

@@ -1,0 +1,60 @@
+// Common helpers for the MI355X (gfx950) fingerprint-matching kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+#include <math.h>
+
+#define FPM_WAVE 64
+
+typedef uint16_t bf16_t;  // raw bf16 bits (storage type for MFMA operands)
+
+namespace fpm {
+
+void set_error(const char* fmt, ...);
+int check_launch(const char* what);
+
+__device__ __forceinline__ float bf2f(bf16_t h) {
+    return __uint_as_float(((uint32_t)h) << 16);
+}
+
+// round-to-nearest-even f32 -> bf16 (inputs are finite here; NaN handling not required)
+__device__ __forceinline__ bf16_t f2bf(float f) {
+    uint32_t u = __float_as_uint(f);
+    u += 0x7FFFu + ((u >> 16) & 1u);
+    return (bf16_t)(u >> 16);
+}
+
+template <typename T> __device__ __forceinline__ float to_f(T v);
+template <> __device__ __forceinline__ float to_f<float>(float v) { return v; }
+template <> __device__ __forceinline__ float to_f<bf16_t>(bf16_t v) { return bf2f(v); }
+
+template <typename T> __device__ __forceinline__ T from_f(float v);
+template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
+template <> __device__ __forceinline__ bf16_t from_f<bf16_t>(float v) { return f2bf(v); }
+
+__device__ __forceinline__ float warp_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ float warp_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// torch.nn.functional.softplus(beta=1, threshold=20)
+__device__ __forceinline__ float softplus_f(float x) {
+    return x > 20.0f ? x : log1pf(expf(x));
+}
+
+}  // namespace fpm
+
+#define FPM_CHECK_ARG(cond, ...)                 \
+    do {                                         \
+        if (!(cond)) {                           \
+            fpm::set_error(__VA_ARGS__);         \
+            return 1;                            \
+        }                                        \
+    } while (0)

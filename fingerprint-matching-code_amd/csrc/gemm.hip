@@ -1,0 +1,45 @@
+// C-ABI entry for the generic (batched, optionally row-gathered) MFMA GEMM with fused epilogues.
+// Used by: SplineConv root term, global-weight coefficient (affinity_layer.py:13), vertex
+// affinity Kp (affinity_layer.py:15-18), AFA-U projections/FFN (afau.py:99-103,188-199).
+#include "gemm_core.h"
+
+extern "C" int fpm_gemm(int dtype, const void* A, long lda, long sA, const int* a_rows, const void* B, long ldb,
+                        long sB, int M, int N, int K, int batch, int epi, const float* bias, float* Cf, void* Ct,
+                        long ldc, long sC, const int* n1, const int* n2, void* stream) {
+    using namespace fpm;
+    FPM_CHECK_ARG(dtype == 0 || dtype == 1, "gemm: dtype must be 0 (f32) or 1 (bf16)");
+    FPM_CHECK_ARG(M >= 0 && N > 0 && K > 0 && batch >= 0, "gemm: bad sizes M=%d N=%d K=%d", M, N, K);
+    FPM_CHECK_ARG(K % (dtype ? 8 : 4) == 0, "gemm: K=%d must be a multiple of %d", K, dtype ? 8 : 4);
+    FPM_CHECK_ARG(lda % (dtype ? 8 : 4) == 0 && ldb % (dtype ? 8 : 4) == 0, "gemm: lda/ldb must keep rows 16-B aligned");
+    FPM_CHECK_ARG(epi != EPI_AFFINITY || (n1 && n2), "gemm: affinity epilogue needs n1/n2");
+    if (M == 0 || batch == 0) return 0;
+    GemmParams p = {};
+    p.A = A; p.lda = lda; p.sA = sA; p.a_rows = a_rows;
+    p.B = B; p.ldb = ldb; p.sB = sB; p.sB_seg = 0;
+    p.row_scale = nullptr;
+    p.M = M; p.N = N; p.K = K; p.nseg = 1;
+    p.tile_info = nullptr; p.group_off = nullptr;
+    p.epi = epi; p.bias = bias; p.Cf = Cf; p.Ct = Ct; p.ldc = ldc; p.sC = sC; p.n1 = n1; p.n2 = n2;
+    dim3 grid((N + GBN - 1) / GBN, (M + GBM - 1) / GBM, batch);
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == 0) hipLaunchKernelGGL((gemm_kernel<float, false>), grid, dim3(GTHREADS), 0, st, p);
+    else hipLaunchKernelGGL((gemm_kernel<bf16_t, false>), grid, dim3(GTHREADS), 0, st, p);
+    return check_launch("fpm_gemm");
+}
+
+// f32 -> bf16 conversion (operand copies for the bf16 MFMA path)
+namespace {
+__global__ void cast_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long n) {
+    long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    long stride = (long)gridDim.x * blockDim.x;
+    for (; i < n; i += stride) y[i] = fpm::f2bf(x[i]);
+}
+}  // namespace
+
+extern "C" int fpm_cast_bf16(const float* x, void* y, long n, void* stream) {
+    if (n <= 0) return 0;
+    long blocks = (n + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(cast_bf16_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, (bf16_t*)y, n);
+    return fpm::check_launch("fpm_cast_bf16");
+}

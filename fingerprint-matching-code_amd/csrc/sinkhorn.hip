@@ -1,0 +1,234 @@
+// Log-domain Sinkhorn (pygmtools 0.5.3 ``sinkhorn`` semantics, called at
+// reference src/model/sinkhorn.py:87 and src/model/gnn.py:221) — one workgroup per pair, the
+// whole n1max x n2max block resident in VGPRs (1024 threads x ER*EC values).
+//
+// Dual-potential form: L = S/tau - u_row - v_col.  A row step sets u = lse_cols(S/tau - v), a
+// column step v = lse_rows(S/tau - u); this is the reference's alternating
+// ``L -= logsumexp(L, dim)`` with the running sums kept as potentials, so S is read once and the
+// only per-iteration state is u, v.  Semantics kept: row step first, per-pair valid block
+// [:n1, :n2], n1 > n2 handled on the transpose, dummy rows (value -100 in log space) when
+// dummy_row and rows < cols, output exp(L) on the block and 0 in the padding.
+#include "fpm_common.h"
+
+namespace {
+
+struct SinkArgs {
+    const float* in;
+    long in_sb, in_si, in_sj;
+    float* out;
+    long out_sb, out_si, out_sj;
+    const int* n1;
+    const int* n2;
+    int n1max, n2max;
+    int iters;
+    float tau;
+    int dummy_row;
+    int contig_j;  // 1: j (column) is the unit-stride dimension of in/out
+};
+
+__device__ __forceinline__ void lse_combine(float& m, float& s, float mo, float so) {
+    float mn = fmaxf(m, mo);
+    if (mn == -INFINITY) { m = mn; s = 0.f; return; }
+    s = s * expf(m - mn) + so * expf(mo - mn);
+    m = mn;
+}
+
+// Reduce (max, then sum of exp) over the 32 lanes sharing tr (xor 1..16 stays inside a half-wave).
+__device__ __forceinline__ float lane32_max(float v) {
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ float lane32_sum(float v) {
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+template <int ER, int EC>
+__global__ __launch_bounds__(1024) void sinkhorn_reg_kernel(SinkArgs a) {
+    constexpr int NCOL = 32 * EC;
+    __shared__ float red_m[16][NCOL];
+    __shared__ float red_s[16][NCOL];
+    __shared__ float fin[NCOL];
+    __shared__ float blk_m[16], blk_s[16];
+
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int tr = tid >> 5, tc = tid & 31, wv = tid >> 6;
+    const int n1b = a.n1[b], n2b = a.n2[b];
+    const bool transposed = n1b > n2b;
+    const int R = transposed ? n2b : n1b;   // algorithmic rows
+    const int C = transposed ? n1b : n2b;   // algorithmic cols
+    const int nd = (a.dummy_row && C > R) ? (C - R) : 0;
+    const float lognd = nd > 0 ? logf((float)nd) : 0.f;
+    // physical dims: pc (lanes) = unit-stride dim
+    const int limPR = a.contig_j ? n1b : n2b;
+    const int limPC = a.contig_j ? n2b : n1b;
+    const int boxPR = a.contig_j ? a.n1max : a.n2max;
+    const int boxPC = a.contig_j ? a.n2max : a.n1max;
+    // u (row potential) lives on the pr side iff the algorithmic row dim is the pr dim
+    const bool u_on_R = (a.contig_j != 0) == (!transposed);
+
+    const float* in = a.in + (long)b * a.in_sb;
+    const long spr = a.contig_j ? a.in_si : a.in_sj;
+    const long spc = a.contig_j ? a.in_sj : a.in_si;
+
+    float M[ER][EC];
+    float pR[ER], pC[EC];
+#pragma unroll
+    for (int e = 0; e < ER; ++e) {
+        pR[e] = 0.f;
+        const int pr = tr + 32 * e;
+#pragma unroll
+        for (int f = 0; f < EC; ++f) {
+            const int pc = tc + 32 * f;
+            float v = -INFINITY;
+            if (pr < limPR && pc < limPC) v = in[pr * spr + pc * spc] / a.tau;
+            M[e][f] = v;
+        }
+    }
+#pragma unroll
+    for (int f = 0; f < EC; ++f) pC[f] = 0.f;
+
+    float ud = 0.f;  // potential of the (identical) dummy rows
+
+    // potR[e] = lse_f(M - pC) (+ dummy term)
+    auto update_R = [&](bool add_dummy) {
+#pragma unroll
+        for (int e = 0; e < ER; ++e) {
+            float m = -INFINITY;
+#pragma unroll
+            for (int f = 0; f < EC; ++f) m = fmaxf(m, M[e][f] - pC[f]);
+            m = lane32_max(m);
+            float dv = -100.f - ud;
+            if (add_dummy) m = fmaxf(m, dv);
+            float s = 0.f;
+            if (m != -INFINITY) {
+#pragma unroll
+                for (int f = 0; f < EC; ++f) s += expf(M[e][f] - pC[f] - m);
+            }
+            s = lane32_sum(s);
+            if (add_dummy && m != -INFINITY) s += (float)nd * expf(dv - m);
+            pR[e] = (m == -INFINITY) ? 0.f : m + logf(s);
+        }
+    };
+    // potC[f] = lse_e(M - pR) (+ dummy term): across the 32 thread-rows via LDS
+    auto update_C = [&](bool add_dummy) {
+#pragma unroll
+        for (int f = 0; f < EC; ++f) {
+            float m = -INFINITY;
+#pragma unroll
+            for (int e = 0; e < ER; ++e) m = fmaxf(m, M[e][f] - pR[e]);
+            float s = 0.f;
+            if (m != -INFINITY) {
+#pragma unroll
+                for (int e = 0; e < ER; ++e) s += expf(M[e][f] - pR[e] - m);
+            }
+            float mo = __shfl_xor(m, 32), so = __shfl_xor(s, 32);
+            lse_combine(m, s, mo, so);
+            if ((tid & 63) < 32) {
+                red_m[wv][tc + 32 * f] = m;
+                red_s[wv][tc + 32 * f] = s;
+            }
+        }
+        __syncthreads();
+        if (tid < NCOL) {
+            float m = red_m[0][tid], s = red_s[0][tid];
+            for (int w = 1; w < 16; ++w) lse_combine(m, s, red_m[w][tid], red_s[w][tid]);
+            if (add_dummy) lse_combine(m, s, -100.f - ud, (float)nd);
+            fin[tid] = (m == -INFINITY) ? 0.f : m + logf(s);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int f = 0; f < EC; ++f) pC[f] = fin[tc + 32 * f];
+    };
+    // ud = lse over valid algorithmic columns of (-100 - v)
+    auto update_dummy = [&]() {
+        float m = -INFINITY, s = 0.f;
+        if (u_on_R) {  // v on the pc side
+#pragma unroll
+            for (int f = 0; f < EC; ++f)
+                if (tc + 32 * f < limPC) m = fmaxf(m, -100.f - pC[f]);
+            m = lane32_max(m);
+#pragma unroll
+            for (int f = 0; f < EC; ++f)
+                if (tc + 32 * f < limPC) s += expf(-100.f - pC[f] - m);
+            s = lane32_sum(s);
+            ud = m + logf(s);
+        } else {       // v on the pr side: block reduction over threads with tc == 0
+            if (tc == 0) {
+#pragma unroll
+                for (int e = 0; e < ER; ++e)
+                    if (tr + 32 * e < limPR) m = fmaxf(m, -100.f - pR[e]);
+#pragma unroll
+                for (int e = 0; e < ER; ++e)
+                    if (tr + 32 * e < limPR) s += expf(-100.f - pR[e] - m);
+            }
+            float mo = __shfl_xor(m, 32), so = __shfl_xor(s, 32);
+            lse_combine(m, s, mo, so);
+            if ((tid & 63) == 0) { blk_m[wv] = m; blk_s[wv] = s; }
+            __syncthreads();
+            m = blk_m[0]; s = blk_s[0];
+            for (int w = 1; w < 16; ++w) lse_combine(m, s, blk_m[w], blk_s[w]);
+            ud = m + logf(s);
+            __syncthreads();
+        }
+    };
+
+    for (int it = 0; it < a.iters; ++it) {
+        if ((it & 1) == 0) {           // row normalisation: update u
+            if (u_on_R) update_R(false); else update_C(false);
+            if (nd > 0) update_dummy();
+        } else {                       // column normalisation: update v
+            if (u_on_R) update_C(nd > 0); else update_R(nd > 0);
+        }
+    }
+    (void)lognd;
+
+    float* out = a.out + (long)b * a.out_sb;
+    const long opr = a.contig_j ? a.out_si : a.out_sj;
+    const long opc = a.contig_j ? a.out_sj : a.out_si;
+#pragma unroll
+    for (int e = 0; e < ER; ++e) {
+        const int pr = tr + 32 * e;
+        if (pr >= boxPR) continue;
+#pragma unroll
+        for (int f = 0; f < EC; ++f) {
+            const int pc = tc + 32 * f;
+            if (pc >= boxPC) continue;
+            float v = 0.f;
+            if (pr < limPR && pc < limPC) v = expf(M[e][f] - pR[e] - pC[f]);
+            out[pr * opr + pc * opc] = v;
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" int fpm_sinkhorn_log_fwd(const float* s, long s_sb, long s_si, long s_sj, float* out,
+                                    long o_sb, long o_si, long o_sj, const int* n1, const int* n2,
+                                    int B, int n1max, int n2max, int iters, float tau, int dummy_row,
+                                    void* stream) {
+    FPM_CHECK_ARG(B >= 0 && n1max > 0 && n2max > 0, "sinkhorn: bad sizes");
+    FPM_CHECK_ARG(n1max <= 256 && n2max <= 256, "sinkhorn: n1max/n2max > 256 not supported yet (%d,%d)",
+                  n1max, n2max);
+    if (B == 0) return 0;
+    SinkArgs a;
+    a.in = s; a.in_sb = s_sb; a.in_si = s_si; a.in_sj = s_sj;
+    a.out = out; a.out_sb = o_sb; a.out_si = o_si; a.out_sj = o_sj;
+    a.n1 = n1; a.n2 = n2; a.n1max = n1max; a.n2max = n2max;
+    a.iters = iters; a.tau = tau; a.dummy_row = dummy_row;
+    a.contig_j = (s_sj == 1) ? 1 : 0;
+    int nmax = n1max > n2max ? n1max : n2max;
+    hipStream_t st = (hipStream_t)stream;
+    if (nmax <= 32)
+        hipLaunchKernelGGL((sinkhorn_reg_kernel<1, 1>), dim3(B), dim3(1024), 0, st, a);
+    else if (nmax <= 64)
+        hipLaunchKernelGGL((sinkhorn_reg_kernel<2, 2>), dim3(B), dim3(1024), 0, st, a);
+    else if (nmax <= 128)
+        hipLaunchKernelGGL((sinkhorn_reg_kernel<4, 4>), dim3(B), dim3(1024), 0, st, a);
+    else
+        hipLaunchKernelGGL((sinkhorn_reg_kernel<8, 8>), dim3(B), dim3(1024), 0, st, a);
+    return fpm::check_launch("fpm_sinkhorn_log_fwd");
+}

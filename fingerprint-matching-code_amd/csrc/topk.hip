@@ -1,0 +1,274 @@
+// Soft top-k (reference src/model/soft_topk.py:8-53 + Sinkhorn_m.forward_log :166-255) and the
+// greedy top-k selector over the Hungarian matches (ngm.py:444-449, soft_topk.py:56-77).
+//
+// soft top-k: one 1024-thread workgroup per pair; the valid block of ss (n1b*n2b <= 65536) is held
+// in VGPRs.  The 2-column Sinkhorn runs in dual form: L[q,c] = D[q,c] - u[q] - v[c] with
+// D[q,0] = -|ss_q - min|/tau, D[q,1] = -|ss_q - max|/tau.  u[q] = lse_c(D[q,c] - vu[c]) is a
+// function of the column potentials seen at the last row step (vu), so the state is four
+// scalars and one pass over q per column step is a whole iteration.  The reference's
+// data-dependent ``while any(L > 0)`` continuation is kept (bounded at 64 extra steps).
+#include "fpm_common.h"
+
+namespace {
+
+struct TopkState {
+    float vu0, vu1, v0, v1;
+};
+
+__device__ __forceinline__ float urow(float a0, float a1) {
+    float m = fmaxf(a0, a1);
+    if (m == -INFINITY) return INFINITY;
+    return m + logf(expf(a0 - m) + expf(a1 - m));
+}
+
+template <int NQ>
+__global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict__ ss, long sb, long ld,
+                                                         const int* __restrict__ n1, const int* __restrict__ n2,
+                                                         const float* __restrict__ kvec, float* __restrict__ out,
+                                                         long ob, long old_, int n1max, int n2max, int iters,
+                                                         float tau, int* __restrict__ steps_out) {
+    __shared__ float sa[16], sb_[16];
+    __shared__ int sflag[16];
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int n1b = n1[b], n2b = n2[b];
+    const int N = n1b * n2b;
+    const float* S = ss + (long)b * sb;
+
+    float s[NQ];
+    float mn = INFINITY, mx = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+        int q = tid + 1024 * k;
+        float v = 0.f;
+        if (q < N) {
+            int i = q / n2b, j = q - i * n2b;
+            v = S[i * ld + j];
+            mn = fminf(mn, v);
+            mx = fmaxf(mx, v);
+        }
+        s[k] = v;
+    }
+    mn = -fpm::warp_max(-mn);
+    mx = fpm::warp_max(mx);
+    if (lane == 0) { sa[wv] = mn; sb_[wv] = mx; }
+    __syncthreads();
+    mn = sa[0]; mx = sb_[0];
+    for (int w = 1; w < 16; ++w) { mn = fminf(mn, sa[w]); mx = fmaxf(mx, sb_[w]); }
+    __syncthreads();
+
+    // dist_mat = -|s - anchor| (soft_topk.py:28-29), then Sinkhorn_m divides by tau (:180)
+    float d0[NQ], d1[NQ];
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+        d0[k] = (-fabsf(s[k] - mn)) / tau;
+        d1[k] = (-fabsf(s[k] - mx)) / tau;
+    }
+    const float kk = kvec[b];
+    const float lcp0 = logf((float)N - kk);   // log(col_prob[:,0]) = log(n1*n2 - k)
+    const float lcp1 = logf(kk);              // log(col_prob[:,1]) = log(k)
+    TopkState st = {0.f, 0.f, 0.f, 0.f};
+
+    auto colstep = [&]() {
+        float m0 = -INFINITY, m1 = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) {
+            int q = tid + 1024 * k;
+            if (q < N) {
+                float u = urow(d0[k] - st.vu0, d1[k] - st.vu1);
+                m0 = fmaxf(m0, d0[k] - u - st.v0);
+                m1 = fmaxf(m1, d1[k] - u - st.v1);
+            }
+        }
+        m0 = fpm::warp_max(m0);
+        m1 = fpm::warp_max(m1);
+        if (lane == 0) { sa[wv] = m0; sb_[wv] = m1; }
+        __syncthreads();
+        m0 = sa[0]; m1 = sb_[0];
+        for (int w = 1; w < 16; ++w) { m0 = fmaxf(m0, sa[w]); m1 = fmaxf(m1, sb_[w]); }
+        __syncthreads();
+        float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) {
+            int q = tid + 1024 * k;
+            if (q < N) {
+                float u = urow(d0[k] - st.vu0, d1[k] - st.vu1);
+                if (m0 != -INFINITY) a0 += expf(d0[k] - u - st.v0 - m0);
+                if (m1 != -INFINITY) a1 += expf(d1[k] - u - st.v1 - m1);
+            }
+        }
+        a0 = fpm::warp_sum(a0);
+        a1 = fpm::warp_sum(a1);
+        if (lane == 0) { sa[wv] = a0; sb_[wv] = a1; }
+        __syncthreads();
+        a0 = 0.f; a1 = 0.f;
+        for (int w = 0; w < 16; ++w) { a0 += sa[w]; a1 += sb_[w]; }
+        __syncthreads();
+        // L_new = L - lse_q(L) + log cp  =>  v_new = v + lse_q(L) - log cp ; NaN -> -inf
+        if (m0 == -INFINITY) st.v0 = INFINITY;
+        else { float t = st.v0 + (m0 + logf(a0)) - lcp0; st.v0 = (t != t) ? INFINITY : t; }
+        if (m1 == -INFINITY) st.v1 = INFINITY;
+        else { float t = st.v1 + (m1 + logf(a1)) - lcp1; st.v1 = (t != t) ? INFINITY : t; }
+    };
+    auto any_pos = [&]() -> bool {
+        int flag = 0;
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) {
+            int q = tid + 1024 * k;
+            if (q < N) {
+                float u = urow(d0[k] - st.vu0, d1[k] - st.vu1);
+                flag |= ((d0[k] - u - st.v0) > 0.f) | ((d1[k] - u - st.v1) > 0.f);
+            }
+        }
+        int wf = __any(flag) ? 1 : 0;
+        if (lane == 0) sflag[wv] = wf;
+        __syncthreads();
+        int r = 0;
+        for (int w = 0; w < 16; ++w) r |= sflag[w];
+        __syncthreads();
+        return r != 0;
+    };
+
+    int step = 0;
+    for (; step < iters; ++step) {
+        if (step & 1) colstep();
+        else { st.vu0 = st.v0; st.vu1 = st.v1; }
+    }
+    for (int guard = 0; guard < 64 && any_pos(); ++guard, ++step) {
+        if (step & 1) colstep();
+        else { st.vu0 = st.v0; st.vu1 = st.v1; }
+    }
+    if (steps_out && tid == 0) steps_out[b] = step;
+
+    // ds_mat[i][j] = exp(L[q(i,j), 1]) on the valid block, 0 elsewhere
+    float* O = out + (long)b * ob;
+    for (int idx = tid; idx < n1max * n2max; idx += 1024) {
+        int i = idx / n2max, j = idx - i * n2max;
+        if (i >= n1b || j >= n2b) O[i * old_ + j] = 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+        int q = tid + 1024 * k;
+        if (q < N) {
+            int i = q / n2b, j = q - i * n2b;
+            float u = urow(d0[k] - st.vu0, d1[k] - st.vu1);
+            O[i * old_ + j] = expf(d1[k] - u - st.v1);
+        }
+    }
+}
+
+// Greedy top-k over Hungarian matches: prod = x * ds; argsort(prod, desc); accept (r,c) while
+// row r and column c are free until round(k) (half-to-even) are accepted.  Positive entries are
+// exactly the matched ones (pairwise row/col disjoint), taken in descending value; the
+// zero-valued tie region is scanned in ascending flat index (stable order, quirk A.10(v)).
+__global__ __launch_bounds__(256) void topk_select_kernel(const float* __restrict__ ds, long sb, long ld,
+                                                          const int* __restrict__ assign, long asb,
+                                                          const float* __restrict__ kvec, int n1max, int n2max,
+                                                          float* __restrict__ perm, long pb, long pld,
+                                                          float* __restrict__ lsa_out, long lb, long lld) {
+    __shared__ float val[512];
+    __shared__ int key[512];
+    __shared__ unsigned char rowt[1024], colt[1024];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const float* D = ds + (long)b * sb;
+    const int* A = assign + (long)b * asb;
+    float* P = perm + (long)b * pb;
+    for (int idx = tid; idx < n1max * n2max; idx += 256) {
+        int i = idx / n2max, j = idx - i * n2max;
+        P[i * pld + j] = 0.f;
+        if (lsa_out) lsa_out[(long)b * lb + i * lld + j] = 0.f;
+    }
+    for (int r = tid; r < 1024; r += 256) { rowt[r] = 0; colt[r] = 0; }
+    int n = 1;
+    while (n < n1max) n <<= 1;
+    for (int r = tid; r < n; r += 256) {
+        float v = -1.f;
+        int kq = 0x7fffffff;
+        if (r < n1max) {
+            int c = A[r];
+            if (c >= 0) {
+                v = D[r * ld + c];
+                kq = r * n2max + c;
+            }
+        }
+        val[r] = v;
+        key[r] = kq;
+    }
+    __syncthreads();
+    if (lsa_out) {
+        for (int r = tid; r < n1max; r += 256) {
+            int c = A[r];
+            if (c >= 0) lsa_out[(long)b * lb + r * lld + c] = 1.f;
+        }
+    }
+    // bitonic sort: descending value, ascending flat index on ties
+    for (int size = 2; size <= n; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int t = tid; t < n / 2; t += 256) {
+                int lo = 2 * t - (t & (stride - 1));
+                int hi = lo + stride;
+                bool up = ((lo & size) == 0);
+                float va = val[lo], vb = val[hi];
+                int ka = key[lo], kb = key[hi];
+                bool a_first = (va > vb) || (va == vb && ka < kb);
+                if (a_first != up) {
+                    val[lo] = vb; val[hi] = va;
+                    key[lo] = kb; key[hi] = ka;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if (tid == 0) {
+        const int K = (int)rintf(kvec[b]);
+        int matched = 0;
+        for (int t = 0; t < n && matched < K; ++t) {
+            if (!(val[t] > 0.f)) break;
+            int q = key[t];
+            int r = q / n2max, c = q - r * n2max;
+            if (!rowt[r] && !colt[c]) {
+                rowt[r] = 1; colt[c] = 1;
+                P[r * pld + c] = 1.f;
+                ++matched;
+            }
+        }
+        int cp = 0;
+        for (int r = 0; r < n1max && matched < K; ++r) {
+            if (rowt[r]) continue;
+            while (cp < n2max && colt[cp]) ++cp;
+            if (cp >= n2max) break;
+            rowt[r] = 1; colt[cp] = 1;
+            P[r * pld + cp] = 1.f;
+            ++matched;
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" int fpm_soft_topk_fwd(const float* ss, long s_sb, long s_ld, const int* n1, const int* n2,
+                                 const float* k, int B, int n1max, int n2max, int iters, float tau,
+                                 float* out, long o_sb, long o_ld, int* steps_out, void* stream) {
+    FPM_CHECK_ARG(B >= 0 && n1max > 0 && n2max > 0, "soft_topk: bad sizes");
+    long nn = (long)n1max * n2max;
+    FPM_CHECK_ARG(nn <= 65536, "soft_topk: n1max*n2max=%ld > 65536 not supported yet", nn);
+    if (B == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+#define LAUNCH(NQ) hipLaunchKernelGGL((soft_topk_kernel<NQ>), dim3(B), dim3(1024), 0, st, ss, s_sb, s_ld, n1, n2, \
+                                       k, out, o_sb, o_ld, n1max, n2max, iters, tau, steps_out)
+    if (nn <= 1024) LAUNCH(1);
+    else if (nn <= 4096) LAUNCH(4);
+    else if (nn <= 16384) LAUNCH(16);
+    else LAUNCH(64);
+#undef LAUNCH
+    return fpm::check_launch("fpm_soft_topk_fwd");
+}
+
+extern "C" int fpm_topk_select(const float* ds, long d_sb, long d_ld, const int* assign, long a_sb,
+                               const float* k, int B, int n1max, int n2max, float* perm, long p_sb, long p_ld,
+                               float* lsa_out, long l_sb, long l_ld, void* stream) {
+    FPM_CHECK_ARG(n1max <= 512 && n2max <= 1024, "topk_select: n1max<=512, n2max<=1024 required");
+    if (B == 0) return 0;
+    hipLaunchKernelGGL(topk_select_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, ds, d_sb, d_ld, assign, a_sb,
+                       k, n1max, n2max, perm, p_sb, p_ld, lsa_out, l_sb, l_ld);
+    return fpm::check_launch("fpm_topk_select");
+}

@@ -1,0 +1,303 @@
+"""``Net``: the fingerprint QAP matcher's graph-matching forward on MI355X.
+
+Drop-in for the reference's ``Net`` (``src/model/ngm.py:117-491``): same constructor
+(``Net(regression=False)``), same ``forward(data_dict, regression=True) -> data_dict`` writing
+``ds_mat``, ``perm_mat``, ``ks_loss``, ``ks_error``, ``cls_loss``, ``cls_prob``, ``k_prob``
+(ngm.py:479-487), and the same state_dict names/shapes (so ``utils/models_sl.load_model`` works).
+The forward starts from per-graph node features (``data_dict['node_features']`` /
+``['global_features']``, or a prebuilt ``data_dict['fpm_batch']``); the ResNet-18 backbone and
+``feature_align`` are out of scope.  Every compute stage runs in ``libfpm_hip.so``; the
+Hungarian step runs on host threads (``fpm_lsa_batch_host``) as the reference's does.
+
+``dtype``: ``"f32"`` (parity mode: fp32 MFMA, matches the CPU oracle) or ``"bf16"`` (bf16 MFMA
+operands with fp32 accumulation for the GEMMs; everything else fp32).
+"""
+import os
+import time
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import config as C
+from . import ops
+from . import params as P
+from .batch import DeviceBatch
+
+
+class _Node(nn.Module):
+    pass
+
+
+def _build_tree(root, sd):
+    """Register every state_dict entry under its dotted name (float tensors as Parameters)."""
+    for name, t in sd.items():
+        parts = name.split(".")
+        m = root
+        for p in parts[:-1]:
+            if not hasattr(m, p) or not isinstance(getattr(m, p), nn.Module):
+                m.add_module(p, _Node())
+            m = getattr(m, p)
+        leaf = parts[-1]
+        is_buf = (not t.is_floating_point()) or leaf in ("running_mean", "running_var")
+        if is_buf:
+            m.register_buffer(leaf, t.clone())
+        else:
+            m.register_parameter(leaf, nn.Parameter(t.clone(), requires_grad=False))
+
+
+class Net(nn.Module):
+    def __init__(self, regression=False, dtype="f32", seed=0, lsa_threads=None):
+        super().__init__()
+        _build_tree(self, P.init_params(seed))
+        self.regression = regression
+        self.mean_k = True
+        self.tau = C.SK_TAU
+        self.univ_size = C.UNIV_SIZE
+        self.k_factor = C.K_FACTOR
+        if dtype not in ("f32", "bf16"):
+            raise ValueError("dtype must be 'f32' or 'bf16'")
+        self.dtype_mode = dtype
+        self.lsa_threads = lsa_threads or max(1, min(16, len(os.sched_getaffinity(0))))
+        self._pack = None
+        self._pack_key = None
+        self._pinned = None
+        self._keep_feats = False
+        self.last_timing = {}
+        self.eval()
+
+    # ------------------------------------------------------------------------------------------
+    def _sd(self):
+        return dict(self.state_dict())
+
+    def _key(self, device):
+        return (str(device), self.dtype_mode, tuple(p._version for p in self.parameters()),
+                tuple(b._version for b in self.buffers()))
+
+    def packed(self, device):
+        """Device-resident, kernel-layout copies of the parameters (rebuilt if they change)."""
+        key = self._key(device)
+        if self._pack is not None and self._pack_key == key:
+            return self._pack
+        sd = {k: v.detach() for k, v in self.state_dict().items()}
+        op = torch.bfloat16 if self.dtype_mode == "bf16" else torch.float32
+        d = {}
+        g = lambda k: sd[k].to(device=device, dtype=torch.float32).contiguous()
+        for l in range(2):
+            pre = "%s.%d" % (P.SPLINE_PREFIX, l)
+            d["W%d" % l] = sd[pre + ".weight"].to(device).transpose(1, 2).contiguous().to(op)   # [cell][out][in]
+            d["R%d" % l] = sd[pre + ".root"].to(device).t().contiguous().to(op)                # [out][in]
+            d["bias%d" % l] = g(pre + ".bias")
+        d["aff_w"] = g("vertex_affinity.A.weight")          # [768][1024] = N x K
+        d["aff_b"] = g("vertex_affinity.A.bias")
+        for l in range(C.GNN_LAYER):
+            pre = "gnn_layer_%d" % l
+            parts = [sd[pre + ".conv2.lin_l.weight"], sd[pre + ".conv2.lin_l.bias"], sd[pre + ".conv2.lin_r.weight"],
+                     sd[pre + ".n_self_func.0.weight"], sd[pre + ".n_self_func.0.bias"],
+                     sd[pre + ".n_self_func.2.weight"], sd[pre + ".n_self_func.2.bias"],
+                     sd[pre + ".classifier.weight"], sd[pre + ".classifier.bias"]]
+            d["gnn%d" % l] = torch.cat([t.reshape(-1).float() for t in parts]).to(device).contiguous()
+        d["cls_w"] = g("classifier.weight").reshape(-1).contiguous()
+        d["cls_b"] = g("classifier.bias")
+        for blk in ("row", "col"):
+            pre = "encoder_k.layers.0.%s_encoding_block" % blk
+            d[blk + "_Wv"] = g(pre + ".Wv.weight")                                  # (256, 600)
+            d[blk + "_mix1w"] = g(pre + ".mixed_score_MHA.mix1_weight")
+            d[blk + "_mix1b"] = g(pre + ".mixed_score_MHA.mix1_bias")
+            d[blk + "_mix2w"] = g(pre + ".mixed_score_MHA.mix2_weight")
+            d[blk + "_mix2b"] = g(pre + ".mixed_score_MHA.mix2_bias")
+            d[blk + "_Wc"] = sd[pre + ".multi_head_combine.weight"].to(device).contiguous().to(op)   # (600, 256)
+            d[blk + "_bc"] = g(pre + ".multi_head_combine.bias")
+            d[blk + "_W1"] = sd[pre + ".feed_forward.W1.weight"].to(device).contiguous().to(op)      # (256, 600)
+            d[blk + "_b1"] = g(pre + ".feed_forward.W1.bias")
+            d[blk + "_W2"] = sd[pre + ".feed_forward.W2.weight"].to(device).contiguous().to(op)      # (600, 256)
+            d[blk + "_b2"] = g(pre + ".feed_forward.W2.bias")
+            for k in (1, 2):
+                d["%s_n%dw" % (blk, k)] = g(pre + ".add_n_normalization_%d.norm.weight" % k)
+                d["%s_n%db" % (blk, k)] = g(pre + ".add_n_normalization_%d.norm.bias" % k)
+        for h in ("final_row", "final_col"):
+            for i in (0, 2):
+                d["%s%dw" % (h, i)] = g("%s.%d.weight" % (h, i)).reshape(-1).contiguous()
+                d["%s%db" % (h, i)] = g("%s.%d.bias" % (h, i))
+        for ci, bi, tag in ((0, 2, "1"), (4, 6, "2")):
+            d["mc_w" + tag] = g("match_cls.conv.%d.weight" % ci).reshape(-1).contiguous()
+            d["mc_b" + tag] = g("match_cls.conv.%d.bias" % ci)
+            rm, rv = sd["match_cls.conv.%d.running_mean" % bi].double(), sd["match_cls.conv.%d.running_var" % bi].double()
+            gw, gb = sd["match_cls.conv.%d.weight" % bi].double(), sd["match_cls.conv.%d.bias" % bi].double()
+            sc = gw / torch.sqrt(rv + C.BN_EPS)
+            d["mc_sc" + tag] = sc.float().to(device)
+            d["mc_sh" + tag] = (gb - rm * sc).float().to(device)
+        d["mc_fcw"] = g("match_cls.fc.weight").reshape(-1).contiguous()
+        d["mc_fcb"] = g("match_cls.fc.bias")
+        self._pack, self._pack_key = d, key
+        return d
+
+    # ------------------------------------------------------------------------------------------
+    def _spline_side(self, wp, bt, side, cscale):
+        """SiameseSConvOnNodes over one side's batch (spline_conv.py:28-57) -> operand rows."""
+        dev = bt.device
+        op = torch.bfloat16 if self.dtype_mode == "bf16" else torch.float32
+        nn_ = bt.B * bt.nmax[side]
+        E = bt.E[side]
+        plan = ops.spline_plan(bt.src[side], bt.dst[side], bt.pseudo[side], nn_, bt.nmax[side])
+        x0 = bt.x[side]
+        x_op = ops.cast_bf16(x0) if op == torch.bfloat16 else x0
+        msg = torch.empty(max(E, 1), C.NODE_FEATURE_DIM, device=dev, dtype=op)
+        root = torch.empty(nn_, C.NODE_FEATURE_DIM, device=dev, dtype=torch.float32)
+        h = torch.empty(nn_, C.NODE_FEATURE_DIM, device=dev, dtype=op)
+        ops.spline_conv(x_op, plan, E, nn_, bt.nmax[side], bt.n[side], wp["W0"], wp["R0"], wp["bias0"], msg, root,
+                        0, out_t=h)
+        out = torch.empty(nn_, C.NODE_FEATURE_DIM, device=dev, dtype=op)
+        outf = torch.empty(nn_, C.NODE_FEATURE_DIM, device=dev, dtype=torch.float32) if self._keep_feats else None
+        ops.spline_conv(h, plan, E, nn_, bt.nmax[side], bt.n[side], wp["W1"], wp["R1"], wp["bias1"], msg, root,
+                        1, xres=x0, cscale=cscale, out_f=outf, out_t=out)
+        return plan, out, outf
+
+    def _afau(self, wp, ss, bt):
+        """AFA-U k regression (ngm.py:386-412) -> ks (B,)."""
+        dev = ss.device
+        B, n1max, n2max = bt.B, bt.n1max, bt.n2max
+        op = torch.bfloat16 if self.dtype_mode == "bf16" else torch.float32
+        E, HD, FF = C.AFAU_EMB, C.AFAU_HEADS * C.AFAU_QKV, C.AFAU_FF
+        if max(n1max, n2max) > self.univ_size:
+            raise AssertionError("UNIV_SIZE cap: n1max/n2max must be <= %d (ngm.py:387-389)" % self.univ_size)
+        att = torch.empty(B * n1max, HD, device=dev, dtype=op)
+        ops.crossset_attn(ss, bt.n2, wp["row_Wv"], wp["row_mix1w"], wp["row_mix1b"], wp["row_mix2w"],
+                          wp["row_mix2b"], att)
+        mh = torch.empty(B * n1max, E, device=dev, dtype=torch.float32)
+        ops.gemm(att, wp["row_Wc"], B * n1max, E, HD, HD, HD, bias=wp["row_bc"], out_f=mh, ldc=E)
+        gmax = {}
+        for blk, rows, P_ in (("row", B * n1max, n1max), ("col", B * n2max, n2max)):
+            o1f = torch.empty(rows, E, device=dev, dtype=torch.float32)
+            o1t = o1f if op == torch.float32 else torch.empty(rows, E, device=dev, dtype=op)
+            if blk == "row":
+                ops.instnorm(mh, B, P_, E, wp["row_n1w"], wp["row_n1b"], out_f=o1f,
+                             out_t=None if op == torch.float32 else o1t)
+            else:
+                ops.instnorm(None, B, P_, E, wp["col_n1w"], wp["col_n1b"], nvalid=bt.n2, onehot_bias=wp["col_bc"],
+                             out_f=o1f, out_t=None if op == torch.float32 else o1t)
+            hbuf = torch.empty(rows, FF, device=dev, dtype=op)
+            ops.gemm(o1t, wp[blk + "_W1"], rows, FF, E, E, E, epi=ops.EPI_RELU, bias=wp[blk + "_b1"],
+                     out_t=hbuf if op != torch.float32 else None, out_f=hbuf if op == torch.float32 else None,
+                     ldc=FF)
+            ff = torch.empty(rows, E, device=dev, dtype=torch.float32)
+            ops.gemm(hbuf, wp[blk + "_W2"], rows, E, FF, FF, FF, bias=wp[blk + "_b2"], out_f=ff, ldc=E)
+            gm = torch.empty(B, E, device=dev, dtype=torch.float32)
+            ops.instnorm(o1f, B, P_, E, wp[blk + "_n2w"], wp[blk + "_n2b"], in2=ff, gmax=gm)
+            gmax[blk] = gm
+        ks = torch.empty(B, device=dev, dtype=torch.float32)
+        ops.afau_head(gmax["row"], gmax["col"], B, E, wp["final_row0w"], wp["final_row0b"], wp["final_row2w"],
+                      wp["final_row2b"], wp["final_col0w"], wp["final_col0b"], wp["final_col2w"], wp["final_col2b"], ks)
+        return ks
+
+    def run_gpu_stage(self, bt, keep_feats=False):
+        """Everything up to ds_mat on the GPU.  Returns a dict of device tensors."""
+        self._keep_feats = keep_feats
+        wp = self.packed(bt.device)
+        dev = bt.device
+        B, n1max, n2max = bt.B, bt.n1max, bt.n2max
+        N = n1max * n2max
+        # global weights + vertex-affinity coefficients c_b = tanh(A w_b + a)  (ngm.py:262-268, affinity_layer.py:13)
+        gw = torch.cat([bt.w[0], bt.w[1]], dim=1)
+        gw = (gw / torch.norm(gw, dim=1, keepdim=True)).contiguous()
+        coef = torch.empty(B, C.NODE_FEATURE_DIM, device=dev, dtype=torch.float32)
+        ops.gemm(gw, wp["aff_w"], B, C.NODE_FEATURE_DIM, C.GLOBAL_STATE_DIM, C.GLOBAL_STATE_DIM, C.GLOBAL_STATE_DIM,
+                 epi=ops.EPI_TANH, bias=wp["aff_b"], out_f=coef)
+        plan0, x1c, f1 = self._spline_side(wp, bt, 0, coef)
+        plan1, x2, f2 = self._spline_side(wp, bt, 1, None)
+        # Kp^T per pair: emb0[b][j][i] = softplus((x1_i o c) . x2_j) - 0.5 on the valid block (ngm.py:277-321)
+        X = torch.empty(B, 1, n2max, n1max, device=dev, dtype=torch.float32)
+        ops.gemm(x2, x1c, n2max, n1max, C.NODE_FEATURE_DIM, C.NODE_FEATURE_DIM, C.NODE_FEATURE_DIM, batch=B,
+                 sA=n2max * C.NODE_FEATURE_DIM, sB=n1max * C.NODE_FEATURE_DIM, epi=ops.EPI_AFFINITY, out_f=X,
+                 ldc=n1max, sC=N, n1=bt.n1, n2=bt.n2)
+        Kp = X
+        csr1 = ops.plan_csr(plan0, bt.E[0], B * n1max)
+        csr2 = ops.plan_csr(plan1, bt.E[1], B * n2max)
+        zbuf = torch.empty(B, n2max, n1max, device=dev, dtype=torch.float32)
+        Cin = 1
+        for l in range(C.GNN_LAYER):
+            Xn = torch.empty(B, 17, n2max, n1max, device=dev, dtype=torch.float32)
+            ops.gnn_layer(X, Cin, B, n1max, n2max, csr1, csr2, bt.n1, bt.n2, wp["gnn%d" % l], Xn, zbuf)
+            # Sinkhorn(20, tau) on Z[i][j] = z[j*n1max + i], written into channel 16 (gnn.py:217-222)
+            ops.sinkhorn(zbuf.transpose(1, 2), bt.n1, bt.n2, C.GNN_SK_ITER, self.tau, True,
+                         out=Xn[:, 16].transpose(1, 2))
+            X, Cin = Xn, 17
+        s = torch.empty(B, n1max, n2max, device=dev, dtype=torch.float32)
+        ops.node_classifier(X, B, n1max, n2max, wp["cls_w"], wp["cls_b"], s)
+        ss = ops.sinkhorn(s, bt.n1, bt.n2, C.SK_ITER_NUM, self.tau, True)
+        out = dict(s=s, ss=ss, Kp=Kp[:, 0].transpose(1, 2), coef=coef)
+        if keep_feats:
+            out["feat0"], out["feat1"] = f1, f2
+        return out
+
+    # ------------------------------------------------------------------------------------------
+    def run(self, bt, gt_perm=None, label=None, keep_feats=False):
+        dev = bt.device
+        B, n1max, n2max = bt.B, bt.n1max, bt.n2max
+        t0 = time.perf_counter()
+        out = self.run_gpu_stage(bt, keep_feats)
+        s, ss = out["s"], out["ss"]
+        min_pt = torch.minimum(bt.n1, bt.n2).to(torch.float32)
+        if gt_perm is None:
+            gt_ks = min_pt.clone()     # synthetic pairs: identity ground truth
+        else:
+            gt_ks = torch.as_tensor(gt_perm).to(dev).reshape(B, -1).sum(-1).to(torch.float32)
+        if self.regression:
+            ks = self._afau(self.packed(dev), ss, bt)
+        else:
+            ks = gt_ks / min_pt
+        k_used = gt_ks if self.training else ks * min_pt
+        steps = torch.empty(B, device=dev, dtype=torch.int32)
+        ds = ops.soft_topk(ss, bt.n1, bt.n2, k_used.contiguous(), C.SK_ITER_NUM, self.tau, steps=steps)
+        # Hungarian on host threads (utils/hungarian.py): D2H ds_mat, LSA, H2D assignment
+        if self._pinned is None or self._pinned.shape != ds.shape:
+            self._pinned = torch.empty(ds.shape, dtype=torch.float32, pin_memory=True)
+        ds_host = self._pinned
+        ds_host.copy_(ds, non_blocking=True)
+        torch.cuda.current_stream(dev).synchronize()
+        t1 = time.perf_counter()
+        assign = ops.lsa_batch_host(ds_host, bt.n_host[0], bt.n_host[1], self.lsa_threads)
+        t2 = time.perf_counter()
+        assign_d = assign.to(dev, non_blocking=True)
+        lsa = torch.empty(B, n1max, n2max, device=dev, dtype=torch.float32)
+        kk = (ks * min_pt).contiguous()
+        perm = ops.topk_select(ds, assign_d, kk, lsa_out=lsa)
+        logits, prob = ops.match_cls(s, perm, self._pack["mc_w1"], self._pack["mc_b1"], self._pack["mc_sc1"],
+                                     self._pack["mc_sh1"], self._pack["mc_w2"], self._pack["mc_b2"],
+                                     self._pack["mc_sc2"], self._pack["mc_sh2"], self._pack["mc_fcw"],
+                                     self._pack["mc_fcb"])
+        res = dict(out)
+        res.update(ds_mat=ds, perm_mat=perm, k_prob=ks, cls_prob=prob, cls_logits=logits, lsa=lsa,
+                   sk_steps=steps)
+        if label is not None:
+            res["cls_loss"] = F.binary_cross_entropy_with_logits(logits, torch.as_tensor(label).to(dev).view(-1).float())
+        else:
+            res["cls_loss"] = torch.tensor(0.0, device=dev)
+        if self.regression:
+            sup = gt_ks / min_pt
+            res["ks_loss"] = F.mse_loss(ks, sup) * self.k_factor
+            res["ks_error"] = F.l1_loss(ks * min_pt, gt_ks)
+        else:
+            res["ks_loss"] = 0.0
+            res["ks_error"] = 0.0
+        self.last_timing = dict(gpu_stage_s=t1 - t0, lsa_s=t2 - t1)
+        return res
+
+    def forward(self, data_dict, regression=True):
+        """Reference signature (ngm.py:205).  ``regression`` is accepted and ignored there too."""
+        dev = torch.device("cuda", torch.cuda.current_device())
+        bt = data_dict.get("fpm_batch")
+        if bt is None:
+            bt = DeviceBatch.from_data_dict(data_dict, dev)
+        gt = data_dict.get("gt_perm_mat")
+        res = self.run(bt, gt_perm=gt, label=data_dict.get("label"))
+        data_dict.update({
+            "ds_mat": res["ds_mat"],
+            "perm_mat": res["perm_mat"],
+            "ks_loss": res["ks_loss"],
+            "ks_error": res["ks_error"],
+            "cls_loss": res["cls_loss"],
+            "cls_prob": res["cls_prob"],
+            "k_prob": res["k_prob"],
+        })
+        return data_dict

@@ -1,0 +1,188 @@
+"""Thin torch-tensor wrappers over the C-ABI (``include/fpm.h``).
+
+Every op takes device tensors, checks shapes/dtypes on the host, and launches on the current
+torch stream.  Outputs are caller-allocated (``torch.empty`` on the tensor's device).  There is
+no CPU fallback: a CPU tensor or a missing library raises.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+
+F32, BF16 = 0, 1
+EPI_STORE, EPI_RELU, EPI_TANH, EPI_AFFINITY = 0, 1, 2, 3
+
+
+def _p(t):
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def _stream(t=None):
+    dev = t.device if t is not None else torch.device("cuda")
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _dev(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise _lib.FpmError("fpm op called with a CPU tensor: the HIP path has no CPU fallback")
+
+
+def _code(t):
+    if t.dtype == torch.float32:
+        return F32
+    if t.dtype == torch.bfloat16:
+        return BF16
+    raise _lib.FpmError("unsupported operand dtype %s" % t.dtype)
+
+
+def sinkhorn(s, n1, n2, iters, tau, dummy_row=True, out=None, n1max=None, n2max=None):
+    """pygm-style log Sinkhorn on the (n1max, n2max) box of each pair.  ``s`` may be any strided
+    3-D view (B, n1max, n2max); ``out`` likewise (allocated contiguous if None)."""
+    _dev(s, n1, n2)
+    B = s.shape[0]
+    n1max = n1max or s.shape[1]
+    n2max = n2max or s.shape[2]
+    if out is None:
+        out = torch.empty(B, n1max, n2max, device=s.device, dtype=torch.float32)
+    _lib.call("fpm_sinkhorn_log_fwd", _p(s), s.stride(0), s.stride(1), s.stride(2), _p(out), out.stride(0),
+              out.stride(1), out.stride(2), _p(n1), _p(n2), B, n1max, n2max, int(iters), float(tau),
+              int(bool(dummy_row)), _stream(s))
+    return out
+
+
+def soft_topk(ss, n1, n2, k, iters=10, tau=0.01, out=None, steps=None):
+    _dev(ss, n1, n2, k)
+    B, n1max, n2max = ss.shape
+    if out is None:
+        out = torch.empty(B, n1max, n2max, device=ss.device, dtype=torch.float32)
+    _lib.call("fpm_soft_topk_fwd", _p(ss), ss.stride(0), ss.stride(1), _p(n1), _p(n2), _p(k), B, n1max, n2max,
+              int(iters), float(tau), _p(out), out.stride(0), out.stride(1), _p(steps), _stream(ss))
+    return out
+
+
+def topk_select(ds, assign, k, lsa_out=None):
+    _dev(ds, assign, k)
+    B, n1max, n2max = ds.shape
+    perm = torch.empty(B, n1max, n2max, device=ds.device, dtype=torch.float32)
+    _lib.call("fpm_topk_select", _p(ds), ds.stride(0), ds.stride(1), _p(assign), assign.stride(0), _p(k), B,
+              n1max, n2max, _p(perm), perm.stride(0), perm.stride(1), _p(lsa_out),
+              lsa_out.stride(0) if lsa_out is not None else 0, lsa_out.stride(1) if lsa_out is not None else 0,
+              _stream(ds))
+    return perm
+
+
+def gemm(A, B, M, N, K, lda, ldb, batch=1, sA=0, sB=0, a_rows=None, epi=EPI_STORE, bias=None, out_f=None,
+         out_t=None, ldc=None, sC=0, n1=None, n2=None):
+    """C = epi(A @ B^T (+bias)); A: rows of length >= K (lda), B: N x K (ldb)."""
+    _dev(A, B)
+    code = _code(A)
+    if _code(B) != code:
+        raise _lib.FpmError("gemm: A and B dtypes differ")
+    if out_t is not None and _code(out_t) != code:
+        raise _lib.FpmError("gemm: out_t dtype must match operands")
+    _lib.call("fpm_gemm", code, _p(A), lda, sA, _p(a_rows), _p(B), ldb, sB, int(M), int(N), int(K), int(batch),
+              int(epi), _p(bias), _p(out_f), _p(out_t), ldc if ldc is not None else N, sC, _p(n1), _p(n2),
+              _stream(A))
+
+
+def cast_bf16(x, out=None):
+    _dev(x)
+    if out is None:
+        out = torch.empty(x.shape, device=x.device, dtype=torch.bfloat16)
+    _lib.call("fpm_cast_bf16", _p(x), _p(out), x.numel(), _stream(x))
+    return out
+
+
+def spline_plan(src, dst, pseudo, num_nodes, nmax):
+    _dev(src, dst, pseudo)
+    E = src.numel()
+    nbytes = _lib.load().fpm_spline_plan_bytes(E, num_nodes)
+    ws = torch.empty(nbytes, device=src.device, dtype=torch.uint8)
+    _lib.call("fpm_spline_plan", _p(src), _p(dst), _p(pseudo), E, num_nodes, nmax, _p(ws), nbytes, _stream(src))
+    return ws
+
+
+def plan_csr(ws, E, num_nodes):
+    """(dst_ptr, nbr_local) raw device pointers (ints) inside a plan workspace."""
+    a, b = ctypes.c_void_p(), ctypes.c_void_p()
+    _lib.call("fpm_spline_plan_csr", _p(ws), E, num_nodes, ctypes.byref(a), ctypes.byref(b))
+    return a.value, b.value
+
+
+def spline_conv(x_op, plan, E, num_nodes, nmax, nvalid, W, R, bias, msg_ws, root_ws, mode, xres=None, cscale=None,
+                out_f=None, out_t=None):
+    _dev(x_op, plan, W, R, bias, msg_ws, root_ws)
+    code = _code(x_op)
+    _lib.call("fpm_spline_conv_fwd", code, _p(x_op), _p(plan), E, num_nodes, nmax, _p(nvalid), _p(W), _p(R),
+              _p(bias), _p(msg_ws), _p(root_ws), int(mode), _p(xres), _p(cscale), _p(out_f), _p(out_t),
+              _stream(x_op))
+
+
+def edge_diff(x, src, dst):
+    _dev(x, src, dst)
+    E, D = src.numel(), x.shape[-1]
+    out = torch.empty(E, D, device=x.device, dtype=torch.float32)
+    _lib.call("fpm_edge_diff", _p(x), _p(src), _p(dst), E, D, _p(out), _stream(x))
+    return out
+
+
+def gnn_layer(X, C, B, n1max, n2max, csr1, csr2, n1, n2, params, Xout, zbuf):
+    _dev(X, n1, n2, params, Xout, zbuf)
+    _lib.call("fpm_kron_gnn_layer_fwd", _p(X), C, B, n1max, n2max, ctypes.c_void_p(csr1[0]),
+              ctypes.c_void_p(csr1[1]), ctypes.c_void_p(csr2[0]), ctypes.c_void_p(csr2[1]), _p(n1), _p(n2),
+              _p(params), _p(Xout), _p(zbuf), _stream(X))
+
+
+def node_classifier(X, B, n1max, n2max, w, b, out):
+    _dev(X, w, b, out)
+    _lib.call("fpm_node_classifier", _p(X), B, n1max, n2max, _p(w), _p(b), _p(out), _stream(X))
+
+
+def crossset_attn(cost, n2, Wv, mix1w, mix1b, mix2w, mix2b, out):
+    _dev(cost, n2, Wv, out)
+    B, n1max, n2max = cost.shape
+    _lib.call("fpm_crossset_attn_fwd", _code(out), _p(cost), cost.stride(0), cost.stride(1), B, n1max, n2max,
+              _p(n2), _p(Wv), Wv.shape[1], _p(mix1w), _p(mix1b), _p(mix2w), _p(mix2b), _p(out), _stream(cost))
+
+
+def instnorm(in1, B, P, Cn, w, b, in2=None, nvalid=None, onehot_bias=None, out_f=None, out_t=None, gmax=None,
+             eps=1e-5):
+    code = _code(out_t) if out_t is not None else F32
+    ref = in1 if in1 is not None else w
+    _lib.call("fpm_instnorm", code, _p(in1), _p(in2), B, P, Cn, _p(nvalid), _p(onehot_bias), _p(w), _p(b),
+              float(eps), _p(out_f), _p(out_t), _p(gmax), _stream(ref))
+
+
+def afau_head(gr, gc, B, E, r0w, r0b, r2w, r2b, c0w, c0b, c2w, c2b, ks):
+    _lib.call("fpm_afau_head", _p(gr), _p(gc), B, E, _p(r0w), _p(r0b), _p(r2w), _p(r2b), _p(c0w), _p(c0b),
+              _p(c2w), _p(c2b), _p(ks), _stream(gr))
+
+
+def match_cls(s, perm, w1, b1, bn1_sc, bn1_sh, w2, b2, bn2_sc, bn2_sh, fcw, fcb):
+    _dev(s, perm)
+    B, H, W = s.shape
+    nws = _lib.load().fpm_match_cls_ws_floats(B, H, W)
+    ws = torch.empty(max(int(nws), 1), device=s.device, dtype=torch.float32)
+    logits = torch.empty(B, device=s.device, dtype=torch.float32)
+    prob = torch.empty(B, device=s.device, dtype=torch.float32)
+    _lib.call("fpm_match_cls_fwd", _p(s), _p(perm), B, H, W, _p(w1), _p(b1), _p(bn1_sc), _p(bn1_sh), _p(w2), _p(b2),
+              _p(bn2_sc), _p(bn2_sh), _p(fcw), _p(fcb), _p(ws), _p(logits), _p(prob), _stream(s))
+    return logits, prob
+
+
+def lsa_batch_host(s_host, n1_host, n2_host, nthreads=1):
+    """Host LSA (maximise s) over a pinned/CPU float32 (B, n1max, n2max) tensor -> (B, n1max) int32."""
+    if s_host.is_cuda:
+        raise _lib.FpmError("lsa_batch_host expects host memory")
+    s_host = s_host.contiguous()
+    B, n1max, n2max = s_host.shape
+    n1c = n1_host.to(torch.int32).contiguous()
+    n2c = n2_host.to(torch.int32).contiguous()
+    out = torch.empty(B, n1max, dtype=torch.int32)
+    rc = _lib.load().fpm_lsa_batch_host(_p(s_host), n1max * n2max, n2max, _p(n1c), _p(n2c), B, n1max, _p(out),
+                                        int(nthreads))
+    if rc != 0:
+        raise _lib.FpmError("fpm_lsa_batch_host: pair %d is infeasible or has NaN/-inf costs" % (rc - 1))
+    return out

@@ -1,0 +1,127 @@
+/*
+ * fpm.h — C-ABI of libfpm_hip.so, the MI355X (gfx950) graph-matching forward of the fingerprint
+ * QAP matcher (reference: dayne-2stacks/Fingerprint-Matching-Code).
+ *
+ * Conventions
+ *   - extern "C", plain pointers and sizes; no C++/torch types cross the boundary.
+ *   - Return value: 0 = ok, nonzero = error; fpm_last_error() returns a thread-local message.
+ *   - Device ops take a hipStream_t (passed as void*) and are asynchronous on it.
+ *   - The caller allocates every output and workspace (device memory unless noted "host").
+ *   - dtype codes for MFMA operands: 0 = fp32, 1 = bf16 (raw 16-bit); accumulation is fp32.
+ *   - Batched matrices are addressed by (base, batch stride, row stride[, col stride]) in elements.
+ *
+ * What this replaces: the reference's pybind11 extensions JIT-built at import time
+ * (src/sparse_torch/csx_matrix.py:10-17, src/sparse.py:12-16) and the third-party operators its
+ * live forward calls (PyG SplineConv/SAGEConv, torch_sparse, pygmtools, scipy LSA).  Each entry
+ * point cites the reference interface it stands in for.
+ */
+#ifndef FPM_H_
+#define FPM_H_
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- plumbing ------------------------------------------------------------------------------ */
+const char* fpm_last_error(void);
+int fpm_version(void);
+int fpm_device_sync(void);
+
+/* ---- log-domain Sinkhorn ---------------------------------------------------------------------
+ * Replaces Sinkhorn.forward_log -> pygmtools.sinkhorn (src/model/sinkhorn.py:85-87), used by
+ * PYGNNLayer (src/model/gnn.py:221, 20 iterations) and Net.forward (ngm.py:371, 10 iterations).
+ * out[b] = exp(L) on the valid block [:n1[b], :n2[b]] of the (n1max, n2max) box, 0 elsewhere.
+ * Any strides; n1max, n2max <= 256 (VGPR-resident block). */
+int fpm_sinkhorn_log_fwd(const float* s, long s_sb, long s_si, long s_sj, float* out, long o_sb, long o_si,
+                         long o_sj, const int* n1, const int* n2, int B, int n1max, int n2max, int iters,
+                         float tau, int dummy_row, void* stream);
+
+/* ---- soft top-k -------------------------------------------------------------------------------
+ * Replaces soft_topk(..., return_prob=True)[1] (src/model/soft_topk.py:8-53) incl. Sinkhorn_m's
+ * data-dependent continuation (:232-241).  k[b] = number of matches (ks * min(n1,n2) in eval).
+ * steps_out (optional, int32[B]) receives the number of normalisation steps run. */
+int fpm_soft_topk_fwd(const float* ss, long s_sb, long s_ld, const int* n1, const int* n2, const float* k, int B,
+                      int n1max, int n2max, int iters, float tau, float* out, long o_sb, long o_ld, int* steps_out,
+                      void* stream);
+
+/* ---- greedy top-k selection -------------------------------------------------------------------
+ * Replaces argsort(x * ss_out) + greedy_perm (ngm.py:445-449, soft_topk.py:56-77).
+ * assign[b][r] = column matched to row r by the LSA (or -1); perm receives the 0/1 matrix;
+ * lsa_out (optional) receives the dense LSA matrix x. */
+int fpm_topk_select(const float* ds, long d_sb, long d_ld, const int* assign, long a_sb, const float* k, int B,
+                    int n1max, int n2max, float* perm, long p_sb, long p_ld, float* lsa_out, long l_sb, long l_ld,
+                    void* stream);
+
+/* ---- generic MFMA GEMM with fused epilogue ----------------------------------------------------
+ * C[b][r][n] = epi(sum_k A[b][row(r)][k] * B[b][n][k] (+ bias[n])), row(r) = a_rows ? a_rows[r] : r.
+ * epi: 0 store, 1 relu, 2 tanh, 3 affinity (softplus(v) - 0.5 inside [:n2[b], :n1[b]], else 0).
+ * Stands in for nn.Linear / torch.matmul on the hot path: InnerProductWithWeightsAffinity
+ * (affinity_layer.py:13-18), AFA-U projections and FFN (afau.py:99-103, 188-199). */
+int fpm_gemm(int dtype, const void* A, long lda, long sA, const int* a_rows, const void* B, long ldb, long sB, int M,
+             int N, int K, int batch, int epi, const float* bias, float* Cf, void* Ct, long ldc, long sC,
+             const int* n1, const int* n2, void* stream);
+int fpm_cast_bf16(const float* x, void* y, long n, void* stream);
+
+/* ---- SplineConv message passing ---------------------------------------------------------------
+ * Replaces PyG 1.6.3 SplineConv(768, 768, dim=2, kernel_size=5, aggr='max') inside SConv /
+ * SiameseSConvOnNodes (src/model/spline_conv.py:17, 28-57).
+ * fpm_spline_plan: bucket the side-batch's edges by B-spline group (device workspace of
+ * fpm_spline_plan_bytes bytes; reused by both layers and by the GNN layer's CSR).
+ * fpm_spline_conv_fwd: one layer; mode 0 -> relu(conv(x)), mode 1 -> xres + 0.1 * conv(x). */
+long fpm_spline_plan_bytes(long E, long num_nodes);
+int fpm_spline_plan(const int* src, const int* dst, const float* pseudo, long E, long num_nodes, int nmax, void* ws,
+                    long ws_bytes, void* stream);
+int fpm_spline_plan_csr(void* ws, long E, long num_nodes, int** dst_ptr, int** nbr_local);
+int fpm_spline_conv_fwd(int dtype, const void* x_op, const void* plan_ws, long E, long num_nodes, int nmax,
+                        const int* nvalid, const void* W, const void* R, const float* bias, void* msg_ws,
+                        float* root_ws, int mode, const float* xres, const float* cscale, float* out_f, void* out_t,
+                        void* stream);
+/* vertex_attr_to_edge_attr (spline_conv.py:73-81): out[e] = x[src[e]] - x[dst[e]] */
+int fpm_edge_diff(const float* x, const int* src, const int* dst, long E, int D, float* out, void* stream);
+
+/* ---- association-graph GNN layer --------------------------------------------------------------
+ * Replaces PYGNNLayer.forward's SAGEConv mean aggregation over the Kronecker pattern + MLPs +
+ * classifier (src/model/gnn.py:207-218; pattern from factorize_graph_matching.py:57-95 and
+ * gmdataset.py:614-642), factorised so the n1*n2 x n1*n2 pattern is never built.
+ * X: (B, C, n2max, n1max) with C in {1, 17}; Xout channels 0..15 and zbuf (B, n2max, n1max)
+ * are written; the caller runs fpm_sinkhorn_log_fwd(zbuf -> Xout channel 16). */
+int fpm_kron_gnn_layer_fwd(const float* X, int C, int B, int n1max, int n2max, const int* ptr1, const int* nbr1,
+                           const int* ptr2, const int* nbr2, const int* n1, const int* n2, const float* params,
+                           float* Xout, float* zbuf, void* stream);
+int fpm_gnn_param_count(int C);
+/* final classifier (ngm.py:368-369): s[b][i][j] = w . X[b][:, j, i] + bias */
+int fpm_node_classifier(const float* X, int B, int n1max, int n2max, const float* w, const float* bias, float* s,
+                        void* stream);
+
+/* ---- AFA-U k regressor (ngm.py:386-412, src/model/afau.py) ------------------------------------ */
+int fpm_crossset_attn_fwd(int dtype, const float* cost, long c_sb, long c_ld, int B, int n1max, int n2max,
+                          const int* n2, const float* Wv, int emb, const float* mix1w, const float* mix1b,
+                          const float* mix2w, const float* mix2b, void* out, void* stream);
+int fpm_instnorm(int dtype, const float* in1, const float* in2, int B, int P, int Cn, const int* nvalid,
+                 const float* onehot_bias, const float* w, const float* bias, float eps, float* out_f, void* out_t,
+                 float* gmax, void* stream);
+int fpm_afau_head(const float* gr, const float* gc, int B, int E, const float* r0w, const float* r0b,
+                  const float* r2w, const float* r2b, const float* c0w, const float* c0b, const float* c2w,
+                  const float* c2b, float* ks, void* stream);
+
+/* ---- MatchClassifier (ngm.py:75-106, applied at :451-455) ------------------------------------- */
+long fpm_match_cls_ws_floats(int B, int H, int W);
+int fpm_match_cls_fwd(const float* s, const float* perm, int B, int H, int W, const float* w1, const float* b1,
+                      const float* bn1_sc, const float* bn1_sh, const float* w2, const float* b2,
+                      const float* bn2_sc, const float* bn2_sh, const float* fcw, const float* fcb, float* ws,
+                      float* logits, float* prob, void* stream);
+
+/* ---- profiling hooks: HIP-event timing of the dominant kernel (edge-message GEMM) ------------ */
+int fpm_profile_enable(int on);
+int fpm_profile_read(double* ms_total, double* flops_total, int* count);
+
+/* ---- host: batched linear sum assignment ------------------------------------------------------
+ * Replaces utils/hungarian.py:8-66 (scipy linear_sum_assignment on -s, per pair).  Synchronous,
+ * HOST memory, nthreads worker threads.  assign[b][r] = column or -1.  Returns 0 or (pair + 1). */
+int fpm_lsa_batch_host(const float* s, long sb, long ld, const int* n1, const int* n2, int B, int n1max, int* assign,
+                       int nthreads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FPM_H_ */

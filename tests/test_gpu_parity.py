@@ -1,0 +1,209 @@
+"""Parity of the HIP path (through the C-ABI) against the CPU oracle on identical inputs.
+
+Tolerances (fp32 mode): 1e-4 abs on ss / ds_mat / k_prob (the north-star gate), identical
+perm_mat; per-stage tolerances are tighter where the stage is well conditioned.  The bf16 mode
+is reported against the fp32 oracle with a loose bound (it is a throughput mode).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import fpm
+from fpm import ops, params, synth
+from fpm.batch import DeviceBatch
+import oracle as O
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+
+
+def _i32(x):
+    return torch.as_tensor(np.asarray(x), dtype=torch.int32, device=DEV)
+
+
+@pytest.fixture(scope="module")
+def sd():
+    return params.init_params(7)
+
+
+# ---------------------------------------------------------------------------------------- sinkhorn
+@pytest.mark.parametrize("n1s,n2s,iters,tau", [
+    ((8, 8, 8), (8, 8, 8), 10, 0.05),
+    ((32, 20, 32), (32, 32, 17), 20, 0.01),          # dummy rows + transposed pair
+    ((100, 64, 128), (128, 128, 90), 10, 0.01),
+    ((256, 256), (256, 256), 20, 0.01),
+    ((200, 256, 131), (256, 190, 256), 10, 0.01),
+])
+def test_sinkhorn_vs_oracle(n1s, n2s, iters, tau):
+    g = torch.Generator().manual_seed(len(n1s) * 100 + n1s[0])
+    B = len(n1s)
+    n1max, n2max = max(n1s), max(n2s)
+    s = torch.randn(B, n1max, n2max, generator=g) * 0.3
+    ref = O.pygm_sinkhorn(s.double(), n1s, n2s, dummy_row=True, max_iter=iters, tau=tau)
+    out = ops.sinkhorn(s.to(DEV), _i32(n1s), _i32(n2s), iters, tau, True).cpu()
+    assert (out.double() - ref).abs().max() < 1e-4
+    # strided (transposed) input and output views
+    sT = s.transpose(1, 2).contiguous().to(DEV).transpose(1, 2)
+    o2 = torch.zeros(B, n2max, n1max, device=DEV).transpose(1, 2)
+    ops.sinkhorn(sT, _i32(n1s), _i32(n2s), iters, tau, True, out=o2)
+    assert (o2.cpu().double() - ref).abs().max() < 1e-4
+
+
+# ---------------------------------------------------------------------------------------- soft top-k
+def test_soft_topk_golden():
+    z = np.load(os.path.join(GOLDEN, "soft_topk.npz"))
+    for i in range(int(z["ncases"])):
+        g = lambda k: z["c%d_%s" % (i, k)]
+        sc = torch.from_numpy(g("scores")).to(DEV)
+        out = ops.soft_topk(sc, _i32(g("n1")), _i32(g("n2")), torch.from_numpy(g("ks")).to(DEV), 10, 0.01)
+        np.testing.assert_allclose(out.cpu().numpy(), g("ss_out"), atol=1e-5, rtol=0)
+
+
+def test_soft_topk_vs_oracle_large():
+    g = torch.Generator().manual_seed(5)
+    B, n = 4, 256
+    ss = torch.rand(B, n, n, generator=g) ** 6
+    k = torch.tensor([30.5, 100.0, 5.2, 250.0])
+    nn_ = [n] * B
+    ref = O.soft_topk(ss, k, nn_, nn_, 10, 0.01)
+    out = ops.soft_topk(ss.to(DEV), _i32(nn_), _i32(nn_), k.to(DEV), 10, 0.01).cpu()
+    assert (out - ref).abs().max() < 1e-4
+
+
+# ---------------------------------------------------------------------------------------- top-k select
+def test_topk_select_golden():
+    z = np.load(os.path.join(GOLDEN, "hungarian_greedy.npz"))
+    s = torch.from_numpy(z["s"])
+    assign = ops.lsa_batch_host(s, torch.from_numpy(z["n1"]), torch.from_numpy(z["n2"]))
+    perm = ops.topk_select(s.to(DEV), assign.to(DEV), torch.from_numpy(z["ks"]).to(DEV))
+    np.testing.assert_array_equal(perm.cpu().numpy(), z["perm"])
+
+
+# ---------------------------------------------------------------------------------------- GEMM
+@pytest.mark.parametrize("dt,tol", [(torch.float32, 2e-5), (torch.bfloat16, 2e-2)])
+def test_gemm_vs_torch(dt, tol):
+    g = torch.Generator().manual_seed(3)
+    M, N, K = 300, 200, 600
+    A = torch.randn(M, K, generator=g)
+    Bm = torch.randn(N, K, generator=g)
+    bias = torch.randn(N, generator=g)
+    rows = torch.randint(0, M, (257,), generator=g)
+    out = torch.empty(257, N, device=DEV)
+    ops.gemm(A.to(DEV).to(dt), Bm.to(DEV).to(dt), 257, N, K, K, K, a_rows=rows.to(DEV).int(), epi=ops.EPI_RELU,
+             bias=bias.to(DEV), out_f=out)
+    ref = torch.relu(A.to(dt).float()[rows] @ Bm.to(dt).float().t() + bias)
+    assert ((out.cpu() - ref).abs().max() / ref.abs().max()) < tol
+
+
+# ---------------------------------------------------------------------------------------- SplineConv
+def test_spline_conv_vs_oracle(sd):
+    pairs = synth.make_batch(11, 3, 40, n2=[40, 33, 21])
+    bt = DeviceBatch.from_pairs(pairs, DEV)
+    net = fpm.Net(regression=True)
+    net.load_state_dict(sd)
+    out = net.run_gpu_stage(bt, keep_feats=True)
+    for side, key in ((0, "feat0"), (1, "feat1")):
+        nmax = bt.nmax[side]
+        f = out[key].view(bt.B, nmax, -1).cpu()
+        for b in range(bt.B):
+            gph = pairs[b][side]
+            ref = O.siamese_sconv(torch.from_numpy(gph["x"]), torch.from_numpy(gph["edge_index"]),
+                                  torch.from_numpy(gph["pseudo"]), sd)
+            assert (f[b, :gph["n"]] - ref).abs().max() < 2e-5
+            assert f[b, gph["n"]:].abs().max() == 0 if gph["n"] < nmax else True
+
+
+# ---------------------------------------------------------------------------------------- forward
+def _compare_forward(pairs, sd, dtype="f32", tol=1e-4, regression=True):
+    net = fpm.Net(regression=regression, dtype=dtype)
+    net.load_state_dict(sd)
+    bt = DeviceBatch.from_pairs(pairs, DEV)
+    res = net.run(bt)
+    ref = O.forward(pairs, sd, regression=regression)
+    d = {}
+    for k in ("Kp", "s", "ss", "ds_mat", "k_prob", "cls_prob"):
+        d[k] = float((res[k].float().cpu() - ref[k]).abs().max())
+    d["perm_equal"] = bool(torch.equal(res["perm_mat"].cpu(), ref["perm_mat"]))
+    return d
+
+
+def test_forward_c1_parity(sd):
+    """Config 1: single pair, 32 keypoints."""
+    d = _compare_forward(synth.make_batch(1, 1, 32), sd)
+    assert d["Kp"] < 1e-5 and d["s"] < 1e-4, d
+    assert d["ss"] < 1e-4 and d["ds_mat"] < 1e-4 and d["k_prob"] < 1e-4, d
+    assert d["perm_equal"], d
+    assert d["cls_prob"] < 1e-4, d
+
+
+def test_forward_batch_parity(sd):
+    d = _compare_forward(synth.make_batch(2, 4, 64), sd)
+    assert d["ss"] < 1e-4 and d["ds_mat"] < 1e-4 and d["k_prob"] < 1e-4, d
+    assert d["perm_equal"], d
+
+
+def test_forward_ragged_parity(sd):
+    """Ragged batch: padded p-space diagonal, dummy rows, transposed Sinkhorn, AFA-U padding."""
+    d = _compare_forward(synth.make_batch(3, 3, [30, 24, 28], n2=[26, 30, 28]), sd)
+    assert d["ss"] < 1e-4 and d["ds_mat"] < 1e-4 and d["k_prob"] < 1e-4, d
+    assert d["perm_equal"], d
+
+
+def test_forward_no_regression_parity(sd):
+    d = _compare_forward(synth.make_batch(4, 2, 48), sd, regression=False)
+    assert d["ss"] < 1e-4 and d["ds_mat"] < 1e-4, d
+    assert d["perm_equal"], d
+
+
+def test_forward_n256_parity(sd):
+    """Benchmark graph size (C3's n=256) at a batch the CPU oracle finishes in seconds."""
+    d = _compare_forward(synth.make_batch(5, 2, 256), sd)
+    assert d["ss"] < 1e-4 and d["ds_mat"] < 1e-4 and d["k_prob"] < 1e-4, d
+    assert d["perm_equal"], d
+
+
+def test_forward_bf16_reported(sd):
+    """bf16 MFMA mode vs the fp32 oracle: reported deviation, loose bound."""
+    d = _compare_forward(synth.make_batch(6, 2, 128), sd, dtype="bf16")
+    print("bf16 deviation vs fp32 oracle:", d)
+    assert d["Kp"] < 0.05 and d["k_prob"] < 0.1, d
+
+
+def test_forward_data_dict_surface(sd):
+    """Reference-shaped data_dict in, reference keys out (ngm.py:479-487)."""
+    pairs = synth.make_batch(8, 2, 24, n2=[24, 20])
+    B = 2
+
+    class G:
+        pass
+    dd = {"ns": [torch.tensor([p[0]["n"] for p in pairs]), torch.tensor([p[1]["n"] for p in pairs])],
+          "pyg_graphs": [], "node_features": [], "global_features": []}
+    for side in range(2):
+        g = G()
+        offs = np.cumsum([0] + [p[side]["n"] for p in pairs])
+        g.edge_index = torch.from_numpy(np.concatenate([p[side]["edge_index"] + offs[b] for b, p in enumerate(pairs)], 1))
+        g.edge_attr = torch.from_numpy(np.concatenate([p[side]["pseudo"] for p in pairs]))
+        g.ptr = torch.from_numpy(offs)
+        dd["pyg_graphs"].append(g)
+        dd["node_features"].append(torch.from_numpy(np.concatenate([p[side]["x"] for p in pairs])))
+        dd["global_features"].append(torch.from_numpy(np.stack([p[side]["w"] for p in pairs])))
+    gt = torch.zeros(B, 24, 24)
+    for b in range(B):
+        m = min(pairs[b][0]["n"], pairs[b][1]["n"])
+        gt[b, range(m), range(m)] = 1
+    dd["gt_perm_mat"] = gt
+    dd["label"] = torch.tensor([1.0, 0.0])
+    net = fpm.Net(regression=True)
+    net.load_state_dict(sd)
+    out = net(dd)
+    for k in ("ds_mat", "perm_mat", "ks_loss", "ks_error", "cls_loss", "cls_prob", "k_prob"):
+        assert k in out
+    ref = O.forward(pairs, sd, gt_perm=gt, labels=torch.tensor([1.0, 0.0]))
+    assert (out["ds_mat"].cpu() - ref["ds_mat"]).abs().max() < 1e-4
+    assert abs(float(out["ks_loss"]) - float(ref["ks_loss"])) < 1e-3
+    assert abs(float(out["cls_loss"]) - float(ref["cls_loss"])) < 1e-4
