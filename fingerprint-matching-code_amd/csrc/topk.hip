@@ -11,10 +11,6 @@
 
 namespace {
 
-struct TopkState {
-    float vu0, vu1, v0, v1;
-};
-
 __device__ __forceinline__ float urow(float a0, float a1) {
     float m = fmaxf(a0, a1);
     if (m == -INFINITY) return INFINITY;
@@ -66,17 +62,41 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
     const float kk = kvec[b];
     const float lcp0 = logf((float)N - kk);   // log(col_prob[:,0]) = log(n1*n2 - k)
     const float lcp1 = logf(kk);              // log(col_prob[:,1]) = log(k)
-    TopkState st = {0.f, 0.f, 0.f, 0.f};
+    // state: L_c(q) = a_c - u(q) [after a row step]  or  ((a_c - u) - lse_c) + lcp_c [after a
+    // column step], a_c = D_c - vu_c, u = lse(a_0, a_1).  The last two steps are evaluated with the
+    // reference's own operation order, so "L <= 0 after a row step" holds exactly as it does there.
+    float vu0 = 0.f, vu1 = 0.f, lse0 = 0.f, lse1 = 0.f;
+    int last = 0;   // 0: none, 1: row, 2: column
 
-    auto colstep = [&]() {
+    auto Lpair = [&](int k, float& L0, float& L1) {
+        float a0 = d0[k] - vu0, a1 = d1[k] - vu1;
+        float u = urow(a0, a1);
+        L0 = a0 - u;
+        L1 = a1 - u;
+        if (last == 2) {
+            L0 = (L0 - lse0) + lcp0;
+            L1 = (L1 - lse1) + lcp1;
+        }
+        if (L0 != L0) L0 = -INFINITY;
+        if (L1 != L1) L1 = -INFINITY;
+    };
+    auto rowstep = [&]() {
+        if (last == 2) {
+            float t0 = vu0 + (lse0 - lcp0), t1 = vu1 + (lse1 - lcp1);
+            vu0 = (lse0 == -INFINITY || t0 != t0) ? INFINITY : t0;
+            vu1 = (lse1 == -INFINITY || t1 != t1) ? INFINITY : t1;
+        }
+        last = 1;
+    };
+    auto colstep = [&]() {   // always follows a row step
         float m0 = -INFINITY, m1 = -INFINITY;
 #pragma unroll
         for (int k = 0; k < NQ; ++k) {
-            int q = tid + 1024 * k;
-            if (q < N) {
-                float u = urow(d0[k] - st.vu0, d1[k] - st.vu1);
-                m0 = fmaxf(m0, d0[k] - u - st.v0);
-                m1 = fmaxf(m1, d1[k] - u - st.v1);
+            if (tid + 1024 * k < N) {
+                float L0, L1;
+                Lpair(k, L0, L1);
+                m0 = fmaxf(m0, L0);
+                m1 = fmaxf(m1, L1);
             }
         }
         m0 = fpm::warp_max(m0);
@@ -89,11 +109,11 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
         float a0 = 0.f, a1 = 0.f;
 #pragma unroll
         for (int k = 0; k < NQ; ++k) {
-            int q = tid + 1024 * k;
-            if (q < N) {
-                float u = urow(d0[k] - st.vu0, d1[k] - st.vu1);
-                if (m0 != -INFINITY) a0 += expf(d0[k] - u - st.v0 - m0);
-                if (m1 != -INFINITY) a1 += expf(d1[k] - u - st.v1 - m1);
+            if (tid + 1024 * k < N) {
+                float L0, L1;
+                Lpair(k, L0, L1);
+                if (m0 != -INFINITY) a0 += expf(L0 - m0);
+                if (m1 != -INFINITY) a1 += expf(L1 - m1);
             }
         }
         a0 = fpm::warp_sum(a0);
@@ -103,20 +123,18 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
         a0 = 0.f; a1 = 0.f;
         for (int w = 0; w < 16; ++w) { a0 += sa[w]; a1 += sb_[w]; }
         __syncthreads();
-        // L_new = L - lse_q(L) + log cp  =>  v_new = v + lse_q(L) - log cp ; NaN -> -inf
-        if (m0 == -INFINITY) st.v0 = INFINITY;
-        else { float t = st.v0 + (m0 + logf(a0)) - lcp0; st.v0 = (t != t) ? INFINITY : t; }
-        if (m1 == -INFINITY) st.v1 = INFINITY;
-        else { float t = st.v1 + (m1 + logf(a1)) - lcp1; st.v1 = (t != t) ? INFINITY : t; }
+        lse0 = (m0 == -INFINITY) ? -INFINITY : m0 + logf(a0);
+        lse1 = (m1 == -INFINITY) ? -INFINITY : m1 + logf(a1);
+        last = 2;
     };
     auto any_pos = [&]() -> bool {
         int flag = 0;
 #pragma unroll
         for (int k = 0; k < NQ; ++k) {
-            int q = tid + 1024 * k;
-            if (q < N) {
-                float u = urow(d0[k] - st.vu0, d1[k] - st.vu1);
-                flag |= ((d0[k] - u - st.v0) > 0.f) | ((d1[k] - u - st.v1) > 0.f);
+            if (tid + 1024 * k < N) {
+                float L0, L1;
+                Lpair(k, L0, L1);
+                flag |= (L0 > 0.f) | (L1 > 0.f);
             }
         }
         int wf = __any(flag) ? 1 : 0;
@@ -131,11 +149,11 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
     int step = 0;
     for (; step < iters; ++step) {
         if (step & 1) colstep();
-        else { st.vu0 = st.v0; st.vu1 = st.v1; }
+        else rowstep();
     }
     for (int guard = 0; guard < 64 && any_pos(); ++guard, ++step) {
         if (step & 1) colstep();
-        else { st.vu0 = st.v0; st.vu1 = st.v1; }
+        else rowstep();
     }
     if (steps_out && tid == 0) steps_out[b] = step;
 
@@ -150,8 +168,9 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
         int q = tid + 1024 * k;
         if (q < N) {
             int i = q / n2b, j = q - i * n2b;
-            float u = urow(d0[k] - st.vu0, d1[k] - st.vu1);
-            O[i * old_ + j] = expf(d1[k] - u - st.v1);
+            float L0, L1;
+            Lpair(k, L0, L1);
+            O[i * old_ + j] = expf(L1);
         }
     }
 }
