@@ -38,7 +38,8 @@ def cpu_baseline(n, npairs, seed, sd):
     """The CPU oracle (PyTorch CPU restatement of the same forward) on a bounded sample."""
     import torch
     import oracle as O
-    cores = len(os.sched_getaffinity(0))
+    # the box's CPU share (OMP_NUM_THREADS, 16 on the GPU pool), not the whole machine's affinity
+    cores = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16")), len(os.sched_getaffinity(0))))
     torch.set_num_threads(cores)
     pairs = make_pairs(seed + 7919, 0, npairs, n, 1)
     O.forward(pairs[:1], sd)                   # warm-up
@@ -47,6 +48,13 @@ def cpu_baseline(n, npairs, seed, sd):
     dt = time.perf_counter() - t
     return {"value": npairs / dt, "unit": "pairs/s", "cores": cores, "kind": "port",
             "sample": "%d pairs, n=%d, fp32 oracle forward incl. scipy Hungarian (1 process)" % (npairs, n)}
+
+
+def log(*a):
+    print("[bench %.1fs]" % (time.perf_counter() - T0), *a, file=sys.stderr, flush=True)
+
+
+T0 = time.perf_counter()
 
 
 def main():
@@ -58,7 +66,7 @@ def main():
     ap.add_argument("--n", type=int, default=256, help="keypoints per graph")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--cpu-pairs", type=int, default=8)
+    ap.add_argument("--cpu-pairs", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--lsa-threads", type=int, default=0)
     ap.add_argument("--gen-workers", type=int, default=16)
@@ -74,6 +82,7 @@ def main():
     t_gen = time.perf_counter()
     pairs = make_pairs(args.seed, rank * args.batch, args.batch, args.n, args.gen_workers)
     t_gen = time.perf_counter() - t_gen
+    log("generated %d pairs in %.1fs" % (args.batch, t_gen))
 
     import torch
     import torch.distributed as dist
@@ -96,8 +105,10 @@ def main():
         if world > 1:
             dist.barrier()
 
+    log("batch on device, E/graph=%.1f" % (E_tot / (2.0 * args.batch)))
     for _ in range(args.warmup):
         net.run(bt)
+        log("warmup step: gpu-stage %.3fs lsa %.3fs" % (net.last_timing["gpu_stage_s"], net.last_timing["lsa_s"]))
     torch.cuda.synchronize()
     lib = _lib.load()
     import ctypes
@@ -111,6 +122,7 @@ def main():
         net.run(bt)
         gpu_s += net.last_timing["gpu_stage_s"]
         lsa_s += net.last_timing["lsa_s"]
+        log("step: gpu-stage %.3fs lsa %.3fs" % (net.last_timing["gpu_stage_s"], net.last_timing["lsa_s"]))
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier()
@@ -132,7 +144,9 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
+            log("cpu baseline ...")
             cpu = cpu_baseline(args.n, args.cpu_pairs, args.seed, sd)
+            log("cpu baseline %.3f pairs/s" % cpu["value"])
         res = {
             "metric": "graph-match pairs/sec @ n=256 kpts, batch=1024, 1 & 8 GPU",
             "value": value,

@@ -58,11 +58,14 @@ class Net(nn.Module):
         if dtype not in ("f32", "bf16"):
             raise ValueError("dtype must be 'f32' or 'bf16'")
         self.dtype_mode = dtype
-        self.lsa_threads = lsa_threads or max(1, min(16, len(os.sched_getaffinity(0))))
+        self.lsa_threads = lsa_threads or max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16")), len(os.sched_getaffinity(0))))
         self._pack = None
         self._pack_key = None
         self._pinned = None
         self._keep_feats = False
+        self._stage_timing = os.environ.get("FPM_STAGE_TIMING", "0") == "1"
+        self.stage_times = {}
+        self._t_last = 0.0
         self.last_timing = {}
         self.eval()
 
@@ -190,9 +193,20 @@ class Net(nn.Module):
                       wp["final_row2b"], wp["final_col0w"], wp["final_col0b"], wp["final_col2w"], wp["final_col2b"], ks)
         return ks
 
+    def _mark(self, name):
+        """Diagnostic stage timing (FPM_STAGE_TIMING=1): synchronises, so never in timed runs."""
+        if self._stage_timing:
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            self.stage_times[name] = self.stage_times.get(name, 0.0) + (t - self._t_last)
+            self._t_last = t
+
     def run_gpu_stage(self, bt, keep_feats=False):
         """Everything up to ds_mat on the GPU.  Returns a dict of device tensors."""
         self._keep_feats = keep_feats
+        if self._stage_timing:
+            torch.cuda.synchronize()
+            self._t_last = time.perf_counter()
         wp = self.packed(bt.device)
         dev = bt.device
         B, n1max, n2max = bt.B, bt.n1max, bt.n2max
@@ -203,14 +217,17 @@ class Net(nn.Module):
         coef = torch.empty(B, C.NODE_FEATURE_DIM, device=dev, dtype=torch.float32)
         ops.gemm(gw, wp["aff_w"], B, C.NODE_FEATURE_DIM, C.GLOBAL_STATE_DIM, C.GLOBAL_STATE_DIM, C.GLOBAL_STATE_DIM,
                  epi=ops.EPI_TANH, bias=wp["aff_b"], out_f=coef)
+        self._mark("coef")
         plan0, x1c, f1 = self._spline_side(wp, bt, 0, coef)
         plan1, x2, f2 = self._spline_side(wp, bt, 1, None)
+        self._mark("splineconv")
         # Kp^T per pair: emb0[b][j][i] = softplus((x1_i o c) . x2_j) - 0.5 on the valid block (ngm.py:277-321)
         X = torch.empty(B, 1, n2max, n1max, device=dev, dtype=torch.float32)
         ops.gemm(x2, x1c, n2max, n1max, C.NODE_FEATURE_DIM, C.NODE_FEATURE_DIM, C.NODE_FEATURE_DIM, batch=B,
                  sA=n2max * C.NODE_FEATURE_DIM, sB=n1max * C.NODE_FEATURE_DIM, epi=ops.EPI_AFFINITY, out_f=X,
                  ldc=n1max, sC=N, n1=bt.n1, n2=bt.n2)
         Kp = X
+        self._mark("affinity")
         csr1 = ops.plan_csr(plan0, bt.E[0], B * n1max)
         csr2 = ops.plan_csr(plan1, bt.E[1], B * n2max)
         zbuf = torch.empty(B, n2max, n1max, device=dev, dtype=torch.float32)
@@ -222,9 +239,11 @@ class Net(nn.Module):
             ops.sinkhorn(zbuf.transpose(1, 2), bt.n1, bt.n2, C.GNN_SK_ITER, self.tau, True,
                          out=Xn[:, 16].transpose(1, 2))
             X, Cin = Xn, 17
+            self._mark("gnn%d" % l)
         s = torch.empty(B, n1max, n2max, device=dev, dtype=torch.float32)
         ops.node_classifier(X, B, n1max, n2max, wp["cls_w"], wp["cls_b"], s)
         ss = ops.sinkhorn(s, bt.n1, bt.n2, C.SK_ITER_NUM, self.tau, True)
+        self._mark("final_sinkhorn")
         out = dict(s=s, ss=ss, Kp=Kp[:, 0].transpose(1, 2), coef=coef)
         if keep_feats:
             out["feat0"], out["feat1"] = f1, f2
@@ -246,9 +265,11 @@ class Net(nn.Module):
             ks = self._afau(self.packed(dev), ss, bt)
         else:
             ks = gt_ks / min_pt
+        self._mark("afau")
         k_used = gt_ks if self.training else ks * min_pt
         steps = torch.empty(B, device=dev, dtype=torch.int32)
         ds = ops.soft_topk(ss, bt.n1, bt.n2, k_used.contiguous(), C.SK_ITER_NUM, self.tau, steps=steps)
+        self._mark("soft_topk")
         # Hungarian on host threads (utils/hungarian.py): D2H ds_mat, LSA, H2D assignment
         if self._pinned is None or self._pinned.shape != ds.shape:
             self._pinned = torch.empty(ds.shape, dtype=torch.float32, pin_memory=True)
@@ -262,10 +283,12 @@ class Net(nn.Module):
         lsa = torch.empty(B, n1max, n2max, device=dev, dtype=torch.float32)
         kk = (ks * min_pt).contiguous()
         perm = ops.topk_select(ds, assign_d, kk, lsa_out=lsa)
+        self._mark("lsa+h2d+select")
         logits, prob = ops.match_cls(s, perm, self._pack["mc_w1"], self._pack["mc_b1"], self._pack["mc_sc1"],
                                      self._pack["mc_sh1"], self._pack["mc_w2"], self._pack["mc_b2"],
                                      self._pack["mc_sc2"], self._pack["mc_sh2"], self._pack["mc_fcw"],
                                      self._pack["mc_fcb"])
+        self._mark("match_cls")
         res = dict(out)
         res.update(ds_mat=ds, perm_mat=perm, k_prob=ks, cls_prob=prob, cls_logits=logits, lsa=lsa,
                    sk_steps=steps)
