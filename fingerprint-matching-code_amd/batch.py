@@ -16,14 +16,49 @@ from . import config as C
 
 
 class DeviceBatch:
-    def __init__(self, B, n1, n2, x, w, src, dst, pseudo, device):
+    def __init__(self, B, n1, n2, x, w, src, dst, pseudo, device, nmax=None, edge_off=None):
         self.B = B
         self.device = device
         self.n_host = [torch.as_tensor(n1, dtype=torch.int32), torch.as_tensor(n2, dtype=torch.int32)]
         self.n = [t.to(device) for t in self.n_host]
-        self.nmax = [int(self.n_host[0].max()), int(self.n_host[1].max())]
+        # padded sizes; a sub-batch keeps its parent's (results depend on the batch maxima, quirk A.10(iii))
+        self.nmax = list(nmax) if nmax is not None else [int(self.n_host[0].max()), int(self.n_host[1].max())]
         self.x, self.w, self.src, self.dst, self.pseudo = x, w, src, dst, pseudo
         self.E = [int(s.numel()) for s in src]
+        # per side, cumulative edge offsets per pair (host), for splitting into sub-batches
+        self.edge_off = edge_off
+        self._splits = {}
+
+    def split(self, k):
+        """k contiguous sub-batches of pairs (views of x/w, renumbered edge copies); cached."""
+        if k <= 1 or self.B < 2:
+            return [self]
+        if k in self._splits:
+            return self._splits[k]
+        if self.edge_off is None:
+            raise ValueError("split() needs per-pair edge offsets")
+        bounds = [round(i * self.B / k) for i in range(k + 1)]
+        parts = []
+        for c in range(k):
+            b0, b1 = bounds[c], bounds[c + 1]
+            if b1 <= b0:
+                continue
+            xs, ws, ss, ds, ps = [], [], [], [], []
+            for side in range(2):
+                nm = self.nmax[side]
+                e0, e1 = int(self.edge_off[side][b0]), int(self.edge_off[side][b1])
+                xs.append(self.x[side][b0 * nm:b1 * nm])
+                ws.append(self.w[side][b0:b1])
+                ss.append((self.src[side][e0:e1] - b0 * nm).contiguous())
+                ds.append((self.dst[side][e0:e1] - b0 * nm).contiguous())
+                ps.append(self.pseudo[side][e0:e1])
+            eo = [self.edge_off[side][b0:b1 + 1] - self.edge_off[side][b0] for side in range(2)]
+            sub = DeviceBatch(b1 - b0, self.n_host[0][b0:b1], self.n_host[1][b0:b1], xs, ws, ss, ds, ps, self.device,
+                              nmax=self.nmax, edge_off=eo)
+            sub.pair_range = (b0, b1)
+            parts.append(sub)
+        self._splits[k] = parts
+        return parts
 
     @property
     def n1(self):
@@ -46,9 +81,11 @@ class DeviceBatch:
         """From ``fpm.synth`` pairs (list of (g0, g1) dicts)."""
         B = len(pairs)
         xs, ws, srcs, dsts, pss = [], [], [], [], []
-        ns = []
+        ns, eoffs = [], []
         for side in range(2):
             n = np.array([p[side]["n"] for p in pairs], dtype=np.int32)
+            eoffs.append(torch.from_numpy(np.concatenate(
+                [[0], np.cumsum([p[side]["edge_index"].shape[1] for p in pairs])]).astype(np.int64)))
             nmax = int(n.max())
             X = np.zeros((B, nmax, C.NODE_FEATURE_DIM), np.float32)
             s_l, d_l, p_l = [], [], []
@@ -65,7 +102,7 @@ class DeviceBatch:
             srcs.append(torch.from_numpy(np.concatenate(s_l).astype(np.int32)).to(device))
             dsts.append(torch.from_numpy(np.concatenate(d_l).astype(np.int32)).to(device))
             pss.append(torch.from_numpy(np.concatenate(p_l).astype(np.float32)).to(device).contiguous())
-        return DeviceBatch(B, ns[0], ns[1], xs, ws, srcs, dsts, pss, device)
+        return DeviceBatch(B, ns[0], ns[1], xs, ws, srcs, dsts, pss, device, edge_off=eoffs)
 
     @staticmethod
     def from_data_dict(data_dict, device):
@@ -82,7 +119,7 @@ class DeviceBatch:
                 "pass data_dict['node_features'] and data_dict['global_features']")
         ns = [torch.as_tensor(t).view(-1).to(torch.int32).cpu() for t in data_dict["ns"]]
         B = int(ns[0].numel())
-        xs, ws, srcs, dsts, pss = [], [], [], [], []
+        xs, ws, srcs, dsts, pss, eoffs = [], [], [], [], [], []
         for side in range(2):
             n = ns[side]
             nmax = int(n.max())
@@ -94,10 +131,17 @@ class DeviceBatch:
             ptr = torch.as_tensor(ptr).cpu().long()
             ei = torch.as_tensor(g.edge_index).cpu().long()
             gidx = torch.searchsorted(ptr, ei[0], right=True) - 1
+            if ei.shape[1] and not bool((gidx[1:] >= gidx[:-1]).all()):
+                order = torch.argsort(gidx, stable=True)
+                ei, gidx = ei[:, order], gidx[order]
+                g_attr = torch.as_tensor(g.edge_attr)[order]
+            else:
+                g_attr = torch.as_tensor(g.edge_attr)
+            eoffs.append(torch.cat([torch.zeros(1, dtype=torch.long), torch.bincount(gidx, minlength=B).cumsum(0)]))
             off = gidx * nmax - ptr[gidx]
             srcs.append((ei[0] + off).to(torch.int32).to(device))
             dsts.append((ei[1] + off).to(torch.int32).to(device))
-            pss.append(torch.as_tensor(g.edge_attr).to(torch.float32).to(device).contiguous())
+            pss.append(g_attr.to(torch.float32).to(device).contiguous())
             nf = torch.as_tensor(data_dict["node_features"][side]).to(torch.float32)
             if nf.dim() == 3:
                 X = torch.zeros(B, nmax, nf.shape[-1], dtype=torch.float32, device=nf.device)
@@ -110,4 +154,4 @@ class DeviceBatch:
                     X[b, :int(n[b])] = nf[int(ptr[b]):int(ptr[b + 1])]
             xs.append(X.reshape(B * nmax, -1).to(device).contiguous())
             ws.append(torch.as_tensor(data_dict["global_features"][side]).to(torch.float32).to(device).contiguous())
-        return DeviceBatch(B, ns[0], ns[1], xs, ws, srcs, dsts, pss, device)
+        return DeviceBatch(B, ns[0], ns[1], xs, ws, srcs, dsts, pss, device, edge_off=eoffs)

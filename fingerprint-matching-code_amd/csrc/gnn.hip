@@ -4,9 +4,9 @@
 // torch_sparse mean aggregation over {Kronecker edge pairs} U {diagonal} factorises exactly:
 //   agg[c][d][i] = ( sum_{a in N1(i)} sum_{b in N2(d)} X[c][b][a] + D[d][i] X[c][d][i] )
 //                  / ( deg1(i) deg2(d) + D[d][i] ),   D = [d*n1max + i < n1b*n2b]  (quirk A.10(ii))
-// One workgroup per (graph-2 node d, pair): the rows X[c][b][:] of d's neighbours are summed
-// (coalesced) into LDS, then each thread gathers its i's graph-1 neighbours from LDS and runs the
-// node MLPs: x1 = lin_l(agg) + lin_r(x) + relu(W2 relu(W1 x + b1) + b2), z = classifier(x1).
+// One workgroup per (graph-2 node d, pair), one thread per graph-1 node i: the rows X[c][b][:] of
+// d's neighbours are summed (coalesced) into LDS, then each thread gathers its i's graph-1
+// neighbours from LDS and runs the node MLPs: x1 = lin_l(agg) + lin_r(x) + relu(W2 relu(W1 x + b1) + b2), z = classifier(x1).
 // Layout: X[b][c][d][i] (channel-major, i = graph-1 node fastest), p(i,d) = d*n1max + i.
 #include "fpm_common.h"
 
@@ -20,24 +20,23 @@ struct GnnPack {
 };
 
 template <int C>
-__global__ __launch_bounds__(256) void gnn_layer_kernel(const float* __restrict__ X, int n1max, int n2max,
-                                                        const int* __restrict__ ptr1, const int* __restrict__ nbr1,
-                                                        const int* __restrict__ ptr2, const int* __restrict__ nbr2,
-                                                        const int* __restrict__ n1, const int* __restrict__ n2,
-                                                        const float* __restrict__ prm, float* __restrict__ Xo,
-                                                        float* __restrict__ zbuf) {
+__global__ __launch_bounds__(1024) void gnn_layer_kernel(const float* __restrict__ X, int n1max, int n2max,
+                                                         const int* __restrict__ ptr1, const int* __restrict__ nbr1,
+                                                         const int* __restrict__ ptr2, const int* __restrict__ nbr2,
+                                                         const int* __restrict__ n1, const int* __restrict__ n2,
+                                                         const float* __restrict__ W, float* __restrict__ Xo,
+                                                         float* __restrict__ zbuf) {
+    // one thread per graph-1 node i (blockDim >= n1max): no loop, so the uniform weight loads
+    // stay scalar (s_load, SGPR operands of the FMAs) instead of being hoisted into VGPRs.
     using P = GnnPack<C>;
-    extern __shared__ float lds[];
-    float* W = lds;                       // P::total
-    float* T = lds + ((P::total + 3) & ~3);  // [C][n1max]
+    extern __shared__ float T[];          // [C][n1max]: sum of graph-2 neighbour rows
     __shared__ int nb2[64];
     __shared__ int nnb2;
 
-    const int d = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+    const int d = blockIdx.x, b = blockIdx.y, i = threadIdx.x;
     const long N = (long)n1max * n2max;
     const float* Xb = X + (long)b * C * N;
-    for (int k = tid; k < P::total; k += 256) W[k] = prm[k];
-    if (tid == 0) {
+    if (i == 0) {
         int beg = ptr2[(long)b * n2max + d], end = ptr2[(long)b * n2max + d + 1];
         int n = end - beg;
         if (n > 64) n = 64;   // Delaunay in-degree is far below 64; guarded
@@ -46,62 +45,62 @@ __global__ __launch_bounds__(256) void gnn_layer_kernel(const float* __restrict_
     }
     __syncthreads();
     const int nn2 = nnb2;
-    for (int c = 0; c < C; ++c) {
-        for (int a = tid; a < n1max; a += 256) {
+    if (i < n1max) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
             float s = 0.f;
-            for (int k = 0; k < nn2; ++k) s += Xb[(long)c * N + (long)nb2[k] * n1max + a];
-            T[c * n1max + a] = s;
+            for (int k = 0; k < nn2; ++k) s += Xb[(long)c * N + (long)nb2[k] * n1max + i];
+            T[c * n1max + i] = s;
         }
     }
     __syncthreads();
+    if (i >= n1max) return;
     const int n1b = n1[b], n2b = n2[b];
-    const int deg2 = nn2;
-    for (int i = tid; i < n1max; i += 256) {
-        const long p = (long)d * n1max + i;
-        const int beg = ptr1[(long)b * n1max + i], end = ptr1[(long)b * n1max + i + 1];
-        const bool self = p < (long)n1b * n2b;
-        float x[C], agg[C];
+    const long p = (long)d * n1max + i;
+    const int beg = ptr1[(long)b * n1max + i], end = ptr1[(long)b * n1max + i + 1];
+    const bool self = p < (long)n1b * n2b;
+    float x[C], agg[C];
 #pragma unroll
-        for (int c = 0; c < C; ++c) {
-            x[c] = Xb[(long)c * N + p];
-            agg[c] = 0.f;
-        }
-        for (int e = beg; e < end; ++e) {
-            const int a = nbr1[e];
-#pragma unroll
-            for (int c = 0; c < C; ++c) agg[c] += T[c * n1max + a];
-        }
-        const float cnt = (float)((end - beg) * deg2 + (self ? 1 : 0));
-#pragma unroll
-        for (int c = 0; c < C; ++c) {
-            float v = self ? agg[c] + x[c] : agg[c];
-            agg[c] = cnt > 0.f ? v / cnt : 0.f;
-        }
-        float h[16];
-#pragma unroll
-        for (int m = 0; m < 16; ++m) {
-            float s = W[P::b1 + m];
-#pragma unroll
-            for (int c = 0; c < C; ++c) s += W[P::W1 + m * C + c] * x[c];
-            h[m] = fmaxf(s, 0.f);
-        }
-        float z = 0.f;
-#pragma unroll
-        for (int o = 0; o < 16; ++o) {
-            float l = 0.f, r = 0.f, t = 0.f;
-#pragma unroll
-            for (int c = 0; c < C; ++c) {
-                l += W[P::Wl + o * C + c] * agg[c];
-                r += W[P::Wr + o * C + c] * x[c];
-            }
-#pragma unroll
-            for (int m = 0; m < 16; ++m) t += W[P::W2 + o * 16 + m] * h[m];
-            float x1 = ((l + W[P::bl + o]) + r) + fmaxf(t + W[P::b2 + o], 0.f);
-            Xo[(long)b * 17 * N + (long)o * N + p] = x1;
-            z += W[P::wc + o] * x1;
-        }
-        zbuf[(long)b * N + p] = z + W[P::bc];
+    for (int c = 0; c < C; ++c) {
+        x[c] = Xb[(long)c * N + p];
+        agg[c] = 0.f;
     }
+    for (int e = beg; e < end; ++e) {
+        const int a = nbr1[e];
+#pragma unroll
+        for (int c = 0; c < C; ++c) agg[c] += T[c * n1max + a];
+    }
+    const float cnt = (float)((end - beg) * nn2 + (self ? 1 : 0));
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        float v = self ? agg[c] + x[c] : agg[c];
+        agg[c] = cnt > 0.f ? v / cnt : 0.f;
+    }
+    float h[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        float s = W[P::b1 + m];
+#pragma unroll
+        for (int c = 0; c < C; ++c) s += W[P::W1 + m * C + c] * x[c];
+        h[m] = fmaxf(s, 0.f);
+    }
+    float z = 0.f;
+    float* Xob = Xo + (long)b * 17 * N + p;
+#pragma unroll
+    for (int o = 0; o < 16; ++o) {
+        float l = 0.f, r = 0.f, t = 0.f;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            l += W[P::Wl + o * C + c] * agg[c];
+            r += W[P::Wr + o * C + c] * x[c];
+        }
+#pragma unroll
+        for (int m = 0; m < 16; ++m) t += W[P::W2 + o * 16 + m] * h[m];
+        float x1 = ((l + W[P::bl + o]) + r) + fmaxf(t + W[P::b2 + o], 0.f);
+        Xob[(long)o * N] = x1;
+        z += W[P::wc + o] * x1;
+    }
+    zbuf[(long)b * N + p] = z + W[P::bc];
 }
 
 // v[p] = classifier(emb[p]) (ngm.py:368), written as s[b][i][j] = v[b][j*n1max + i] (ngm.py:369)
@@ -126,17 +125,17 @@ extern "C" int fpm_kron_gnn_layer_fwd(const float* X, int C, int B, int n1max, i
                                       const float* params, float* Xout, float* zbuf, void* stream) {
     FPM_CHECK_ARG(C == 1 || C == 17, "gnn_layer: C must be 1 or 17 (got %d)", C);
     if (B == 0) return 0;
+    FPM_CHECK_ARG(n1max <= 1024, "gnn_layer: n1max must be <= 1024");
     dim3 grid(n2max, B);
+    const int threads = (n1max + 63) / 64 * 64;
     hipStream_t st = (hipStream_t)stream;
-    if (C == 1) {
-        size_t sh = (size_t)(((GnnPack<1>::total + 3) & ~3) + 1 * n1max) * 4;
-        hipLaunchKernelGGL((gnn_layer_kernel<1>), grid, dim3(256), sh, st, X, n1max, n2max, ptr1, nbr1, ptr2, nbr2, n1,
-                           n2, params, Xout, zbuf);
-    } else {
-        size_t sh = (size_t)(((GnnPack<17>::total + 3) & ~3) + 17 * n1max) * 4;
-        hipLaunchKernelGGL((gnn_layer_kernel<17>), grid, dim3(256), sh, st, X, n1max, n2max, ptr1, nbr1, ptr2, nbr2,
+    const size_t sh = (size_t)C * n1max * 4;
+    if (C == 1)
+        hipLaunchKernelGGL((gnn_layer_kernel<1>), grid, dim3(threads), sh, st, X, n1max, n2max, ptr1, nbr1, ptr2, nbr2,
                            n1, n2, params, Xout, zbuf);
-    }
+    else
+        hipLaunchKernelGGL((gnn_layer_kernel<17>), grid, dim3(threads), sh, st, X, n1max, n2max, ptr1, nbr1, ptr2,
+                           nbr2, n1, n2, params, Xout, zbuf);
     return fpm::check_launch("fpm_kron_gnn_layer_fwd");
 }
 

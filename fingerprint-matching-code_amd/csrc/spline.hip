@@ -51,34 +51,48 @@ PlanLayout plan_layout(long E, long num_nodes, long max_tiles) {
     return L;
 }
 
-__global__ void plan_count_kernel(const int* __restrict__ src, const int* __restrict__ dst,
-                                  const float* __restrict__ pseudo, long E, int* cnt, int* slot, int* dslot,
-                                  int* gidx, int* indeg, float* basis_tmp) {
-    long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= E) return;
-    // torch-spline-conv basis, open spline degree 1: v = u * (kernel - 1), frac, floor
-    float b4[4];
-    int f[2];
-    float fr[2];
+// per-edge basis + group; slots within a group come from a block-local LDS histogram plus one
+// global atomic per (block, group) (25 global counters would otherwise serialise 1.5M atomics)
+__global__ __launch_bounds__(256) void plan_count_kernel(const int* __restrict__ src, const int* __restrict__ dst,
+                                                         const float* __restrict__ pseudo, long E, int* cnt, int* slot,
+                                                         int* dslot, int* gidx, int* indeg, float* basis_tmp) {
+    __shared__ int lcnt[32], lbase[32];
+    if (threadIdx.x < 32) lcnt[threadIdx.x] = 0;
+    __syncthreads();
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    int g = -1, lslot = 0;
+    if (e < E) {
+        // torch-spline-conv basis, open spline degree 1: v = u * (kernel - 1), frac, floor
+        int f[2];
+        float fr[2];
 #pragma unroll
-    for (int d = 0; d < 2; ++d) {
-        float v = pseudo[2 * e + d] * 4.0f;
-        float fl = floorf(v);
-        f[d] = (int)fl;
-        fr[d] = v - fl;
-    }
+        for (int d = 0; d < 2; ++d) {
+            float v = pseudo[2 * e + d] * 4.0f;
+            float fl = floorf(v);
+            f[d] = (int)fl;
+            fr[d] = v - fl;
+        }
+        float b4[4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        float b = 1.0f;
-        b = b * ((s & 1) ? fr[0] : 1.0f - fr[0]);
-        b = b * ((s >> 1) ? fr[1] : 1.0f - fr[1]);
-        b4[s] = b;
+        for (int s = 0; s < 4; ++s) {
+            float b = 1.0f;
+            b = b * ((s & 1) ? fr[0] : 1.0f - fr[0]);
+            b = b * ((s >> 1) ? fr[1] : 1.0f - fr[1]);
+            b4[s] = b;
+        }
+        g = f[0] + 5 * f[1];
+        gidx[e] = g;
+        lslot = atomicAdd(&lcnt[g], 1);
+        dslot[e] = atomicAdd(&indeg[dst[e]], 1);
+        *(float4*)(basis_tmp + 4 * e) = make_float4(b4[0], b4[1], b4[2], b4[3]);
     }
-    int g = f[0] + 5 * f[1];
-    gidx[e] = g;
-    slot[e] = atomicAdd(&cnt[g], 1);
-    dslot[e] = atomicAdd(&indeg[dst[e]], 1);
-    *(float4*)(basis_tmp + 4 * e) = make_float4(b4[0], b4[1], b4[2], b4[3]);
+    __syncthreads();
+    if (threadIdx.x < 25) {
+        int c = lcnt[threadIdx.x];
+        lbase[threadIdx.x] = c ? atomicAdd(&cnt[threadIdx.x], c) : 0;
+    }
+    __syncthreads();
+    if (e < E) slot[e] = lbase[g] + lslot;
 }
 
 __global__ __launch_bounds__(1024) void plan_scan_kernel(const int* cnt, int* grp_off, int* tile_info,
@@ -142,6 +156,26 @@ __global__ void plan_fill_kernel(const int* __restrict__ src, const int* __restr
     int p = dst_ptr[d] + dslot[e];
     dst_rows[p] = row;
     nbr_local[p] = s % nmax;
+}
+
+// Deterministic in-edge order per node (ascending source): the atomics above fill each list in
+// arbitrary order, and the GNN aggregation sums over these lists in fp32.
+__global__ void plan_sort_kernel(const int* __restrict__ dst_ptr, long num_nodes, int* __restrict__ dst_rows,
+                                 int* __restrict__ nbr_local) {
+    long v = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= num_nodes) return;
+    const int beg = dst_ptr[v], end = dst_ptr[v + 1];
+    for (int a = beg + 1; a < end; ++a) {
+        int kn = nbr_local[a], kr = dst_rows[a];
+        int b = a - 1;
+        while (b >= beg && nbr_local[b] > kn) {
+            nbr_local[b + 1] = nbr_local[b];
+            dst_rows[b + 1] = dst_rows[b];
+            --b;
+        }
+        nbr_local[b + 1] = kn;
+        dst_rows[b + 1] = kr;
+    }
 }
 
 // out[v] = max_{in-edges} msg + root[v] + bias  -> RELU: relu(.) ; RESID: x[v] + 0.1 * (.)
@@ -222,6 +256,8 @@ extern "C" int fpm_spline_plan(const int* src, const int* dst, const float* pseu
                        (const int*)(w + L.slot), (const int*)(w + L.dslot), (const int*)(w + L.gidx),
                        (const int*)(w + L.dst_ptr), (const float*)basis_tmp, (int*)(w + L.rows_src),
                        (float*)(w + L.rows_basis), (int*)(w + L.dst_rows), (int*)(w + L.nbr_local));
+    hipLaunchKernelGGL(plan_sort_kernel, dim3((unsigned)((num_nodes + 255) / 256)), dim3(256), 0, st,
+                       (const int*)(w + L.dst_ptr), num_nodes, (int*)(w + L.dst_rows), (int*)(w + L.nbr_local));
     return fpm::check_launch("fpm_spline_plan");
 }
 

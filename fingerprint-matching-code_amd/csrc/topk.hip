@@ -52,13 +52,11 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
     for (int w = 1; w < 16; ++w) { mn = fminf(mn, sa[w]); mx = fmaxf(mx, sb_[w]); }
     __syncthreads();
 
-    // dist_mat = -|s - anchor| (soft_topk.py:28-29), then Sinkhorn_m divides by tau (:180)
-    float d0[NQ], d1[NQ];
-#pragma unroll
-    for (int k = 0; k < NQ; ++k) {
-        d0[k] = (-fabsf(s[k] - mn)) / tau;
-        d1[k] = (-fabsf(s[k] - mx)) / tau;
-    }
+    // dist_mat = -|s - anchor| (soft_topk.py:28-29), then Sinkhorn_m divides by tau (:180);
+    // recomputed from s on every pass (keeps 64 values per thread resident instead of 128)
+    const float rtau = tau;
+#define D0(k) ((-fabsf(s[k] - mnl)) / rtau)
+#define D1(k) ((-fabsf(s[k] - mxl)) / rtau)
     const float kk = kvec[b];
     const float lcp0 = logf((float)N - kk);   // log(col_prob[:,0]) = log(n1*n2 - k)
     const float lcp1 = logf(kk);              // log(col_prob[:,1]) = log(k)
@@ -68,8 +66,15 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
     float vu0 = 0.f, vu1 = 0.f, lse0 = 0.f, lse1 = 0.f;
     int last = 0;   // 0: none, 1: row, 2: column
 
-    auto Lpair = [&](int k, float& L0, float& L1) {
-        float a0 = d0[k] - vu0, a1 = d1[k] - vu1;
+    // opaque copies of the anchors: stops the compiler from hoisting the 2*NQ distances out of
+    // the iteration loop (that would need 128 more VGPRs and spill)
+    auto anchors = [&](float& lo, float& hi) {
+        lo = mn;
+        hi = mx;
+        asm volatile("" : "+v"(lo), "+v"(hi));
+    };
+    auto Lpair = [&](int k, float mnl, float mxl, float& L0, float& L1) {
+        float a0 = D0(k) - vu0, a1 = D1(k) - vu1;
         float u = urow(a0, a1);
         L0 = a0 - u;
         L1 = a1 - u;
@@ -89,12 +94,14 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
         last = 1;
     };
     auto colstep = [&]() {   // always follows a row step
+        float mnl, mxl;
+        anchors(mnl, mxl);
         float m0 = -INFINITY, m1 = -INFINITY;
 #pragma unroll
         for (int k = 0; k < NQ; ++k) {
             if (tid + 1024 * k < N) {
                 float L0, L1;
-                Lpair(k, L0, L1);
+                Lpair(k, mnl, mxl, L0, L1);
                 m0 = fmaxf(m0, L0);
                 m1 = fmaxf(m1, L1);
             }
@@ -107,11 +114,12 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
         for (int w = 1; w < 16; ++w) { m0 = fmaxf(m0, sa[w]); m1 = fmaxf(m1, sb_[w]); }
         __syncthreads();
         float a0 = 0.f, a1 = 0.f;
+        anchors(mnl, mxl);   // fresh opaque anchors: recompute L instead of keeping 2*NQ values live
 #pragma unroll
         for (int k = 0; k < NQ; ++k) {
             if (tid + 1024 * k < N) {
                 float L0, L1;
-                Lpair(k, L0, L1);
+                Lpair(k, mnl, mxl, L0, L1);
                 if (m0 != -INFINITY) a0 += expf(L0 - m0);
                 if (m1 != -INFINITY) a1 += expf(L1 - m1);
             }
@@ -128,12 +136,14 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
         last = 2;
     };
     auto any_pos = [&]() -> bool {
+        float mnl, mxl;
+        anchors(mnl, mxl);
         int flag = 0;
 #pragma unroll
         for (int k = 0; k < NQ; ++k) {
             if (tid + 1024 * k < N) {
                 float L0, L1;
-                Lpair(k, L0, L1);
+                Lpair(k, mnl, mxl, L0, L1);
                 flag |= (L0 > 0.f) | (L1 > 0.f);
             }
         }
@@ -159,20 +169,26 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
 
     // ds_mat[i][j] = exp(L[q(i,j), 1]) on the valid block, 0 elsewhere
     float* O = out + (long)b * ob;
+    float mnl, mxl;
+    anchors(mnl, mxl);
     for (int idx = tid; idx < n1max * n2max; idx += 1024) {
         int i = idx / n2max, j = idx - i * n2max;
         if (i >= n1b || j >= n2b) O[i * old_ + j] = 0.f;
     }
+    int n2o = n2b;
+    asm volatile("" : "+v"(n2o));   // recompute (i, j) here rather than keep NQ addresses live
 #pragma unroll
     for (int k = 0; k < NQ; ++k) {
         int q = tid + 1024 * k;
         if (q < N) {
-            int i = q / n2b, j = q - i * n2b;
+            int i = q / n2o, j = q - i * n2o;
             float L0, L1;
-            Lpair(k, L0, L1);
+            Lpair(k, mnl, mxl, L0, L1);
             O[i * old_ + j] = expf(L1);
         }
     }
+#undef D0
+#undef D1
 }
 
 // Greedy top-k over Hungarian matches: prod = x * ds; argsort(prod, desc); accept (r,c) while

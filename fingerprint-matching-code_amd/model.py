@@ -47,7 +47,7 @@ def _build_tree(root, sd):
 
 
 class Net(nn.Module):
-    def __init__(self, regression=False, dtype="f32", seed=0, lsa_threads=None):
+    def __init__(self, regression=False, dtype="f32", seed=0, lsa_threads=None, chunks=None):
         super().__init__()
         _build_tree(self, P.init_params(seed))
         self.regression = regression
@@ -59,6 +59,7 @@ class Net(nn.Module):
             raise ValueError("dtype must be 'f32' or 'bf16'")
         self.dtype_mode = dtype
         self.lsa_threads = lsa_threads or max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16")), len(os.sched_getaffinity(0))))
+        self.chunks = chunks
         self._pack = None
         self._pack_key = None
         self._pinned = None
@@ -201,7 +202,7 @@ class Net(nn.Module):
             self.stage_times[name] = self.stage_times.get(name, 0.0) + (t - self._t_last)
             self._t_last = t
 
-    def run_gpu_stage(self, bt, keep_feats=False):
+    def run_gpu_stage(self, bt, keep_feats=False, s_out=None, ss_out=None):
         """Everything up to ds_mat on the GPU.  Returns a dict of device tensors."""
         self._keep_feats = keep_feats
         if self._stage_timing:
@@ -240,9 +241,9 @@ class Net(nn.Module):
                          out=Xn[:, 16].transpose(1, 2))
             X, Cin = Xn, 17
             self._mark("gnn%d" % l)
-        s = torch.empty(B, n1max, n2max, device=dev, dtype=torch.float32)
+        s = s_out if s_out is not None else torch.empty(B, n1max, n2max, device=dev, dtype=torch.float32)
         ops.node_classifier(X, B, n1max, n2max, wp["cls_w"], wp["cls_b"], s)
-        ss = ops.sinkhorn(s, bt.n1, bt.n2, C.SK_ITER_NUM, self.tau, True)
+        ss = ops.sinkhorn(s, bt.n1, bt.n2, C.SK_ITER_NUM, self.tau, True, out=ss_out)
         self._mark("final_sinkhorn")
         out = dict(s=s, ss=ss, Kp=Kp[:, 0].transpose(1, 2), coef=coef)
         if keep_feats:
@@ -250,48 +251,86 @@ class Net(nn.Module):
         return out
 
     # ------------------------------------------------------------------------------------------
-    def run(self, bt, gt_perm=None, label=None, keep_feats=False):
+    def pipeline_chunks(self, B):
+        """Sub-batches per forward so the host Hungarian of chunk c overlaps the GPU work of c+1."""
+        if self.chunks is not None:
+            return max(1, min(self.chunks, B))
+        return max(1, min(8, B // 128))
+
+    def run(self, bt, gt_perm=None, label=None, keep_feats=False, chunks=None):
+        """Full forward.  The GPU stage of every chunk is queued at once on the stream; the host
+        LSA of chunk c starts as soon as its ds_mat lands in pinned memory, while the GPU keeps
+        going with the next chunks; the selection + classifier of chunk c follow its LSA."""
         dev = bt.device
         B, n1max, n2max = bt.B, bt.n1max, bt.n2max
+        K = chunks if chunks is not None else self.pipeline_chunks(B)
+        parts = bt.split(K)
         t0 = time.perf_counter()
-        out = self.run_gpu_stage(bt, keep_feats)
-        s, ss = out["s"], out["ss"]
         min_pt = torch.minimum(bt.n1, bt.n2).to(torch.float32)
         if gt_perm is None:
             gt_ks = min_pt.clone()     # synthetic pairs: identity ground truth
         else:
             gt_ks = torch.as_tensor(gt_perm).to(dev).reshape(B, -1).sum(-1).to(torch.float32)
-        if self.regression:
-            ks = self._afau(self.packed(dev), ss, bt)
-        else:
-            ks = gt_ks / min_pt
-        self._mark("afau")
-        k_used = gt_ks if self.training else ks * min_pt
+        f32 = dict(device=dev, dtype=torch.float32)
+        s = torch.empty(B, n1max, n2max, **f32)
+        ss = torch.empty(B, n1max, n2max, **f32)
+        ds = torch.empty(B, n1max, n2max, **f32)
+        perm = torch.empty(B, n1max, n2max, **f32)
+        lsa = torch.empty(B, n1max, n2max, **f32)
+        ks = torch.empty(B, **f32)
+        logits = torch.empty(B, **f32)
+        prob = torch.empty(B, **f32)
         steps = torch.empty(B, device=dev, dtype=torch.int32)
-        ds = ops.soft_topk(ss, bt.n1, bt.n2, k_used.contiguous(), C.SK_ITER_NUM, self.tau, steps=steps)
-        self._mark("soft_topk")
-        # Hungarian on host threads (utils/hungarian.py): D2H ds_mat, LSA, H2D assignment
         if self._pinned is None or self._pinned.shape != ds.shape:
             self._pinned = torch.empty(ds.shape, dtype=torch.float32, pin_memory=True)
-        ds_host = self._pinned
-        ds_host.copy_(ds, non_blocking=True)
-        torch.cuda.current_stream(dev).synchronize()
-        t1 = time.perf_counter()
-        assign = ops.lsa_batch_host(ds_host, bt.n_host[0], bt.n_host[1], self.lsa_threads)
-        t2 = time.perf_counter()
-        assign_d = assign.to(dev, non_blocking=True)
-        lsa = torch.empty(B, n1max, n2max, device=dev, dtype=torch.float32)
+        host = self._pinned
+        stream = torch.cuda.current_stream(dev)
+        ev_start = torch.cuda.Event(enable_timing=True)
+        ev_start.record(stream)
+        outs, events = [], []
+        for part in parts:
+            b0, b1 = getattr(part, "pair_range", (0, B))
+            o = self.run_gpu_stage(part, keep_feats, s_out=s[b0:b1], ss_out=ss[b0:b1])
+            if self.regression:
+                ks[b0:b1] = self._afau(self.packed(dev), ss[b0:b1], part)
+            else:
+                ks[b0:b1] = gt_ks[b0:b1] / min_pt[b0:b1]
+            self._mark("afau")
+            k_used = gt_ks[b0:b1] if self.training else ks[b0:b1] * min_pt[b0:b1]
+            ops.soft_topk(ss[b0:b1], part.n1, part.n2, k_used.contiguous(), C.SK_ITER_NUM, self.tau,
+                          out=ds[b0:b1], steps=steps[b0:b1])
+            self._mark("soft_topk")
+            host[b0:b1].copy_(ds[b0:b1], non_blocking=True)
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(stream)
+            events.append(ev)
+            outs.append(o)
+        t_lsa = 0.0
+        t_first = None
         kk = (ks * min_pt).contiguous()
-        perm = ops.topk_select(ds, assign_d, kk, lsa_out=lsa)
-        self._mark("lsa+h2d+select")
-        logits, prob = ops.match_cls(s, perm, self._pack["mc_w1"], self._pack["mc_b1"], self._pack["mc_sc1"],
-                                     self._pack["mc_sh1"], self._pack["mc_w2"], self._pack["mc_b2"],
-                                     self._pack["mc_sc2"], self._pack["mc_sh2"], self._pack["mc_fcw"],
-                                     self._pack["mc_fcb"])
-        self._mark("match_cls")
-        res = dict(out)
-        res.update(ds_mat=ds, perm_mat=perm, k_prob=ks, cls_prob=prob, cls_logits=logits, lsa=lsa,
+        wp = self._pack
+        for part, ev in zip(parts, events):
+            b0, b1 = getattr(part, "pair_range", (0, B))
+            ev.synchronize()
+            if t_first is None:
+                t_first = time.perf_counter()
+            t = time.perf_counter()
+            # Hungarian on host threads (utils/hungarian.py): LSA of -ds_mat per pair
+            assign = ops.lsa_batch_host(host[b0:b1], part.n_host[0], part.n_host[1], self.lsa_threads)
+            t_lsa += time.perf_counter() - t
+            assign_d = assign.to(dev, non_blocking=True)
+            ops.topk_select(ds[b0:b1], assign_d, kk[b0:b1], lsa_out=lsa[b0:b1], out=perm[b0:b1])
+            self._mark("lsa+h2d+select")
+            ops.match_cls(s[b0:b1], perm[b0:b1], wp["mc_w1"], wp["mc_b1"], wp["mc_sc1"], wp["mc_sh1"], wp["mc_w2"],
+                          wp["mc_b2"], wp["mc_sc2"], wp["mc_sh2"], wp["mc_fcw"], wp["mc_fcb"],
+                          logits=logits[b0:b1], prob=prob[b0:b1])
+            self._mark("match_cls")
+        res = dict(s=s, ss=ss, ds_mat=ds, perm_mat=perm, k_prob=ks, cls_prob=prob, cls_logits=logits, lsa=lsa,
                    sk_steps=steps)
+        if len(outs) == 1 or keep_feats:
+            for k in outs[0]:
+                if k not in ("s", "ss"):
+                    res[k] = outs[0][k] if len(outs) == 1 else torch.cat([o[k] for o in outs])
         if label is not None:
             res["cls_loss"] = F.binary_cross_entropy_with_logits(logits, torch.as_tensor(label).to(dev).view(-1).float())
         else:
@@ -303,7 +342,9 @@ class Net(nn.Module):
         else:
             res["ks_loss"] = 0.0
             res["ks_error"] = 0.0
-        self.last_timing = dict(gpu_stage_s=t1 - t0, lsa_s=t2 - t1)
+        # GPU time of the stage before the Hungarian (all chunks), from events on the stream
+        self.last_timing = dict(gpu_stage_s=ev_start.elapsed_time(events[-1]) / 1e3, lsa_s=t_lsa,
+                                first_chunk_wait_s=(t_first or t0) - t0, chunks=len(parts))
         return res
 
     def forward(self, data_dict, regression=True):

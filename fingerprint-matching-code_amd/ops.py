@@ -62,10 +62,10 @@ def soft_topk(ss, n1, n2, k, iters=10, tau=0.01, out=None, steps=None):
     return out
 
 
-def topk_select(ds, assign, k, lsa_out=None):
+def topk_select(ds, assign, k, lsa_out=None, out=None):
     _dev(ds, assign, k)
     B, n1max, n2max = ds.shape
-    perm = torch.empty(B, n1max, n2max, device=ds.device, dtype=torch.float32)
+    perm = out if out is not None else torch.empty(B, n1max, n2max, device=ds.device, dtype=torch.float32)
     _lib.call("fpm_topk_select", _p(ds), ds.stride(0), ds.stride(1), _p(assign), assign.stride(0), _p(k), B,
               n1max, n2max, _p(perm), perm.stride(0), perm.stride(1), _p(lsa_out),
               lsa_out.stride(0) if lsa_out is not None else 0, lsa_out.stride(1) if lsa_out is not None else 0,
@@ -160,13 +160,15 @@ def afau_head(gr, gc, B, E, r0w, r0b, r2w, r2b, c0w, c0b, c2w, c2b, ks):
               _p(c2w), _p(c2b), _p(ks), _stream(gr))
 
 
-def match_cls(s, perm, w1, b1, bn1_sc, bn1_sh, w2, b2, bn2_sc, bn2_sh, fcw, fcb):
+def match_cls(s, perm, w1, b1, bn1_sc, bn1_sh, w2, b2, bn2_sc, bn2_sh, fcw, fcb, logits=None, prob=None):
     _dev(s, perm)
+    if not (s.is_contiguous() and perm.is_contiguous()):
+        raise _lib.FpmError("match_cls: s and perm must be contiguous")
     B, H, W = s.shape
     nws = _lib.load().fpm_match_cls_ws_floats(B, H, W)
     ws = torch.empty(max(int(nws), 1), device=s.device, dtype=torch.float32)
-    logits = torch.empty(B, device=s.device, dtype=torch.float32)
-    prob = torch.empty(B, device=s.device, dtype=torch.float32)
+    logits = logits if logits is not None else torch.empty(B, device=s.device, dtype=torch.float32)
+    prob = prob if prob is not None else torch.empty(B, device=s.device, dtype=torch.float32)
     _lib.call("fpm_match_cls_fwd", _p(s), _p(perm), B, H, W, _p(w1), _p(b1), _p(bn1_sc), _p(bn1_sh), _p(w2), _p(b2),
               _p(bn2_sc), _p(bn2_sh), _p(fcw), _p(fcb), _p(ws), _p(logits), _p(prob), _stream(s))
     return logits, prob

@@ -207,3 +207,22 @@ def test_forward_data_dict_surface(sd):
     assert (out["ds_mat"].cpu() - ref["ds_mat"]).abs().max() < 1e-4
     assert abs(float(out["ks_loss"]) - float(ref["ks_loss"])) < 1e-3
     assert abs(float(out["cls_loss"]) - float(ref["cls_loss"])) < 1e-4
+
+
+def test_chunked_pipeline_bitwise(sd):
+    """Pipelined sub-batches (host LSA of chunk c overlapping GPU work of c+1) give bit-identical
+    outputs to the single-chunk forward; the same property makes pair-sharding across GPUs exact."""
+    pairs = synth.make_batch(9, 7, 48, n2=[48, 40, 44, 48, 30, 48, 47])
+    net = fpm.Net(regression=True, dtype="bf16")
+    net.load_state_dict(sd)
+    bt = DeviceBatch.from_pairs(pairs, DEV)
+    a = net.run(bt, chunks=1)
+    b = net.run(bt, chunks=3)
+    for k in ("s", "ss", "ds_mat", "perm_mat", "k_prob", "cls_prob"):
+        assert torch.equal(a[k], b[k]), k
+    # a shard computed alone (as another rank would) equals its slice of the full batch
+    sub = DeviceBatch.from_pairs(pairs[2:5], DEV)
+    sub.nmax = list(bt.nmax)
+    c = net.run(sub, chunks=1)
+    for k in ("ds_mat", "perm_mat", "k_prob"):
+        assert torch.equal(c[k], a[k][2:5]), k
