@@ -46,12 +46,20 @@ __global__ __launch_bounds__(1024) void gnn_layer_kernel(const float* __restrict
     __syncthreads();
     const int nn2 = nnb2;
     if (i < n1max) {
+        // neighbour-outer, channel-inner: C independent loads in flight per neighbour row
+        float acc[C];
 #pragma unroll
-        for (int c = 0; c < C; ++c) {
-            float s = 0.f;
-            for (int k = 0; k < nn2; ++k) s += Xb[(long)c * N + (long)nb2[k] * n1max + i];
-            T[c * n1max + i] = s;
+        for (int c = 0; c < C; ++c) acc[c] = 0.f;
+        for (int k = 0; k < nn2; ++k) {
+            const float* row = Xb + (long)nb2[k] * n1max + i;
+            float v[C];
+#pragma unroll
+            for (int c = 0; c < C; ++c) v[c] = row[(long)c * N];
+#pragma unroll
+            for (int c = 0; c < C; ++c) acc[c] += v[c];
         }
+#pragma unroll
+        for (int c = 0; c < C; ++c) T[c * n1max + i] = acc[c];
     }
     __syncthreads();
     if (i >= n1max) return;

@@ -9,6 +9,7 @@
 // double from the float32 input (-s), as scipy converts its input to float64.
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -75,6 +76,147 @@ int lsap_solve(int nr, int nc, const double* cost, std::vector<int>& col4row) {
     return 0;
 }
 
+// ---- vectorised form of the same algorithm ------------------------------------------------------
+// The remaining columns are kept as structure-of-arrays in the scan order (rc = column id, rs =
+// its shortest-path cost, rp = its path row, rv = v[col], ru = column unassigned), so the scan is
+// contiguous except for the cost-row gather.  The tie rule of the scalar loop -- index updates on
+// spc < lowest, or spc == lowest on an unassigned column -- selects: the last unassigned column
+// holding the minimum if there is one, else the first column holding it.  Both forms are the same
+// function of the scan order, and the reduced costs are evaluated with the same operation order
+// ((minVal + c) - u_i) - v_j, so the result is bit-identical to lsap_solve.
+#if defined(__x86_64__)
+#include <immintrin.h>
+
+__attribute__((target("avx2"))) int lsap_solve_avx2(int nr, int nc, const double* cost, std::vector<int>& col4row) {
+    std::vector<double> u(nr, 0.0), v(nc, 0.0), spc(nc);
+    std::vector<int> path(nc, -1), row4col(nc, -1);
+    std::vector<char> SR(nr), SC(nc);
+    const int ncp = (nc + 3) & ~3;
+    std::vector<int> rc(ncp), rp(ncp), ru(ncp);
+    std::vector<double> rs(ncp), rv(ncp);
+    col4row.assign(nr, -1);
+    for (int cur = 0; cur < nr; ++cur) {
+        double minVal = 0.0;
+        int i = cur;
+        int num = nc;
+        for (int it = 0; it < nc; ++it) {
+            const int j = nc - it - 1;
+            rc[it] = j;
+            rs[it] = INFINITY;
+            rp[it] = -1;
+            rv[it] = v[j];
+            ru[it] = row4col[j] == -1 ? -1 : 0;
+        }
+        std::fill(SR.begin(), SR.end(), 0);
+        std::fill(SC.begin(), SC.end(), 0);
+        int sink = -1;
+        while (sink == -1) {
+            SR[i] = 1;
+            const double* crow = cost + (long)i * nc;
+            const double ui = u[i];
+            const __m256d vmin = _mm256_set1_pd(minVal), vui = _mm256_set1_pd(ui);
+            const __m128i vi = _mm_set1_epi32(i);
+            __m256d vlow = _mm256_set1_pd(INFINITY);
+            int it = 0;
+            for (; it + 4 <= num; it += 4) {
+                __m128i cols = _mm_loadu_si128((const __m128i*)&rc[it]);
+                __m256d c = _mm256_i32gather_pd(crow, cols, 8);
+                __m256d r = _mm256_sub_pd(_mm256_sub_pd(_mm256_add_pd(vmin, c), vui), _mm256_loadu_pd(&rv[it]));
+                __m256d sv = _mm256_loadu_pd(&rs[it]);
+                __m256d lt = _mm256_cmp_pd(r, sv, _CMP_LT_OQ);
+                sv = _mm256_blendv_pd(sv, r, lt);
+                _mm256_storeu_pd(&rs[it], sv);
+                __m128i m32 = _mm256_cvtpd_epi32(lt);   // all-ones -> -1 lanes? use movemask instead
+                (void)m32;
+                int mk = _mm256_movemask_pd(lt);
+                if (mk) {
+                    for (int q = 0; q < 4; ++q)
+                        if (mk & (1 << q)) rp[it + q] = i;
+                }
+                vlow = _mm256_min_pd(vlow, sv);
+            }
+            (void)vi;
+            double lowest;
+            {
+                double t[4];
+                _mm256_storeu_pd(t, vlow);
+                lowest = std::min(std::min(t[0], t[1]), std::min(t[2], t[3]));
+            }
+            for (; it < num; ++it) {
+                const double r = minVal + crow[rc[it]] - ui - rv[it];
+                if (r < rs[it]) {
+                    rs[it] = r;
+                    rp[it] = i;
+                }
+                if (rs[it] < lowest) lowest = rs[it];
+            }
+            if (lowest == INFINITY) return -1;
+            // first position holding the minimum, last unassigned one holding it
+            int first = -1, lastu = -1;
+            {
+                const __m256d vl = _mm256_set1_pd(lowest);
+                int q = 0;
+                for (; q + 4 <= num; q += 4) {
+                    int mk = _mm256_movemask_pd(_mm256_cmp_pd(_mm256_loadu_pd(&rs[q]), vl, _CMP_EQ_OQ));
+                    if (mk) {
+                        for (int b = 0; b < 4; ++b)
+                            if (mk & (1 << b)) {
+                                if (first < 0) first = q + b;
+                                if (ru[q + b]) lastu = q + b;
+                            }
+                    }
+                }
+                for (; q < num; ++q)
+                    if (rs[q] == lowest) {
+                        if (first < 0) first = q;
+                        if (ru[q]) lastu = q;
+                    }
+            }
+            const int index = lastu >= 0 ? lastu : first;
+            minVal = lowest;
+            const int j = rc[index];
+            spc[j] = rs[index];
+            path[j] = rp[index];
+            if (row4col[j] == -1) sink = j;
+            else i = row4col[j];
+            SC[j] = 1;
+            --num;
+            rc[index] = rc[num];
+            rs[index] = rs[num];
+            rp[index] = rp[num];
+            rv[index] = rv[num];
+            ru[index] = ru[num];
+        }
+        u[cur] += minVal;
+        for (int r = 0; r < nr; ++r)
+            if (SR[r] && r != cur) u[r] += minVal - spc[col4row[r]];
+        for (int c = 0; c < nc; ++c)
+            if (SC[c]) v[c] -= minVal - spc[c];
+        int j = sink;
+        while (true) {
+            const int r = path[j];
+            row4col[j] = r;
+            std::swap(col4row[r], j);
+            if (r == cur) break;
+        }
+    }
+    return 0;
+}
+#endif
+
+bool use_avx2() {
+#if defined(__x86_64__)
+    static int ok = -1;
+    if (ok < 0) {
+        const char* e = getenv("FPM_LSA_SCALAR");
+        ok = (e && e[0] == '1') ? 0 : (__builtin_cpu_supports("avx2") ? 1 : 0);
+    }
+    return ok == 1;
+#else
+    return false;
+#endif
+}
+
 // one pair: s (ld stride) block [n1 x n2], maximise s  ->  assign[r] = col or -1
 int lsa_pair(const float* s, long ld, int n1, int n2, int* assign, int n1max) {
     for (int r = 0; r < n1max; ++r) assign[r] = -1;
@@ -92,7 +234,11 @@ int lsa_pair(const float* s, long ld, int n1, int n2, int* assign, int n1max) {
     for (size_t k = 0; k < cost.size(); ++k)
         if (cost[k] != cost[k] || cost[k] == -INFINITY) return -2;   // invalid (scipy raises)
     std::vector<int> c4r;
+#if defined(__x86_64__)
+    int rc = use_avx2() ? lsap_solve_avx2(nr, nc, cost.data(), c4r) : lsap_solve(nr, nc, cost.data(), c4r);
+#else
     int rc = lsap_solve(nr, nc, cost.data(), c4r);
+#endif
     if (rc) return rc;
     if (!tr) {
         for (int i = 0; i < nr; ++i) assign[i] = c4r[i];

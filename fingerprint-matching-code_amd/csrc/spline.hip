@@ -99,6 +99,7 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(const int* cnt, int* gr
                                                          int max_tiles, const int* indeg, int* dst_ptr,
                                                          long num_nodes) {
     __shared__ int part[1024];
+    __shared__ int tilebuf[16384];
     __shared__ int ntile_total;
     const int tid = threadIdx.x;
     if (tid == 0) {
@@ -121,25 +122,39 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(const int* cnt, int* gr
         tile_info[2 * t] = -1;
         tile_info[2 * t + 1] = 0;
     }
-    // exclusive scan of indeg -> dst_ptr
-    long chunk = (num_nodes + 1023) / 1024;
-    long lo = tid * chunk, hi = lo + chunk < num_nodes ? lo + chunk : num_nodes;
-    int s = 0;
-    for (long i = lo; i < hi; ++i) s += indeg[i];
-    part[tid] = s;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {
-        int v = tid >= o ? part[tid - o] : 0;
+    // exclusive scan of indeg -> dst_ptr, tiled through LDS (coalesced global reads/writes)
+    constexpr int TILE = 16384, PER = TILE / 1024;
+    int* buf = tilebuf;
+    int carry = 0;
+    for (long t0 = 0; t0 < num_nodes; t0 += TILE) {
+        const int len = (int)(num_nodes - t0 < TILE ? num_nodes - t0 : TILE);
+        for (int k = tid; k < TILE; k += 1024) buf[k] = k < len ? indeg[t0 + k] : 0;
         __syncthreads();
-        part[tid] += v;
+        int loc[PER];
+        int s = 0;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            loc[k] = s;
+            s += buf[tid * PER + k];
+        }
+        part[tid] = s;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {
+            int v = tid >= o ? part[tid - o] : 0;
+            __syncthreads();
+            part[tid] += v;
+            __syncthreads();
+        }
+        const int base = carry + part[tid] - s;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) buf[tid * PER + k] = base + loc[k];
+        const int total = part[1023];
+        __syncthreads();
+        for (int k = tid; k < len; k += 1024) dst_ptr[t0 + k] = buf[k];
+        carry += total;
         __syncthreads();
     }
-    int run = part[tid] - s;
-    for (long i = lo; i < hi; ++i) {
-        dst_ptr[i] = run;
-        run += indeg[i];
-    }
-    if (tid == 1023) dst_ptr[num_nodes] = part[1023];
+    if (tid == 0) dst_ptr[num_nodes] = carry;
 }
 
 __global__ void plan_fill_kernel(const int* __restrict__ src, const int* __restrict__ dst, long E, int nmax,

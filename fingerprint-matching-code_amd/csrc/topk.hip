@@ -30,7 +30,12 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
     const int N = n1b * n2b;
     const float* S = ss + (long)b * sb;
 
-    float s[NQ];
+    // values k < NQR stay in VGPRs, the rest in LDS (keeps the 1024-thread block under 128 VGPRs)
+    constexpr int NQR = NQ < 32 ? NQ : 32;
+    constexpr int NQL = NQ - NQR;
+    __shared__ float sl[NQL > 0 ? NQL * 1024 : 1];
+    float sr[NQR];
+#define SVAL(k) ((k) < NQR ? sr[(k) < NQR ? (k) : 0] : sl[((k) >= NQR ? (k) - NQR : 0) * 1024 + tid])
     float mn = INFINITY, mx = -INFINITY;
 #pragma unroll
     for (int k = 0; k < NQ; ++k) {
@@ -42,7 +47,8 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
             mn = fminf(mn, v);
             mx = fmaxf(mx, v);
         }
-        s[k] = v;
+        if (k < NQR) sr[k < NQR ? k : 0] = v;
+        else sl[(k >= NQR ? k - NQR : 0) * 1024 + tid] = v;
     }
     mn = -fpm::warp_max(-mn);
     mx = fpm::warp_max(mx);
@@ -55,8 +61,15 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
     // dist_mat = -|s - anchor| (soft_topk.py:28-29), then Sinkhorn_m divides by tau (:180);
     // recomputed from s on every pass (keeps 64 values per thread resident instead of 128)
     const float rtau = tau;
-#define D0(k) ((-fabsf(s[k] - mnl)) / rtau)
-#define D1(k) ((-fabsf(s[k] - mxl)) / rtau)
+    // visit every q of this thread: register-resident values (unrolled), then LDS-resident ones
+    // (runtime loop: bounded code size and register pressure)
+    auto forq = [&](auto&& f) {
+#pragma unroll
+        for (int k = 0; k < NQR; ++k)
+            if (tid + 1024 * k < N) f(k, sr[k]);
+        for (int k = NQR; k < NQ; ++k)
+            if (tid + 1024 * k < N) f(k, sl[(k - NQR) * 1024 + tid]);
+    };
     const float kk = kvec[b];
     const float lcp0 = logf((float)N - kk);   // log(col_prob[:,0]) = log(n1*n2 - k)
     const float lcp1 = logf(kk);              // log(col_prob[:,1]) = log(k)
@@ -73,8 +86,8 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
         hi = mx;
         asm volatile("" : "+v"(lo), "+v"(hi));
     };
-    auto Lpair = [&](int k, float mnl, float mxl, float& L0, float& L1) {
-        float a0 = D0(k) - vu0, a1 = D1(k) - vu1;
+    auto Lpair = [&](float sv, float mnl, float mxl, float& L0, float& L1) {
+        float a0 = ((-fabsf(sv - mnl)) / rtau) - vu0, a1 = ((-fabsf(sv - mxl)) / rtau) - vu1;
         float u = urow(a0, a1);
         L0 = a0 - u;
         L1 = a1 - u;
@@ -97,15 +110,12 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
         float mnl, mxl;
         anchors(mnl, mxl);
         float m0 = -INFINITY, m1 = -INFINITY;
-#pragma unroll
-        for (int k = 0; k < NQ; ++k) {
-            if (tid + 1024 * k < N) {
-                float L0, L1;
-                Lpair(k, mnl, mxl, L0, L1);
-                m0 = fmaxf(m0, L0);
-                m1 = fmaxf(m1, L1);
-            }
-        }
+        forq([&](int k, float sv) {
+            float L0, L1;
+            Lpair(sv, mnl, mxl, L0, L1);
+            m0 = fmaxf(m0, L0);
+            m1 = fmaxf(m1, L1);
+        });
         m0 = fpm::warp_max(m0);
         m1 = fpm::warp_max(m1);
         if (lane == 0) { sa[wv] = m0; sb_[wv] = m1; }
@@ -115,15 +125,12 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
         __syncthreads();
         float a0 = 0.f, a1 = 0.f;
         anchors(mnl, mxl);   // fresh opaque anchors: recompute L instead of keeping 2*NQ values live
-#pragma unroll
-        for (int k = 0; k < NQ; ++k) {
-            if (tid + 1024 * k < N) {
-                float L0, L1;
-                Lpair(k, mnl, mxl, L0, L1);
-                if (m0 != -INFINITY) a0 += expf(L0 - m0);
-                if (m1 != -INFINITY) a1 += expf(L1 - m1);
-            }
-        }
+        forq([&](int k, float sv) {
+            float L0, L1;
+            Lpair(sv, mnl, mxl, L0, L1);
+            if (m0 != -INFINITY) a0 += expf(L0 - m0);
+            if (m1 != -INFINITY) a1 += expf(L1 - m1);
+        });
         a0 = fpm::warp_sum(a0);
         a1 = fpm::warp_sum(a1);
         if (lane == 0) { sa[wv] = a0; sb_[wv] = a1; }
@@ -139,14 +146,11 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
         float mnl, mxl;
         anchors(mnl, mxl);
         int flag = 0;
-#pragma unroll
-        for (int k = 0; k < NQ; ++k) {
-            if (tid + 1024 * k < N) {
-                float L0, L1;
-                Lpair(k, mnl, mxl, L0, L1);
-                flag |= (L0 > 0.f) | (L1 > 0.f);
-            }
-        }
+        forq([&](int k, float sv) {
+            float L0, L1;
+            Lpair(sv, mnl, mxl, L0, L1);
+            flag |= (L0 > 0.f) | (L1 > 0.f);
+        });
         int wf = __any(flag) ? 1 : 0;
         if (lane == 0) sflag[wv] = wf;
         __syncthreads();
@@ -177,18 +181,14 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
     }
     int n2o = n2b;
     asm volatile("" : "+v"(n2o));   // recompute (i, j) here rather than keep NQ addresses live
-#pragma unroll
-    for (int k = 0; k < NQ; ++k) {
+    forq([&](int k, float sv) {
         int q = tid + 1024 * k;
-        if (q < N) {
-            int i = q / n2o, j = q - i * n2o;
-            float L0, L1;
-            Lpair(k, mnl, mxl, L0, L1);
-            O[i * old_ + j] = expf(L1);
-        }
-    }
-#undef D0
-#undef D1
+        int i = q / n2o, j = q - i * n2o;
+        float L0, L1;
+        Lpair(sv, mnl, mxl, L0, L1);
+        O[i * old_ + j] = expf(L1);
+    });
+#undef SVAL
 }
 
 // Greedy top-k over Hungarian matches: prod = x * ds; argsort(prod, desc); accept (r,c) while

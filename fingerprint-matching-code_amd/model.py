@@ -63,6 +63,7 @@ class Net(nn.Module):
         self._pack = None
         self._pack_key = None
         self._pinned = None
+        self._stream_cache = {}
         self._keep_feats = False
         self._stage_timing = os.environ.get("FPM_STAGE_TIMING", "0") == "1"
         self.stage_times = {}
@@ -251,16 +252,62 @@ class Net(nn.Module):
         return out
 
     # ------------------------------------------------------------------------------------------
+    def _streams(self, dev):
+        key = str(dev)
+        if key not in self._stream_cache:
+            self._stream_cache[key] = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+        return self._stream_cache[key]
+
     def pipeline_chunks(self, B):
         """Sub-batches per forward so the host Hungarian of chunk c overlaps the GPU work of c+1."""
         if self.chunks is not None:
             return max(1, min(self.chunks, B))
         return max(1, min(8, B // 128))
 
+    def _stage_a(self, part, b0, b1, o, keep_feats, gt_ks, min_pt, st):
+        """GPU stage of one chunk (on its stream): everything up to ds_mat, then its D2H copy."""
+        dev = part.device
+        r = self.run_gpu_stage(part, keep_feats, s_out=o["s"][b0:b1], ss_out=o["ss"][b0:b1])
+        ks = o["k_prob"][b0:b1]
+        if self.regression:
+            ks.copy_(self._afau(self.packed(dev), o["ss"][b0:b1], part))
+        else:
+            ks.copy_(gt_ks[b0:b1] / min_pt[b0:b1])
+        self._mark("afau")
+        k_used = gt_ks[b0:b1] if self.training else ks * min_pt[b0:b1]
+        ops.soft_topk(o["ss"][b0:b1], part.n1, part.n2, k_used.contiguous(), C.SK_ITER_NUM, self.tau,
+                      out=o["ds_mat"][b0:b1], steps=o["sk_steps"][b0:b1])
+        o["_kk"][b0:b1].copy_(ks * min_pt[b0:b1])
+        self._mark("soft_topk")
+        self._pinned[b0:b1].copy_(o["ds_mat"][b0:b1], non_blocking=True)
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(st)
+        return r, ev
+
+    def _stage_c(self, part, b0, b1, o):
+        """Host Hungarian (utils/hungarian.py: LSA of -ds_mat per pair) + greedy selection +
+        MatchClassifier of one chunk; the caller waits for the chunk's D2H event first."""
+        dev = part.device
+        wp = self._pack
+        t = time.perf_counter()
+        assign = ops.lsa_batch_host(self._pinned[b0:b1], part.n_host[0], part.n_host[1], self.lsa_threads)
+        dt = time.perf_counter() - t
+        assign_d = assign.to(dev, non_blocking=True)
+        ops.topk_select(o["ds_mat"][b0:b1], assign_d, o["_kk"][b0:b1], lsa_out=o["lsa"][b0:b1],
+                        out=o["perm_mat"][b0:b1])
+        self._mark("lsa+h2d+select")
+        ops.match_cls(o["s"][b0:b1], o["perm_mat"][b0:b1], wp["mc_w1"], wp["mc_b1"], wp["mc_sc1"], wp["mc_sh1"],
+                      wp["mc_w2"], wp["mc_b2"], wp["mc_sc2"], wp["mc_sh2"], wp["mc_fcw"], wp["mc_fcb"],
+                      logits=o["cls_logits"][b0:b1], prob=o["cls_prob"][b0:b1])
+        self._mark("match_cls")
+        return dt
+
     def run(self, bt, gt_perm=None, label=None, keep_feats=False, chunks=None):
-        """Full forward.  The GPU stage of every chunk is queued at once on the stream; the host
-        LSA of chunk c starts as soon as its ds_mat lands in pinned memory, while the GPU keeps
-        going with the next chunks; the selection + classifier of chunk c follow its LSA."""
+        """Full forward, pipelined over sub-batches ("chunks").  Every chunk's GPU stage is queued
+        at once, alternating over two streams (per-pair kernels of neighbouring chunks -- Sinkhorn,
+        soft top-k, AFA-U, one workgroup per pair -- then fill the 256 CUs together); the host LSA
+        of chunk c starts as soon as its ds_mat lands in pinned memory while the GPU continues;
+        chunk c's selection + classifier follow its LSA on its stream."""
         dev = bt.device
         B, n1max, n2max = bt.B, bt.n1max, bt.n2max
         K = chunks if chunks is not None else self.pipeline_chunks(B)
@@ -272,77 +319,53 @@ class Net(nn.Module):
         else:
             gt_ks = torch.as_tensor(gt_perm).to(dev).reshape(B, -1).sum(-1).to(torch.float32)
         f32 = dict(device=dev, dtype=torch.float32)
-        s = torch.empty(B, n1max, n2max, **f32)
-        ss = torch.empty(B, n1max, n2max, **f32)
-        ds = torch.empty(B, n1max, n2max, **f32)
-        perm = torch.empty(B, n1max, n2max, **f32)
-        lsa = torch.empty(B, n1max, n2max, **f32)
-        ks = torch.empty(B, **f32)
-        logits = torch.empty(B, **f32)
-        prob = torch.empty(B, **f32)
-        steps = torch.empty(B, device=dev, dtype=torch.int32)
-        if self._pinned is None or self._pinned.shape != ds.shape:
-            self._pinned = torch.empty(ds.shape, dtype=torch.float32, pin_memory=True)
-        host = self._pinned
-        stream = torch.cuda.current_stream(dev)
+        o = {k: torch.empty(B, n1max, n2max, **f32) for k in ("s", "ss", "ds_mat", "perm_mat", "lsa")}
+        o.update({k: torch.empty(B, **f32) for k in ("k_prob", "cls_logits", "cls_prob", "_kk")})
+        o["sk_steps"] = torch.empty(B, device=dev, dtype=torch.int32)
+        if self._pinned is None or self._pinned.shape != o["ds_mat"].shape:
+            self._pinned = torch.empty(o["ds_mat"].shape, dtype=torch.float32, pin_memory=True)
+        main = torch.cuda.current_stream(dev)
         ev_start = torch.cuda.Event(enable_timing=True)
-        ev_start.record(stream)
+        ev_start.record(main)
+        streams = self._streams(dev) if len(parts) > 1 else [main]
+        for st in streams:
+            if st is not main:
+                st.wait_event(ev_start)
         outs, events = [], []
-        for part in parts:
+        for c, part in enumerate(parts):
+            st = streams[c % len(streams)]
             b0, b1 = getattr(part, "pair_range", (0, B))
-            o = self.run_gpu_stage(part, keep_feats, s_out=s[b0:b1], ss_out=ss[b0:b1])
-            if self.regression:
-                ks[b0:b1] = self._afau(self.packed(dev), ss[b0:b1], part)
-            else:
-                ks[b0:b1] = gt_ks[b0:b1] / min_pt[b0:b1]
-            self._mark("afau")
-            k_used = gt_ks[b0:b1] if self.training else ks[b0:b1] * min_pt[b0:b1]
-            ops.soft_topk(ss[b0:b1], part.n1, part.n2, k_used.contiguous(), C.SK_ITER_NUM, self.tau,
-                          out=ds[b0:b1], steps=steps[b0:b1])
-            self._mark("soft_topk")
-            host[b0:b1].copy_(ds[b0:b1], non_blocking=True)
-            ev = torch.cuda.Event(enable_timing=True)
-            ev.record(stream)
+            with torch.cuda.stream(st):
+                r, ev = self._stage_a(part, b0, b1, o, keep_feats, gt_ks, min_pt, st)
+            outs.append(r)
             events.append(ev)
-            outs.append(o)
-        t_lsa = 0.0
-        t_first = None
-        kk = (ks * min_pt).contiguous()
-        wp = self._pack
-        for part, ev in zip(parts, events):
+        t_lsa, t_first = 0.0, None
+        for c, (part, ev) in enumerate(zip(parts, events)):
             b0, b1 = getattr(part, "pair_range", (0, B))
             ev.synchronize()
-            if t_first is None:
-                t_first = time.perf_counter()
-            t = time.perf_counter()
-            # Hungarian on host threads (utils/hungarian.py): LSA of -ds_mat per pair
-            assign = ops.lsa_batch_host(host[b0:b1], part.n_host[0], part.n_host[1], self.lsa_threads)
-            t_lsa += time.perf_counter() - t
-            assign_d = assign.to(dev, non_blocking=True)
-            ops.topk_select(ds[b0:b1], assign_d, kk[b0:b1], lsa_out=lsa[b0:b1], out=perm[b0:b1])
-            self._mark("lsa+h2d+select")
-            ops.match_cls(s[b0:b1], perm[b0:b1], wp["mc_w1"], wp["mc_b1"], wp["mc_sc1"], wp["mc_sh1"], wp["mc_w2"],
-                          wp["mc_b2"], wp["mc_sc2"], wp["mc_sh2"], wp["mc_fcw"], wp["mc_fcb"],
-                          logits=logits[b0:b1], prob=prob[b0:b1])
-            self._mark("match_cls")
-        res = dict(s=s, ss=ss, ds_mat=ds, perm_mat=perm, k_prob=ks, cls_prob=prob, cls_logits=logits, lsa=lsa,
-                   sk_steps=steps)
+            t_first = t_first or time.perf_counter()
+            with torch.cuda.stream(streams[c % len(streams)]):
+                t_lsa += self._stage_c(part, b0, b1, o)
+        for st in streams:
+            if st is not main:
+                main.wait_stream(st)
+        res = {k: v for k, v in o.items() if not k.startswith("_")}
         if len(outs) == 1 or keep_feats:
             for k in outs[0]:
                 if k not in ("s", "ss"):
-                    res[k] = outs[0][k] if len(outs) == 1 else torch.cat([o[k] for o in outs])
+                    res[k] = outs[0][k] if len(outs) == 1 else torch.cat([r[k] for r in outs])
+        ks, logits = o["k_prob"], o["cls_logits"]
         if label is not None:
             res["cls_loss"] = F.binary_cross_entropy_with_logits(logits, torch.as_tensor(label).to(dev).view(-1).float())
         else:
             res["cls_loss"] = torch.tensor(0.0, device=dev)
         if self.regression:
-            sup = gt_ks / min_pt
-            res["ks_loss"] = F.mse_loss(ks, sup) * self.k_factor
+            res["ks_loss"] = F.mse_loss(ks, gt_ks / min_pt) * self.k_factor
             res["ks_error"] = F.l1_loss(ks * min_pt, gt_ks)
         else:
             res["ks_loss"] = 0.0
             res["ks_error"] = 0.0
-        # GPU time of the stage before the Hungarian (all chunks), from events on the stream
+        # GPU time of the stages before the Hungarian (all chunks), from events on the streams
         self.last_timing = dict(gpu_stage_s=ev_start.elapsed_time(events[-1]) / 1e3, lsa_s=t_lsa,
                                 first_chunk_wait_s=(t_first or t0) - t0, chunks=len(parts))
         return res
