@@ -14,6 +14,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -250,6 +253,77 @@ int lsa_pair(const float* s, long ld, int n1, int n2, int* assign, int n1max) {
 
 thread_local char g_lsa_err[256];
 
+// Persistent worker pool (created on first use, sized to the largest request seen).
+class Pool {
+  public:
+    void run(int nthreads, int ntasks, const std::function<void(int)>& fn) {
+        std::unique_lock<std::mutex> lk(mu_);
+        while ((int)workers_.size() < nthreads - 1) {
+            const int idx = (int)workers_.size();
+            const long g = gen_;     // generation before this run's increment: the worker joins it
+            workers_.emplace_back([this, idx, g] { loop(idx, g); });
+        }
+        fn_ = &fn;
+        ntasks_ = ntasks;
+        next_.store(0);
+        active_ = nthreads - 1;
+        done_ = 0;
+        ++gen_;
+        cv_.notify_all();
+        lk.unlock();
+        drain();
+        lk.lock();
+        done_cv_.wait(lk, [this] { return done_ == active_; });
+        fn_ = nullptr;
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+            ++gen_;
+        }
+        cv_.notify_all();
+        for (auto& t : workers_) t.join();
+    }
+
+  private:
+    void drain() {
+        while (true) {
+            int t = next_.fetch_add(1);
+            if (t >= ntasks_) break;
+            (*fn_)(t);
+        }
+    }
+    void loop(int idx, long seen) {
+        while (true) {
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_.wait(lk, [&] { return gen_ != seen; });
+            seen = gen_;
+            if (stop_) return;
+            const bool mine = idx < active_;
+            lk.unlock();
+            if (!mine) continue;
+            drain();
+            lk.lock();
+            ++done_;
+            if (done_ == active_) done_cv_.notify_all();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    std::vector<std::thread> workers_;
+    const std::function<void(int)>* fn_ = nullptr;
+    std::atomic<int> next_{0};
+    int ntasks_ = 0, active_ = 0, done_ = 0;
+    long gen_ = 0;
+    bool stop_ = false;
+};
+
+Pool& pool() {
+    static Pool p;
+    return p;
+}
+
 }  // namespace
 
 extern "C" {
@@ -261,25 +335,20 @@ int fpm_lsa_batch_host(const float* s, long sb, long ld, const int* n1, const in
     if (B <= 0) return 0;
     if (nthreads < 1) nthreads = 1;
     if (nthreads > B) nthreads = B;
-    std::atomic<int> next(0), fail(0);
-    auto work = [&]() {
-        while (true) {
-            int b = next.fetch_add(1);
-            if (b >= B) break;
-            int rc = lsa_pair(s + (long)b * sb, ld, n1[b], n2[b], assign + (long)b * n1max, n1max);
-            if (rc) {
-                int expect = 0;
-                fail.compare_exchange_strong(expect, b + 1);
-            }
+    std::atomic<int> fail(0);
+    std::function<void(int)> work = [&](int b) {
+        int rc = lsa_pair(s + (long)b * sb, ld, n1[b], n2[b], assign + (long)b * n1max, n1max);
+        if (rc) {
+            int expect = 0;
+            fail.compare_exchange_strong(expect, b + 1);
         }
     };
     if (nthreads == 1) {
-        work();
+        for (int b = 0; b < B; ++b) work(b);
     } else {
-        std::vector<std::thread> th;
-        th.reserve(nthreads);
-        for (int t = 0; t < nthreads; ++t) th.emplace_back(work);
-        for (auto& t : th) t.join();
+        static std::mutex call_mu;   // one batch at a time through the shared pool
+        std::lock_guard<std::mutex> g(call_mu);
+        pool().run(nthreads, B, work);
     }
     return fail.load();
 }
