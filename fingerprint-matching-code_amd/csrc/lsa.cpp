@@ -207,6 +207,110 @@ __attribute__((target("avx2"))) int lsap_solve_avx2(int nr, int nc, const double
 }
 #endif
 
+// ---- dense-scan form (default) -------------------------------------------------------------------
+// Same algorithm again, but the Dijkstra scan runs over ALL columns with a "remaining" mask, so
+// the cost row, v and spc are read contiguously 4 doubles at a time (no gather, no branches).
+// The scan order of the remaining list matters only when several remaining columns hold the
+// minimum exactly; then their positions in that list (maintained under the swap-remove) decide,
+// with the scalar loop's rule (last unassigned holder of the minimum, else the first holder).
+__attribute__((target("avx2"))) int lsap_solve_dense(int nr, int nc, const double* cost, std::vector<int>& col4row) {
+    const int ncp = (nc + 3) & ~3;
+    std::vector<double> u(nr, 0.0), v(ncp, 0.0), spc(ncp);
+    std::vector<long long> rem(ncp);
+    std::vector<long long> path(ncp, -1);   // 64-bit so it blends with the double lanes
+    std::vector<int> row4col(nc, -1), remaining(nc), pos(nc);
+    std::vector<char> SR(nr), SC(nc);
+    std::vector<int> ties;
+    std::vector<double> crow_pad;
+    const bool pad = ncp != nc;
+    if (pad) crow_pad.assign(ncp, 0.0);
+    col4row.assign(nr, -1);
+    const __m256d vinf = _mm256_set1_pd(INFINITY);
+    for (int cur = 0; cur < nr; ++cur) {
+        double minVal = 0.0;
+        int i = cur;
+        int num = nc;
+        for (int it = 0; it < nc; ++it) {
+            remaining[it] = nc - it - 1;
+            pos[nc - it - 1] = it;
+        }
+        for (int j = 0; j < ncp; ++j) {
+            rem[j] = j < nc ? -1LL : 0LL;
+            spc[j] = INFINITY;
+        }
+        std::fill(SR.begin(), SR.end(), 0);
+        std::fill(SC.begin(), SC.end(), 0);
+        int sink = -1;
+        while (sink == -1) {
+            SR[i] = 1;
+            const double* crow = cost + (long)i * nc;
+            if (pad) {
+                std::copy(crow, crow + nc, crow_pad.begin());
+                crow = crow_pad.data();
+            }
+            const __m256d vmv = _mm256_set1_pd(minVal), vui = _mm256_set1_pd(u[i]);
+            const __m256d vi = _mm256_castsi256_pd(_mm256_set1_epi64x(i));
+            __m256d vlow = vinf;
+            for (int j = 0; j < ncp; j += 4) {
+                const __m256d m = _mm256_castsi256_pd(_mm256_loadu_si256((const __m256i*)&rem[j]));
+                const __m256d r = _mm256_sub_pd(_mm256_sub_pd(_mm256_add_pd(vmv, _mm256_loadu_pd(crow + j)), vui),
+                                                _mm256_loadu_pd(&v[j]));
+                __m256d sv = _mm256_loadu_pd(&spc[j]);
+                const __m256d lt = _mm256_and_pd(_mm256_cmp_pd(r, sv, _CMP_LT_OQ), m);
+                sv = _mm256_blendv_pd(sv, r, lt);
+                _mm256_storeu_pd(&spc[j], sv);
+                const __m256d pv = _mm256_castsi256_pd(_mm256_loadu_si256((const __m256i*)&path[j]));
+                _mm256_storeu_si256((__m256i*)&path[j], _mm256_castpd_si256(_mm256_blendv_pd(pv, vi, lt)));
+                vlow = _mm256_min_pd(vlow, _mm256_blendv_pd(vinf, sv, m));
+            }
+            double t4[4];
+            _mm256_storeu_pd(t4, vlow);
+            const double lowest = std::min(std::min(t4[0], t4[1]), std::min(t4[2], t4[3]));
+            if (lowest == INFINITY) return -1;
+            // remaining columns holding the minimum
+            ties.clear();
+            const __m256d vl = _mm256_set1_pd(lowest);
+            for (int j = 0; j < ncp; j += 4) {
+                const __m256d m = _mm256_castsi256_pd(_mm256_loadu_si256((const __m256i*)&rem[j]));
+                const int mk = _mm256_movemask_pd(_mm256_and_pd(_mm256_cmp_pd(_mm256_loadu_pd(&spc[j]), vl, _CMP_EQ_OQ), m));
+                if (mk)
+                    for (int q = 0; q < 4; ++q)
+                        if (mk & (1 << q)) ties.push_back(j + q);
+            }
+            int j = ties[0];
+            if (ties.size() > 1) {
+                int first = -1, lastu = -1, fpos = nc, upos = -1;
+                for (int t : ties) {
+                    if (pos[t] < fpos) { fpos = pos[t]; first = t; }
+                    if (row4col[t] == -1 && pos[t] > upos) { upos = pos[t]; lastu = t; }
+                }
+                j = lastu >= 0 ? lastu : first;
+            }
+            minVal = lowest;
+            rem[j] = 0;
+            const int p = pos[j], last = remaining[--num];
+            remaining[p] = last;
+            pos[last] = p;
+            if (row4col[j] == -1) sink = j;
+            else i = row4col[j];
+            SC[j] = 1;
+        }
+        u[cur] += minVal;
+        for (int r = 0; r < nr; ++r)
+            if (SR[r] && r != cur) u[r] += minVal - spc[col4row[r]];
+        for (int c = 0; c < nc; ++c)
+            if (SC[c]) v[c] -= minVal - spc[c];
+        int j = sink;
+        while (true) {
+            const int r = (int)path[j];
+            row4col[j] = r;
+            std::swap(col4row[r], j);
+            if (r == cur) break;
+        }
+    }
+    return 0;
+}
+
 bool use_avx2() {
 #if defined(__x86_64__)
     static int ok = -1;
@@ -238,7 +342,7 @@ int lsa_pair(const float* s, long ld, int n1, int n2, int* assign, int n1max) {
         if (cost[k] != cost[k] || cost[k] == -INFINITY) return -2;   // invalid (scipy raises)
     std::vector<int> c4r;
 #if defined(__x86_64__)
-    int rc = use_avx2() ? lsap_solve_avx2(nr, nc, cost.data(), c4r) : lsap_solve(nr, nc, cost.data(), c4r);
+    int rc = use_avx2() ? lsap_solve_dense(nr, nc, cost.data(), c4r) : lsap_solve(nr, nc, cost.data(), c4r);
 #else
     int rc = lsap_solve(nr, nc, cost.data(), c4r);
 #endif
