@@ -167,7 +167,7 @@ def main():
                        "edges_per_graph": E_tot / (2.0 * args.batch), "parallelism": "pair-sharded x%d" % world},
             "gpu_stage_pairs_per_s": args.batch * world * args.steps / gpu_s,
             "host_lsa_ms_per_step": lsa_s / args.steps * 1e3,
-            "roofline": {"kernel": "spline edge-message GEMM (gemm_kernel<%s,SEGSCALE>)" % args.dtype,
+            "roofline": {"kernel": "spline (node, cell) product GEMM (gemm_kernel<%s>, grouped by cell)" % args.dtype,
                          "bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak, "traffic": None,
                          "launches": cnt.value, "avg_launch_ms": ms.value / max(cnt.value, 1),

@@ -27,7 +27,8 @@ SIGNATURES = {
     "fpm_spline_plan_bytes": (L, [L, L]),
     "fpm_spline_plan": (I, [P, P, P, L, L, I, P, L, P]),
     "fpm_spline_plan_csr": (I, [P, L, L, ctypes.POINTER(P), ctypes.POINTER(P)]),
-    "fpm_spline_conv_fwd": (I, [I, P, P, L, L, I, P, P, P, P, P, P, I, P, P, P, P, P]),
+    "fpm_spline_y_bytes": (L, [I, L, L]),
+    "fpm_spline_conv_fwd": (I, [I, P, P, L, L, I, P, P, P, P, L, I, P, P, P, P, P]),
     "fpm_edge_diff": (I, [P, P, P, L, I, P, P]),
     "fpm_kron_gnn_layer_fwd": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, P, P]),
     "fpm_gnn_param_count": (I, [I]),

@@ -20,7 +20,8 @@ extern "C" int fpm_gemm(int dtype, const void* A, long lda, long sA, const int* 
     p.M = M; p.N = N; p.K = K; p.nseg = 1;
     p.tile_info = nullptr; p.group_off = nullptr;
     p.epi = epi; p.bias = bias; p.Cf = Cf; p.Ct = Ct; p.ldc = ldc; p.sC = sC; p.n1 = n1; p.n2 = n2;
-    dim3 grid((N + GBN - 1) / GBN, (M + GBM - 1) / GBM, batch);
+    p.remap_mtiles = (M + GBM - 1) / GBM;
+    dim3 grid(remap_grid(N, p.remap_mtiles), 1, batch);
     hipStream_t st = (hipStream_t)stream;
     if (dtype == 0) hipLaunchKernelGGL((gemm_kernel<float, false>), grid, dim3(GTHREADS), 0, st, p);
     else hipLaunchKernelGGL((gemm_kernel<bf16_t, false>), grid, dim3(GTHREADS), 0, st, p);

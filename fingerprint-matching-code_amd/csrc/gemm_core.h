@@ -7,8 +7,9 @@
 //   nseg segments, each with its own B matrix (SplineConv: the 4 B-spline cells of the edge's
 //   group), and the segment partial sums are folded into the result with a per-row fp32 scale
 //   (the B-spline basis) — so A rows are never rescaled or re-rounded.
-// * Grouped mode (SplineConv): blockIdx.y indexes a device-built tile table (group, first row);
-//   entries past the real tile count have group -1 and exit.
+// * Grouped mode (SplineConv): the row tile indexes a device-built tile table (group, first row);
+//   entries past the real tile count have group -1 and exit.  With nseg == 1 the group selects
+//   its B matrix (B + group * sB_seg): the (node, cell) product GEMM.
 // * T = float  -> v_mfma_f32_16x16x4_f32  (exact fp32 products, parity mode)
 //   T = bf16_t -> v_mfma_f32_16x16x32_bf16 (fp32 accumulate, throughput mode)
 // Tile 128x128, 256 threads = 4 waves (2x2), 64x64 per wave = 4x4 MFMA 16x16 fragments.
@@ -42,7 +43,16 @@ struct GemmParams {
     long ldc, sC;
     const int* n1;
     const int* n2;
+    int remap_mtiles;        // > 0: 1-D XCD-aware grid over remap_mtiles x ceil(N/128) tiles
 };
+
+// 1-D grid for the XCD-aware tile order: padded to whole rounds of 8 chunks so the remap is a
+// bijection (extra blocks exit).
+inline unsigned remap_grid(int N, int mtiles) {
+    long nt = (N + 127) / 128, chunk = 4 * nt;
+    long t = nt * mtiles;
+    return (unsigned)((t + 8 * chunk - 1) / (8 * chunk) * (8 * chunk));
+}
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
@@ -124,16 +134,31 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_kernel(GemmParams p) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
     const int batch = blockIdx.z;
-    const int n0 = blockIdx.x * GBN;
+    int ntile = blockIdx.x, mtile = blockIdx.y;
+    if (p.remap_mtiles > 0) {
+        // Workgroups are dispatched round-robin over the 8 XCDs (blockIdx % 8).  Give each XCD a
+        // contiguous run of logical tiles, N fastest, so the ceil(N/128) column tiles that share an
+        // A row-tile (and consecutive row tiles sharing a weight) hit the same XCD's L2.
+        // Runs are chunks of 4 row tiles x nt column tiles, dealt to the XCDs in turn, so a tail of
+        // empty tiles (grouped mode over-provisions the table) stays spread over all 8 XCDs.
+        const int nt = (p.N + GBN - 1) / GBN;
+        const int chunk = 4 * nt;
+        const int i = blockIdx.x >> 3;
+        const int q = ((i / chunk) * 8 + (blockIdx.x & 7)) * chunk + (i % chunk);
+        mtile = q / nt;
+        ntile = q - mtile * nt;
+        if (mtile >= p.remap_mtiles) return;
+    }
+    const int n0 = ntile * GBN;
 
     int group = 0, row0, row_end;
     if (p.tile_info) {
-        group = p.tile_info[2 * blockIdx.y];
+        group = p.tile_info[2 * mtile];
         if (group < 0) return;
-        row0 = p.tile_info[2 * blockIdx.y + 1];
+        row0 = p.tile_info[2 * mtile + 1];
         row_end = p.group_off[group + 1];
     } else {
-        row0 = blockIdx.y * GBM;
+        row0 = mtile * GBM;
         row_end = p.M;
     }
 
@@ -160,7 +185,7 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_kernel(GemmParams p) {
     auto load_tile = [&](int kt) {
         int seg = kt / ktiles;
         int k0 = (kt - seg * ktiles) * BK + lc * EPC;
-        const T* Bseg = Bb + (p.nseg > 1 ? (long)spline_cell(group, seg) * p.sB_seg : 0);
+        const T* Bseg = Bb + (long)(p.nseg > 1 ? spline_cell(group, seg) : group) * p.sB_seg;
         bool kin = k0 < p.K;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {

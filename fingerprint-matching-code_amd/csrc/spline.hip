@@ -2,127 +2,186 @@
 // as used by the reference's SConv, src/model/spline_conv.py:17,28-41, and the Siamese
 // residual x + 0.1*SConv(x), spline_conv.py:51-57).
 //
-// MI355X design: edges of the whole side-batch are bucketed by their B-spline group
-// g = (floor(4u0), floor(4u1)) (25 groups; every edge of group g uses the same 4 kernel cells), so
-// a layer is one grouped MFMA GEMM with K = 4 x 768 (A = gathered source rows, B = the 4 cells'
-// [out][in] weights, fp32 basis applied per segment) writing one message row per edge, plus the
-// root GEMM x R, plus a segmented max over each node's in-edges fused with root/bias/ReLU or the
-// residual.  The bucketing plan (basis, group offsets, tile table, dst CSR) is built on device
-// once per side and shared by both layers.
+// MI355X design.  A message is msg_e = sum_s basis[e,s] * (x_src W_{cell(e,s)}) over the 4 corners
+// of the edge's B-spline group.  The products x_u W_k depend only on (source node, cell), and the
+// ~6 out-edges x 4 corners of a node touch only ~9 distinct cells (neighbouring directions share
+// cells), so each needed (node, cell) product is computed ONCE: the plan marks a 26-bit cell mask
+// per node (25 spline cells + the root weight as cell 25), ranks the (node, cell) rows per cell in
+// node order, and one grouped MFMA GEMM (group = cell, A = gathered node rows, B = that cell's
+// [out][in] weight) writes the product rows Y.  A combine kernel then forms each in-edge's message
+// from 4 rows of Y in fp32 (basis order s = 0..3, the reference's), takes the max per destination
+// and fuses root + bias + ReLU or the Siamese residual.  That is ~2.5x fewer MFMA flops than the
+// per-edge GEMM, and the message tensor is never materialised.  The plan (dst CSR included) is
+// built on device once per side and shared by both layers and the GNN layers.
 #include "gemm_core.h"
 
 #include <vector>
 
 namespace {
 
-// optional HIP-event timing of the dominant kernel (edge-message GEMM), read by bench.py
+// optional HIP-event timing of the dominant kernel (the (node, cell) product GEMM), read by bench.py
 struct ProfRec {
     hipEvent_t a, b;
-    double flops;
+    int slot;                // g_prof_rows[slot] = product rows of the launch (flops = 2 rows 768^2)
 };
 bool g_prof_on = false;
 std::vector<ProfRec> g_prof;
+int* g_prof_rows = nullptr;   // device copies of each profiled launch's row count
+constexpr int PROF_MAX = 4096;
 
-
+constexpr int NCELL = 26;   // 25 B-spline cells + the root weight (cell 25)
 
 struct PlanLayout {
-    long cnt, grp_off, slot, dslot, gidx, indeg, dst_ptr, rows_src, rows_basis, dst_rows, nbr_local, tile_info,
-        total;
+    long mask, indeg, dslot, basis_e, grp_e, blk_cnt, cell_off, rowid, arows, tile_info, dst_ptr, csr_e, nbr_local,
+        rows4, basis4, total;
+    long nblk, max_rows, max_tiles;
 };
 
 __host__ __device__ inline long al(long x) { return (x + 255) & ~255L; }
 
-PlanLayout plan_layout(long E, long num_nodes, long max_tiles) {
+// Deduplicated message GEMM: every (source node, cell) product x_u W_k that some edge corner needs
+// is computed once (a node's ~6 out-edges x 4 corners touch ~9 distinct cells), root = cell 25.
+inline long plan_max_rows(long E, long num_nodes) {
+    long a = 4 * E, b = 25 * num_nodes;
+    return (a < b ? a : b) + num_nodes;
+}
+
+PlanLayout plan_layout(long E, long num_nodes) {
     PlanLayout L;
+    L.nblk = (num_nodes + 255) / 256;
+    L.max_rows = plan_max_rows(E, num_nodes);
+    L.max_tiles = L.max_rows / fpm::GBM + NCELL + 1;
     long o = 0;
-    L.cnt = o; o += al(32 * 4);
-    L.grp_off = o; o += al(32 * 4);
-    L.slot = o; o += al(E * 4);
-    L.dslot = o; o += al(E * 4);
-    L.gidx = o; o += al(E * 4);
+    L.mask = o; o += al(num_nodes * 4);
     L.indeg = o; o += al(num_nodes * 4);
+    L.dslot = o; o += al(E * 4);
+    L.basis_e = o; o += al(E * 16);
+    L.grp_e = o; o += al(E * 4);
+    L.blk_cnt = o; o += al(L.nblk * NCELL * 4);
+    L.cell_off = o; o += al(32 * 4);
+    L.rowid = o; o += al(num_nodes * NCELL * 4);
+    L.arows = o; o += al(L.max_rows * 4);
+    L.tile_info = o; o += al(L.max_tiles * 8);
     L.dst_ptr = o; o += al((num_nodes + 1) * 4);
-    L.rows_src = o; o += al(E * 4);
-    L.rows_basis = o; o += al(E * 16);
-    L.dst_rows = o; o += al(E * 4);
+    L.csr_e = o; o += al(E * 4);
     L.nbr_local = o; o += al(E * 4);
-    L.tile_info = o; o += al(max_tiles * 8);
+    L.rows4 = o; o += al(E * 16);
+    L.basis4 = o; o += al(E * 16);
     L.total = o;
     return L;
 }
 
-// per-edge basis + group; slots within a group come from a block-local LDS histogram plus one
-// global atomic per (block, group) (25 global counters would otherwise serialise 1.5M atomics)
-__global__ __launch_bounds__(256) void plan_count_kernel(const int* __restrict__ src, const int* __restrict__ dst,
-                                                         const float* __restrict__ pseudo, long E, int* cnt, int* slot,
-                                                         int* dslot, int* gidx, int* indeg, float* basis_tmp) {
-    __shared__ int lcnt[32], lbase[32];
-    if (threadIdx.x < 32) lcnt[threadIdx.x] = 0;
-    __syncthreads();
+// per edge: torch-spline-conv open-spline degree-1 basis, group, the source's cell mask, in-degree slot
+__global__ __launch_bounds__(256) void plan_edge_kernel(const int* __restrict__ src, const int* __restrict__ dst,
+                                                        const float* __restrict__ pseudo, long E, int* mask,
+                                                        int* indeg, int* dslot, float* basis_e, int* grp_e) {
     const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    int g = -1, lslot = 0;
-    if (e < E) {
-        // torch-spline-conv basis, open spline degree 1: v = u * (kernel - 1), frac, floor
-        int f[2];
-        float fr[2];
+    if (e >= E) return;
+    int f[2];
+    float fr[2];
 #pragma unroll
-        for (int d = 0; d < 2; ++d) {
-            float v = pseudo[2 * e + d] * 4.0f;
-            float fl = floorf(v);
-            f[d] = (int)fl;
-            fr[d] = v - fl;
-        }
-        float b4[4];
+    for (int d = 0; d < 2; ++d) {
+        float v = pseudo[2 * e + d] * 4.0f;
+        float fl = floorf(v);
+        f[d] = (int)fl;
+        fr[d] = v - fl;
+    }
+    float b4[4];
+    int bits = 0;
+    const int g = f[0] + 5 * f[1];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            float b = 1.0f;
-            b = b * ((s & 1) ? fr[0] : 1.0f - fr[0]);
-            b = b * ((s >> 1) ? fr[1] : 1.0f - fr[1]);
-            b4[s] = b;
-        }
-        g = f[0] + 5 * f[1];
-        gidx[e] = g;
-        lslot = atomicAdd(&lcnt[g], 1);
-        dslot[e] = atomicAdd(&indeg[dst[e]], 1);
-        *(float4*)(basis_tmp + 4 * e) = make_float4(b4[0], b4[1], b4[2], b4[3]);
+    for (int s = 0; s < 4; ++s) {
+        float b = 1.0f;
+        b = b * ((s & 1) ? fr[0] : 1.0f - fr[0]);
+        b = b * ((s >> 1) ? fr[1] : 1.0f - fr[1]);
+        b4[s] = b;
+        bits |= 1 << fpm::spline_cell(g, s);
     }
-    __syncthreads();
-    if (threadIdx.x < 25) {
-        int c = lcnt[threadIdx.x];
-        lbase[threadIdx.x] = c ? atomicAdd(&cnt[threadIdx.x], c) : 0;
-    }
-    __syncthreads();
-    if (e < E) slot[e] = lbase[g] + lslot;
+    grp_e[e] = g;
+    *(float4*)(basis_e + 4 * e) = make_float4(b4[0], b4[1], b4[2], b4[3]);
+    atomicOr(&mask[src[e]], bits);
+    dslot[e] = atomicAdd(&indeg[dst[e]], 1);
 }
 
-__global__ __launch_bounds__(1024) void plan_scan_kernel(const int* cnt, int* grp_off, int* tile_info,
+// rows of cell k are the nodes whose mask has bit k, in node order (deterministic): per-block
+// counts here, block bases by the scan kernel, ranks by plan_rank_kernel (same ballots).
+__device__ __forceinline__ unsigned long long cell_ballot(int m, int k) {
+    return __ballot((m >> k) & 1);
+}
+
+__global__ __launch_bounds__(256) void plan_blkcount_kernel(const int* __restrict__ mask, long num_nodes,
+                                                            int* __restrict__ blk_cnt) {
+    __shared__ int wc[4][NCELL];
+    const long u = (long)blockIdx.x * 256 + threadIdx.x;
+    const int m = u < num_nodes ? (mask[u] | (1 << 25)) : 0;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int k = 0; k < NCELL; ++k) {
+        unsigned long long b = cell_ballot(m, k);
+        if (lane == 0) wc[wave][k] = __popcll(b);
+    }
+    __syncthreads();
+    if (threadIdx.x < NCELL) {
+        int k = threadIdx.x;
+        blk_cnt[(long)blockIdx.x * NCELL + k] = wc[0][k] + wc[1][k] + wc[2][k] + wc[3][k];
+    }
+}
+
+// one block: per-cell exclusive scan over blocks (in place), cell offsets, GEMM tile table, and the
+// exclusive scan of in-degrees -> dst CSR pointers.
+__global__ __launch_bounds__(1024) void plan_scan_kernel(int* blk_cnt, long nblk, int* cell_off, int* tile_info,
                                                          int max_tiles, const int* indeg, int* dst_ptr,
                                                          long num_nodes) {
     __shared__ int part[1024];
     __shared__ int tilebuf[16384];
-    __shared__ int ntile_total;
+    __shared__ int cell_tot[NCELL], tile_off[NCELL + 1], coff[NCELL + 1];
     const int tid = threadIdx.x;
-    if (tid == 0) {
-        int off = 0, t = 0;
-        for (int g = 0; g < 25; ++g) {
-            grp_off[g] = off;
-            int c = cnt[g];
-            for (int r = 0; r < c; r += fpm::GBM) {
-                tile_info[2 * t] = g;
-                tile_info[2 * t + 1] = off + r;
-                ++t;
+    // (1) per-cell scans over blocks: 26 cells in parallel groups of threads would need a 2-D
+    //     scan; nblk <= a few thousand, so one pass per cell with the block-wide scan is enough.
+    for (int k = 0; k < NCELL; ++k) {
+        int carry = 0;
+        for (long t0 = 0; t0 < nblk; t0 += 1024) {
+            long i = t0 + tid;
+            int v = i < nblk ? blk_cnt[i * NCELL + k] : 0;
+            part[tid] = v;
+            __syncthreads();
+            for (int o = 1; o < 1024; o <<= 1) {
+                int w = tid >= o ? part[tid - o] : 0;
+                __syncthreads();
+                part[tid] += w;
+                __syncthreads();
             }
-            off += c;
+            if (i < nblk) blk_cnt[i * NCELL + k] = carry + part[tid] - v;
+            carry += part[1023];
+            __syncthreads();
         }
-        grp_off[25] = off;
-        ntile_total = t;
+        if (tid == 0) cell_tot[k] = carry;
     }
     __syncthreads();
-    for (int t = ntile_total + tid; t < max_tiles; t += 1024) {
-        tile_info[2 * t] = -1;
-        tile_info[2 * t + 1] = 0;
+    if (tid == 0) {
+        int off = 0, t = 0;
+        for (int k = 0; k < NCELL; ++k) {
+            cell_off[k] = off;
+            coff[k] = off;
+            tile_off[k] = t;
+            off += cell_tot[k];
+            t += (cell_tot[k] + fpm::GBM - 1) / fpm::GBM;
+        }
+        cell_off[NCELL] = off;
+        tile_off[NCELL] = t;
     }
-    // exclusive scan of indeg -> dst_ptr, tiled through LDS (coalesced global reads/writes)
+    __syncthreads();
+    for (int t = tid; t < max_tiles; t += 1024) {
+        int g = -1, r0 = 0;
+        if (t < tile_off[NCELL]) {
+            int k = 0;
+            while (tile_off[k + 1] <= t) ++k;
+            g = k;
+            r0 = coff[k] + (t - tile_off[k]) * fpm::GBM;
+        }
+        tile_info[2 * t] = g;
+        tile_info[2 * t + 1] = r0;
+    }
+    // (2) exclusive scan of indeg -> dst_ptr, tiled through LDS (coalesced global reads/writes)
     constexpr int TILE = 16384, PER = TILE / 1024;
     int* buf = tilebuf;
     int carry = 0;
@@ -157,88 +216,155 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(const int* cnt, int* gr
     if (tid == 0) dst_ptr[num_nodes] = carry;
 }
 
+// rowid[u][k] (or -1) and the GEMM's row gather arows[row] = u
+__global__ __launch_bounds__(256) void plan_rank_kernel(const int* __restrict__ mask, long num_nodes,
+                                                        const int* __restrict__ blk_base,
+                                                        const int* __restrict__ cell_off, int* __restrict__ rowid,
+                                                        int* __restrict__ arows) {
+    __shared__ int wc[4][NCELL];
+    const long u = (long)blockIdx.x * 256 + threadIdx.x;
+    const int m = u < num_nodes ? (mask[u] | (1 << 25)) : 0;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    int myrank[NCELL];
+#pragma unroll
+    for (int k = 0; k < NCELL; ++k) {
+        unsigned long long b = cell_ballot(m, k);
+        if (lane == 0) wc[wave][k] = __popcll(b);
+        myrank[k] = __popcll(b & lt);
+    }
+    __syncthreads();
+    if (u >= num_nodes) return;
+#pragma unroll
+    for (int k = 0; k < NCELL; ++k) {
+        int r = -1;
+        if ((m >> k) & 1) {
+            int pre = 0;
+            for (int w = 0; w < wave; ++w) pre += wc[w][k];
+            r = cell_off[k] + blk_base[(long)blockIdx.x * NCELL + k] + pre + myrank[k];
+            arows[r] = (int)u;
+        }
+        rowid[u * NCELL + k] = r;
+    }
+}
+
 __global__ void plan_fill_kernel(const int* __restrict__ src, const int* __restrict__ dst, long E, int nmax,
-                                 const int* __restrict__ grp_off, const int* __restrict__ slot,
-                                 const int* __restrict__ dslot, const int* __restrict__ gidx,
-                                 const int* __restrict__ dst_ptr, const float* __restrict__ basis_tmp, int* rows_src,
-                                 float* rows_basis, int* dst_rows, int* nbr_local) {
+                                 const int* __restrict__ dslot, const int* __restrict__ dst_ptr, int* csr_e,
+                                 int* nbr_local) {
     long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= E) return;
-    int row = grp_off[gidx[e]] + slot[e];
-    int s = src[e], d = dst[e];
-    rows_src[row] = s;
-    *(float4*)(rows_basis + 4 * (long)row) = *(const float4*)(basis_tmp + 4 * e);
-    int p = dst_ptr[d] + dslot[e];
-    dst_rows[p] = row;
-    nbr_local[p] = s % nmax;
+    int p = dst_ptr[dst[e]] + dslot[e];
+    csr_e[p] = (int)e;
+    nbr_local[p] = src[e] % nmax;
 }
 
 // Deterministic in-edge order per node (ascending source): the atomics above fill each list in
-// arbitrary order, and the GNN aggregation sums over these lists in fp32.
-__global__ void plan_sort_kernel(const int* __restrict__ dst_ptr, long num_nodes, int* __restrict__ dst_rows,
+// arbitrary order, and the max / the GNN aggregation read these lists in order.
+__global__ void plan_sort_kernel(const int* __restrict__ dst_ptr, long num_nodes, int* __restrict__ csr_e,
                                  int* __restrict__ nbr_local) {
     long v = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (v >= num_nodes) return;
     const int beg = dst_ptr[v], end = dst_ptr[v + 1];
     for (int a = beg + 1; a < end; ++a) {
-        int kn = nbr_local[a], kr = dst_rows[a];
+        int kn = nbr_local[a], ke = csr_e[a];
         int b = a - 1;
-        while (b >= beg && nbr_local[b] > kn) {
+        while (b >= beg && (nbr_local[b] > kn || (nbr_local[b] == kn && csr_e[b] > ke))) {
             nbr_local[b + 1] = nbr_local[b];
-            dst_rows[b + 1] = dst_rows[b];
+            csr_e[b + 1] = csr_e[b];
             --b;
         }
         nbr_local[b + 1] = kn;
-        dst_rows[b + 1] = kr;
+        csr_e[b + 1] = ke;
     }
 }
 
-// out[v] = max_{in-edges} msg + root[v] + bias  -> RELU: relu(.) ; RESID: x[v] + 0.1 * (.)
+// CSR slot -> the 4 product rows (source node x corner cell) and the 4 basis weights
+__global__ void plan_expand_kernel(const int* __restrict__ src, const int* __restrict__ csr_e, long E,
+                                   const int* __restrict__ grp_e, const float* __restrict__ basis_e,
+                                   const int* __restrict__ rowid, int4* __restrict__ rows4,
+                                   float4* __restrict__ basis4) {
+    long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= E) return;
+    const int e = csr_e[p];
+    const int g = grp_e[e];
+    const long s = src[e];
+    int4 r;
+    r.x = rowid[s * NCELL + fpm::spline_cell(g, 0)];
+    r.y = rowid[s * NCELL + fpm::spline_cell(g, 1)];
+    r.z = rowid[s * NCELL + fpm::spline_cell(g, 2)];
+    r.w = rowid[s * NCELL + fpm::spline_cell(g, 3)];
+    rows4[p] = r;
+    basis4[p] = *(const float4*)(basis_e + 4 * (long)e);
+}
+
+// out[v] = max_{in-edges e} sum_s basis[e,s] * Y[row(src_e, cell_s)] + Y[root row v] + bias
+//   mode 0: relu(.) ; mode 1: xres[v] + 0.1 * (.)   (+ optional per-pair column scale on out_t)
+// One wave per node, 12 channels per lane (3 x 4 contiguous).
 template <typename T>
-__global__ __launch_bounds__(256) void segmax_kernel(const T* __restrict__ msg, const float* __restrict__ root,
-                                                     const float* __restrict__ bias, const int* __restrict__ dst_ptr,
-                                                     const int* __restrict__ dst_rows, long num_nodes, int nmax,
-                                                     const int* __restrict__ nvalid, int mode,
-                                                     const float* __restrict__ xres, const float* __restrict__ cscale,
-                                                     float* __restrict__ out_f, T* __restrict__ out_t) {
+__global__ __launch_bounds__(256) void combine_kernel(const T* __restrict__ Y, const int* __restrict__ cell_off,
+                                                      const float* __restrict__ bias,
+                                                      const int* __restrict__ dst_ptr, const int4* __restrict__ rows4,
+                                                      const float4* __restrict__ basis4, long num_nodes, int nmax,
+                                                      const int* __restrict__ nvalid, int mode,
+                                                      const float* __restrict__ xres, const float* __restrict__ cscale,
+                                                      float* __restrict__ out_f, T* __restrict__ out_t) {
     const int lane = threadIdx.x & 63;
-    long v = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const long v = (long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (v >= num_nodes) return;
     const int b = (int)(v / nmax), loc = (int)(v - (long)b * nmax);
     const bool valid = loc < nvalid[b];
     const int beg = dst_ptr[v], end = dst_ptr[v + 1];
+    const long root_row = (long)cell_off[25] + v;
+    float m[3][4];
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) m[t][j] = beg < end ? -INFINITY : 0.f;   // torch_scatter: empty -> 0
+    for (int e = beg; e < end; ++e) {
+        const int4 r = rows4[e];
+        const float4 bs = basis4[e];
+        const T* y0 = Y + (long)r.x * 768;
+        const T* y1 = Y + (long)r.y * 768;
+        const T* y2 = Y + (long)r.z * 768;
+        const T* y3 = Y + (long)r.w * 768;
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const int c0 = 4 * lane + 256 * t;
+            float a0[4], a1[4], a2[4], a3[4];
+            fpm::load4(y0 + c0, a0);
+            fpm::load4(y1 + c0, a1);
+            fpm::load4(y2 + c0, a2);
+            fpm::load4(y3 + c0, a3);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float msg = bs.x * a0[j];
+                msg = fmaf(bs.y, a1[j], msg);
+                msg = fmaf(bs.z, a2[j], msg);
+                msg = fmaf(bs.w, a3[j], msg);
+                m[t][j] = fmaxf(m[t][j], msg);
+            }
+        }
+    }
+    const T* yr = Y + root_row * 768;
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
         const int c0 = 4 * lane + 256 * t;
-        float m[4];
-        if (beg < end) {
-            m[0] = m[1] = m[2] = m[3] = -INFINITY;
-            for (int e = beg; e < end; ++e) {
-                const T* row = msg + (long)dst_rows[e] * 768 + c0;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) m[j] = fmaxf(m[j], fpm::to_f<T>(row[j]));
-            }
-        } else {
-            m[0] = m[1] = m[2] = m[3] = 0.f;   // torch_scatter max: empty segment -> 0
-        }
+        float rt[4];
+        fpm::load4(yr + c0, rt);
         float y[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            float o = (m[j] + root[v * 768 + c0 + j]) + bias[c0 + j];
+            float o = (m[t][j] + rt[j]) + bias[c0 + j];
             if (mode == 0) y[j] = fmaxf(o, 0.f);
             else y[j] = xres[v * 768 + c0 + j] + 0.1f * o;
             if (!valid) y[j] = 0.f;
         }
-        if (out_f) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) out_f[v * 768 + c0 + j] = y[j];
-        }
+        if (out_f) *(float4*)(out_f + v * 768 + c0) = make_float4(y[0], y[1], y[2], y[3]);
         if (out_t) {
+            float z[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                float z = cscale ? y[j] * cscale[(long)b * 768 + c0 + j] : y[j];
-                out_t[v * 768 + c0 + j] = fpm::from_f<T>(z);
-            }
+            for (int j = 0; j < 4; ++j) z[j] = cscale ? y[j] * cscale[(long)b * 768 + c0 + j] : y[j];
+            fpm::store4(out_t + v * 768 + c0, z);
         }
     }
 }
@@ -246,40 +372,50 @@ __global__ __launch_bounds__(256) void segmax_kernel(const T* __restrict__ msg, 
 }  // namespace
 
 extern "C" long fpm_spline_plan_bytes(long E, long num_nodes) {
-    long max_tiles = (E + fpm::GBM - 1) / fpm::GBM + 25;
-    return plan_layout(E, num_nodes, max_tiles).total + al(E * 16);
+    return plan_layout(E, num_nodes).total;
+}
+
+// Product-row workspace of fpm_spline_conv_fwd: max_rows x 768 operand-dtype values.
+extern "C" long fpm_spline_y_bytes(int dtype, long E, long num_nodes) {
+    return plan_max_rows(E, num_nodes) * 768L * (dtype == 0 ? 4 : 2);
 }
 
 extern "C" int fpm_spline_plan(const int* src, const int* dst, const float* pseudo, long E, long num_nodes, int nmax,
                                void* ws, long ws_bytes, void* stream) {
-    long max_tiles = (E + fpm::GBM - 1) / fpm::GBM + 25;
-    PlanLayout L = plan_layout(E, num_nodes, max_tiles);
-    FPM_CHECK_ARG(ws_bytes >= fpm_spline_plan_bytes(E, num_nodes), "spline_plan: workspace too small");
+    PlanLayout L = plan_layout(E, num_nodes);
+    FPM_CHECK_ARG(ws_bytes >= L.total, "spline_plan: workspace too small");
     FPM_CHECK_ARG(E > 0 && num_nodes > 0 && nmax > 0, "spline_plan: bad sizes");
+    FPM_CHECK_ARG(num_nodes * NCELL < (1L << 31) && L.max_rows < (1L << 31), "spline_plan: batch too large");
     char* w = (char*)ws;
     hipStream_t st = (hipStream_t)stream;
-    float* basis_tmp = (float*)(w + L.total);
-    (void)hipMemsetAsync(w + L.cnt, 0, 32 * 4, st);
+    (void)hipMemsetAsync(w + L.mask, 0, num_nodes * 4, st);
     (void)hipMemsetAsync(w + L.indeg, 0, num_nodes * 4, st);
-    int blocks = (int)((E + 255) / 256);
-    hipLaunchKernelGGL(plan_count_kernel, dim3(blocks), dim3(256), 0, st, src, dst, pseudo, E, (int*)(w + L.cnt),
-                       (int*)(w + L.slot), (int*)(w + L.dslot), (int*)(w + L.gidx), (int*)(w + L.indeg), basis_tmp);
-    hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, st, (const int*)(w + L.cnt), (int*)(w + L.grp_off),
-                       (int*)(w + L.tile_info), (int)max_tiles, (const int*)(w + L.indeg), (int*)(w + L.dst_ptr),
-                       num_nodes);
-    hipLaunchKernelGGL(plan_fill_kernel, dim3(blocks), dim3(256), 0, st, src, dst, E, nmax, (const int*)(w + L.grp_off),
-                       (const int*)(w + L.slot), (const int*)(w + L.dslot), (const int*)(w + L.gidx),
-                       (const int*)(w + L.dst_ptr), (const float*)basis_tmp, (int*)(w + L.rows_src),
-                       (float*)(w + L.rows_basis), (int*)(w + L.dst_rows), (int*)(w + L.nbr_local));
+    const unsigned eblocks = (unsigned)((E + 255) / 256);
+    const unsigned nblocks = (unsigned)L.nblk;
+    hipLaunchKernelGGL(plan_edge_kernel, dim3(eblocks), dim3(256), 0, st, src, dst, pseudo, E, (int*)(w + L.mask),
+                       (int*)(w + L.indeg), (int*)(w + L.dslot), (float*)(w + L.basis_e), (int*)(w + L.grp_e));
+    hipLaunchKernelGGL(plan_blkcount_kernel, dim3(nblocks), dim3(256), 0, st, (const int*)(w + L.mask), num_nodes,
+                       (int*)(w + L.blk_cnt));
+    hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, st, (int*)(w + L.blk_cnt), L.nblk,
+                       (int*)(w + L.cell_off), (int*)(w + L.tile_info), (int)L.max_tiles, (const int*)(w + L.indeg),
+                       (int*)(w + L.dst_ptr), num_nodes);
+    hipLaunchKernelGGL(plan_rank_kernel, dim3(nblocks), dim3(256), 0, st, (const int*)(w + L.mask), num_nodes,
+                       (const int*)(w + L.blk_cnt), (const int*)(w + L.cell_off), (int*)(w + L.rowid),
+                       (int*)(w + L.arows));
+    hipLaunchKernelGGL(plan_fill_kernel, dim3(eblocks), dim3(256), 0, st, src, dst, E, nmax,
+                       (const int*)(w + L.dslot), (const int*)(w + L.dst_ptr), (int*)(w + L.csr_e),
+                       (int*)(w + L.nbr_local));
     hipLaunchKernelGGL(plan_sort_kernel, dim3((unsigned)((num_nodes + 255) / 256)), dim3(256), 0, st,
-                       (const int*)(w + L.dst_ptr), num_nodes, (int*)(w + L.dst_rows), (int*)(w + L.nbr_local));
+                       (const int*)(w + L.dst_ptr), num_nodes, (int*)(w + L.csr_e), (int*)(w + L.nbr_local));
+    hipLaunchKernelGGL(plan_expand_kernel, dim3(eblocks), dim3(256), 0, st, src, (const int*)(w + L.csr_e), E,
+                       (const int*)(w + L.grp_e), (const float*)(w + L.basis_e), (const int*)(w + L.rowid),
+                       (int4*)(w + L.rows4), (float4*)(w + L.basis4));
     return fpm::check_launch("fpm_spline_plan");
 }
 
 // Pointers into the plan for the GNN layer (dst CSR with local neighbour indices).
 extern "C" int fpm_spline_plan_csr(void* ws, long E, long num_nodes, int** dst_ptr, int** nbr_local) {
-    long max_tiles = (E + fpm::GBM - 1) / fpm::GBM + 25;
-    PlanLayout L = plan_layout(E, num_nodes, max_tiles);
+    PlanLayout L = plan_layout(E, num_nodes);
     *dst_ptr = (int*)((char*)ws + L.dst_ptr);
     *nbr_local = (int*)((char*)ws + L.nbr_local);
     return 0;
@@ -288,50 +424,46 @@ extern "C" int fpm_spline_plan_csr(void* ws, long E, long num_nodes, int** dst_p
 // One SplineConv layer over a whole side-batch.
 //   mode 0: out = relu(max_e msg + x R + b)            (conv 0 + F.relu, spline_conv.py:35)
 //   mode 1: out = xres + 0.1 * (max_e msg + x R + b)   (conv 1 + Siamese residual, :38, :56)
-// x_op: operand copy of the input (dtype); W: (25, 768 out, 768 in); R: (768 out, 768 in).
-// msg_ws: (E, 768) dtype; root_ws: (num_nodes, 768) f32.  cscale (B,768) optionally scales the
+// x_op: operand copy of the input (dtype); W: (26, 768 out, 768 in) = the 25 spline cells then the
+// root weight transposed.  y_ws: fpm_spline_y_bytes bytes.  cscale (B,768) optionally scales the
 // operand output (X o c for the vertex affinity, affinity_layer.py:15).
 extern "C" int fpm_spline_conv_fwd(int dtype, const void* x_op, const void* plan_ws, long E, long num_nodes, int nmax,
-                                   const int* nvalid, const void* W, const void* R, const float* bias, void* msg_ws,
-                                   float* root_ws, int mode, const float* xres, const float* cscale, float* out_f,
-                                   void* out_t, void* stream) {
+                                   const int* nvalid, const void* W, const float* bias, void* y_ws, long y_ws_bytes,
+                                   int mode, const float* xres, const float* cscale, float* out_f, void* out_t,
+                                   void* stream) {
     using namespace fpm;
     FPM_CHECK_ARG(dtype == 0 || dtype == 1, "spline_conv: bad dtype");
     FPM_CHECK_ARG(mode == 0 || (mode == 1 && xres), "spline_conv: mode 1 needs xres");
-    long max_tiles = (E + GBM - 1) / GBM + 25;
-    PlanLayout L = plan_layout(E, num_nodes, max_tiles);
+    FPM_CHECK_ARG(y_ws_bytes >= fpm_spline_y_bytes(dtype, E, num_nodes), "spline_conv: y workspace too small");
+    PlanLayout L = plan_layout(E, num_nodes);
     const char* w = (const char*)plan_ws;
     hipStream_t st = (hipStream_t)stream;
     const int D = 768;
-    // root term: x R  (fp32 out, bias added after the max like PyG: (max + xR) + b)
+    // all (node, cell) products in one grouped GEMM (group = cell, B = that cell's weight)
     {
         GemmParams p = {};
-        p.A = x_op; p.lda = D; p.B = R; p.ldb = D; p.M = (int)num_nodes; p.N = D; p.K = D; p.nseg = 1;
-        p.epi = EPI_STORE; p.Cf = root_ws; p.ldc = D;
-        dim3 grid(D / GBN, (unsigned)((num_nodes + GBM - 1) / GBM), 1);
-        if (dtype == 0) hipLaunchKernelGGL((gemm_kernel<float, false>), grid, dim3(GTHREADS), 0, st, p);
-        else hipLaunchKernelGGL((gemm_kernel<bf16_t, false>), grid, dim3(GTHREADS), 0, st, p);
-    }
-    // edge messages: grouped GEMM, K = 4 segments x 768
-    {
-        GemmParams p = {};
-        p.A = x_op; p.lda = D; p.a_rows = (const int*)(w + L.rows_src);
+        p.A = x_op; p.lda = D; p.a_rows = (const int*)(w + L.arows);
         p.B = W; p.ldb = D; p.sB_seg = (long)D * D;
-        p.row_scale = (const float*)(w + L.rows_basis);
-        p.M = (int)E; p.N = D; p.K = D; p.nseg = 4;
+        p.M = (int)L.max_rows; p.N = D; p.K = D; p.nseg = 1;
         p.tile_info = (const int*)(w + L.tile_info);
-        p.group_off = (const int*)(w + L.grp_off);
-        p.epi = EPI_STORE; p.Ct = msg_ws; p.ldc = D;
-        dim3 grid(D / GBN, (unsigned)max_tiles, 1);
-        ProfRec rec = {nullptr, nullptr, 2.0 * (double)E * 4.0 * D * D};
-        if (g_prof_on) {
+        p.group_off = (const int*)(w + L.cell_off);
+        p.epi = EPI_STORE; p.ldc = D;
+        if (dtype == 0) p.Cf = (float*)y_ws;
+        else p.Ct = y_ws;
+        p.remap_mtiles = (int)L.max_tiles;
+        dim3 grid(remap_grid(D, (int)L.max_tiles), 1, 1);
+        ProfRec rec = {nullptr, nullptr, (int)g_prof.size()};
+        if (g_prof_on && !g_prof_rows) (void)hipMalloc(&g_prof_rows, PROF_MAX * sizeof(int));
+        if (g_prof_on && g_prof_rows && rec.slot < PROF_MAX) {
+            (void)hipMemcpyAsync(g_prof_rows + rec.slot, w + L.cell_off + NCELL * sizeof(int), sizeof(int),
+                                 hipMemcpyDeviceToDevice, st);
             (void)hipEventCreate(&rec.a);
             (void)hipEventCreate(&rec.b);
             (void)hipEventRecord(rec.a, st);
         }
-        if (dtype == 0) hipLaunchKernelGGL((gemm_kernel<float, true>), grid, dim3(GTHREADS), 0, st, p);
-        else hipLaunchKernelGGL((gemm_kernel<bf16_t, true>), grid, dim3(GTHREADS), 0, st, p);
-        if (g_prof_on) {
+        if (dtype == 0) hipLaunchKernelGGL((gemm_kernel<float, false>), grid, dim3(GTHREADS), 0, st, p);
+        else hipLaunchKernelGGL((gemm_kernel<bf16_t, false>), grid, dim3(GTHREADS), 0, st, p);
+        if (g_prof_on && g_prof_rows && rec.slot < PROF_MAX) {
             (void)hipEventRecord(rec.b, st);
             g_prof.push_back(rec);
         }
@@ -339,12 +471,14 @@ extern "C" int fpm_spline_conv_fwd(int dtype, const void* x_op, const void* plan
     {
         dim3 grid((unsigned)((num_nodes + 3) / 4));
         if (dtype == 0)
-            hipLaunchKernelGGL((segmax_kernel<float>), grid, dim3(256), 0, st, (const float*)msg_ws, root_ws, bias,
-                               (const int*)(w + L.dst_ptr), (const int*)(w + L.dst_rows), num_nodes, nmax, nvalid,
+            hipLaunchKernelGGL((combine_kernel<float>), grid, dim3(256), 0, st, (const float*)y_ws,
+                               (const int*)(w + L.cell_off), bias, (const int*)(w + L.dst_ptr),
+                               (const int4*)(w + L.rows4), (const float4*)(w + L.basis4), num_nodes, nmax, nvalid,
                                mode, xres, cscale, out_f, (float*)out_t);
         else
-            hipLaunchKernelGGL((segmax_kernel<bf16_t>), grid, dim3(256), 0, st, (const bf16_t*)msg_ws, root_ws, bias,
-                               (const int*)(w + L.dst_ptr), (const int*)(w + L.dst_rows), num_nodes, nmax, nvalid,
+            hipLaunchKernelGGL((combine_kernel<bf16_t>), grid, dim3(256), 0, st, (const bf16_t*)y_ws,
+                               (const int*)(w + L.cell_off), bias, (const int*)(w + L.dst_ptr),
+                               (const int4*)(w + L.rows4), (const float4*)(w + L.basis4), num_nodes, nmax, nvalid,
                                mode, xres, cscale, out_f, (bf16_t*)out_t);
     }
     return check_launch("fpm_spline_conv_fwd");
@@ -383,8 +517,13 @@ extern "C" int fpm_profile_read(double* ms_total, double* flops_total, int* coun
             fpm::set_error("fpm_profile_read: event query failed");
             return 2;
         }
+        int rows = 0;
+        if (hipMemcpy(&rows, g_prof_rows + r.slot, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) {
+            fpm::set_error("fpm_profile_read: row count read failed");
+            return 2;
+        }
         ms += t;
-        fl += r.flops;
+        fl += 2.0 * rows * 768.0 * 768.0;
         (void)hipEventDestroy(r.a);
         (void)hipEventDestroy(r.b);
     }

@@ -64,6 +64,7 @@ class Net(nn.Module):
         self._pack_key = None
         self._pinned = None
         self._stream_cache = {}
+        self.two_streams = os.environ.get("FPM_STREAMS", "2") != "1"
         self._keep_feats = False
         self._stage_timing = os.environ.get("FPM_STAGE_TIMING", "0") == "1"
         self.stage_times = {}
@@ -90,8 +91,9 @@ class Net(nn.Module):
         g = lambda k: sd[k].to(device=device, dtype=torch.float32).contiguous()
         for l in range(2):
             pre = "%s.%d" % (P.SPLINE_PREFIX, l)
-            d["W%d" % l] = sd[pre + ".weight"].to(device).transpose(1, 2).contiguous().to(op)   # [cell][out][in]
-            d["R%d" % l] = sd[pre + ".root"].to(device).t().contiguous().to(op)                # [out][in]
+            # [cell][out][in] for the 25 spline cells, then the root weight as cell 25
+            d["W%d" % l] = torch.cat([sd[pre + ".weight"].to(device).transpose(1, 2),
+                                      sd[pre + ".root"].to(device).t()[None]]).contiguous().to(op)
             d["bias%d" % l] = g(pre + ".bias")
         d["aff_w"] = g("vertex_affinity.A.weight")          # [768][1024] = N x K
         d["aff_b"] = g("vertex_affinity.A.bias")
@@ -147,15 +149,13 @@ class Net(nn.Module):
         plan = ops.spline_plan(bt.src[side], bt.dst[side], bt.pseudo[side], nn_, bt.nmax[side])
         x0 = bt.x[side]
         x_op = ops.cast_bf16(x0) if op == torch.bfloat16 else x0
-        msg = torch.empty(max(E, 1), C.NODE_FEATURE_DIM, device=dev, dtype=op)
-        root = torch.empty(nn_, C.NODE_FEATURE_DIM, device=dev, dtype=torch.float32)
+        yws = ops.spline_y_ws(ops.BF16 if op == torch.bfloat16 else ops.F32, E, nn_, dev)
         h = torch.empty(nn_, C.NODE_FEATURE_DIM, device=dev, dtype=op)
-        ops.spline_conv(x_op, plan, E, nn_, bt.nmax[side], bt.n[side], wp["W0"], wp["R0"], wp["bias0"], msg, root,
-                        0, out_t=h)
+        ops.spline_conv(x_op, plan, E, nn_, bt.nmax[side], bt.n[side], wp["W0"], wp["bias0"], yws, 0, out_t=h)
         out = torch.empty(nn_, C.NODE_FEATURE_DIM, device=dev, dtype=op)
         outf = torch.empty(nn_, C.NODE_FEATURE_DIM, device=dev, dtype=torch.float32) if self._keep_feats else None
-        ops.spline_conv(h, plan, E, nn_, bt.nmax[side], bt.n[side], wp["W1"], wp["R1"], wp["bias1"], msg, root,
-                        1, xres=x0, cscale=cscale, out_f=outf, out_t=out)
+        ops.spline_conv(h, plan, E, nn_, bt.nmax[side], bt.n[side], wp["W1"], wp["bias1"], yws, 1, xres=x0,
+                        cscale=cscale, out_f=outf, out_t=out)
         return plan, out, outf
 
     def _afau(self, wp, ss, bt):
@@ -327,7 +327,7 @@ class Net(nn.Module):
         main = torch.cuda.current_stream(dev)
         ev_start = torch.cuda.Event(enable_timing=True)
         ev_start.record(main)
-        streams = self._streams(dev) if len(parts) > 1 else [main]
+        streams = self._streams(dev) if (len(parts) > 1 and self.two_streams) else [main]
         for st in streams:
             if st is not main:
                 st.wait_event(ev_start)

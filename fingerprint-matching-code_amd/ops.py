@@ -111,13 +111,21 @@ def plan_csr(ws, E, num_nodes):
     return a.value, b.value
 
 
-def spline_conv(x_op, plan, E, num_nodes, nmax, nvalid, W, R, bias, msg_ws, root_ws, mode, xres=None, cscale=None,
-                out_f=None, out_t=None):
-    _dev(x_op, plan, W, R, bias, msg_ws, root_ws)
+def spline_y_ws(dtype_code, E, num_nodes, device):
+    """Product-row scratch for spline_conv (shared by both layers of a side)."""
+    nbytes = _lib.load().fpm_spline_y_bytes(dtype_code, E, num_nodes)
+    return torch.empty(nbytes, device=device, dtype=torch.uint8)
+
+
+def spline_conv(x_op, plan, E, num_nodes, nmax, nvalid, W, bias, y_ws, mode, xres=None, cscale=None, out_f=None,
+                out_t=None):
+    """W: (26, 768, 768) = spline cells [cell][out][in] then root^T."""
+    _dev(x_op, plan, W, bias, y_ws)
     code = _code(x_op)
-    _lib.call("fpm_spline_conv_fwd", code, _p(x_op), _p(plan), E, num_nodes, nmax, _p(nvalid), _p(W), _p(R),
-              _p(bias), _p(msg_ws), _p(root_ws), int(mode), _p(xres), _p(cscale), _p(out_f), _p(out_t),
-              _stream(x_op))
+    if _code(W) != code or tuple(W.shape) != (26, 768, 768):
+        raise _lib.FpmError("spline_conv: W must be (26, 768, 768) in the operand dtype")
+    _lib.call("fpm_spline_conv_fwd", code, _p(x_op), _p(plan), E, num_nodes, nmax, _p(nvalid), _p(W), _p(bias),
+              _p(y_ws), y_ws.numel(), int(mode), _p(xres), _p(cscale), _p(out_f), _p(out_t), _stream(x_op))
 
 
 def edge_diff(x, src, dst):

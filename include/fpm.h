@@ -65,17 +65,20 @@ int fpm_cast_bf16(const float* x, void* y, long n, void* stream);
 /* ---- SplineConv message passing ---------------------------------------------------------------
  * Replaces PyG 1.6.3 SplineConv(768, 768, dim=2, kernel_size=5, aggr='max') inside SConv /
  * SiameseSConvOnNodes (src/model/spline_conv.py:17, 28-57).
- * fpm_spline_plan: bucket the side-batch's edges by B-spline group (device workspace of
- * fpm_spline_plan_bytes bytes; reused by both layers and by the GNN layer's CSR).
- * fpm_spline_conv_fwd: one layer; mode 0 -> relu(conv(x)), mode 1 -> xres + 0.1 * conv(x). */
+ * fpm_spline_plan: per-node cell masks, (node, cell) product rows ranked per cell, GEMM tile table
+ * and the dst CSR (device workspace of fpm_spline_plan_bytes bytes; reused by both layers and by
+ * the GNN layer's CSR).
+ * fpm_spline_conv_fwd: one layer; mode 0 -> relu(conv(x)), mode 1 -> xres + 0.1 * conv(x).
+ * W: (26, 768 out, 768 in) = the 25 spline-cell weights transposed, then the root weight
+ * transposed; y_ws: fpm_spline_y_bytes(dtype, E, num_nodes) bytes of product-row scratch. */
 long fpm_spline_plan_bytes(long E, long num_nodes);
+long fpm_spline_y_bytes(int dtype, long E, long num_nodes);
 int fpm_spline_plan(const int* src, const int* dst, const float* pseudo, long E, long num_nodes, int nmax, void* ws,
                     long ws_bytes, void* stream);
 int fpm_spline_plan_csr(void* ws, long E, long num_nodes, int** dst_ptr, int** nbr_local);
 int fpm_spline_conv_fwd(int dtype, const void* x_op, const void* plan_ws, long E, long num_nodes, int nmax,
-                        const int* nvalid, const void* W, const void* R, const float* bias, void* msg_ws,
-                        float* root_ws, int mode, const float* xres, const float* cscale, float* out_f, void* out_t,
-                        void* stream);
+                        const int* nvalid, const void* W, const float* bias, void* y_ws, long y_ws_bytes, int mode,
+                        const float* xres, const float* cscale, float* out_f, void* out_t, void* stream);
 /* vertex_attr_to_edge_attr (spline_conv.py:73-81): out[e] = x[src[e]] - x[dst[e]] */
 int fpm_edge_diff(const float* x, const int* src, const int* dst, long E, int D, float* out, void* stream);
 
