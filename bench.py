@@ -167,7 +167,7 @@ def main():
                        "edges_per_graph": E_tot / (2.0 * args.batch), "parallelism": "pair-sharded x%d" % world},
             "gpu_stage_pairs_per_s": args.batch * world * args.steps / gpu_s,
             "host_lsa_ms_per_step": lsa_s / args.steps * 1e3,
-            "roofline": {"kernel": "spline (node, cell) product GEMM (gemm_kernel<%s>, grouped by cell)" % args.dtype,
+            "roofline": {"kernel": "spline (node, cell) product GEMM (%s, grouped by cell)" % ("gemm256_bf16_kernel" if args.dtype == "bf16" else "gemm_kernel<f32>"),
                          "bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak, "traffic": None,
                          "launches": cnt.value, "avg_launch_ms": ms.value / max(cnt.value, 1),

@@ -8,12 +8,12 @@
 // cells), so each needed (node, cell) product is computed ONCE: the plan marks a 26-bit cell mask
 // per node (25 spline cells + the root weight as cell 25), ranks the (node, cell) rows per cell in
 // node order, and one grouped MFMA GEMM (group = cell, A = gathered node rows, B = that cell's
-// [out][in] weight) writes the product rows Y.  A combine kernel then forms each in-edge's message
+// [out][in] weight; bf16: the 256x256 LDS-DMA tile of gemm_big.h) writes the product rows Y.  A combine kernel then forms each in-edge's message
 // from 4 rows of Y in fp32 (basis order s = 0..3, the reference's), takes the max per destination
 // and fuses root + bias + ReLU or the Siamese residual.  That is ~2.5x fewer MFMA flops than the
 // per-edge GEMM, and the message tensor is never materialised.  The plan (dst CSR included) is
 // built on device once per side and shared by both layers and the GNN layers.
-#include "gemm_core.h"
+#include "gemm_big.h"
 
 #include <vector>
 
@@ -32,9 +32,9 @@ constexpr int PROF_MAX = 4096;
 constexpr int NCELL = 26;   // 25 B-spline cells + the root weight (cell 25)
 
 struct PlanLayout {
-    long mask, indeg, dslot, basis_e, grp_e, blk_cnt, cell_off, rowid, arows, tile_info, dst_ptr, csr_e, nbr_local,
-        rows4, basis4, total;
-    long nblk, max_rows, max_tiles;
+    long mask, indeg, dslot, basis_e, grp_e, blk_cnt, cell_off, rowid, arows, tile_info, tile_info2, dst_ptr, csr_e,
+        nbr_local, rows4, basis4, total;
+    long nblk, max_rows, max_tiles, max_tiles2;
 };
 
 __host__ __device__ inline long al(long x) { return (x + 255) & ~255L; }
@@ -50,7 +50,8 @@ PlanLayout plan_layout(long E, long num_nodes) {
     PlanLayout L;
     L.nblk = (num_nodes + 255) / 256;
     L.max_rows = plan_max_rows(E, num_nodes);
-    L.max_tiles = L.max_rows / fpm::GBM + NCELL + 1;
+    L.max_tiles = L.max_rows / fpm::GBM + NCELL + 1;      // 128-row tiles (fp32 kernel)
+    L.max_tiles2 = L.max_rows / fpm::G2_BM + NCELL + 1;   // 256-row tiles (bf16 kernel)
     long o = 0;
     L.mask = o; o += al(num_nodes * 4);
     L.indeg = o; o += al(num_nodes * 4);
@@ -62,6 +63,7 @@ PlanLayout plan_layout(long E, long num_nodes) {
     L.rowid = o; o += al(num_nodes * NCELL * 4);
     L.arows = o; o += al(L.max_rows * 4);
     L.tile_info = o; o += al(L.max_tiles * 8);
+    L.tile_info2 = o; o += al(L.max_tiles2 * 8);
     L.dst_ptr = o; o += al((num_nodes + 1) * 4);
     L.csr_e = o; o += al(E * 4);
     L.nbr_local = o; o += al(E * 4);
@@ -128,15 +130,40 @@ __global__ __launch_bounds__(256) void plan_blkcount_kernel(const int* __restric
 
 // one block: per-cell exclusive scan over blocks (in place), cell offsets, GEMM tile table, and the
 // exclusive scan of in-degrees -> dst CSR pointers.
+__device__ void build_tile_table(const int* coff, const int* cell_tot, int* tile_off, int tb, int* tile_info,
+                                 int max_tiles) {
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        int t = 0;
+        for (int k = 0; k < NCELL; ++k) {
+            tile_off[k] = t;
+            t += (cell_tot[k] + tb - 1) / tb;
+        }
+        tile_off[NCELL] = t;
+    }
+    __syncthreads();
+    for (int t = tid; t < max_tiles; t += blockDim.x) {
+        int g = -1, r0 = 0;
+        if (t < tile_off[NCELL]) {
+            int k = 0;
+            while (tile_off[k + 1] <= t) ++k;
+            g = k;
+            r0 = coff[k] + (t - tile_off[k]) * tb;
+        }
+        tile_info[2 * t] = g;
+        tile_info[2 * t + 1] = r0;
+    }
+    __syncthreads();
+}
+
 __global__ __launch_bounds__(1024) void plan_scan_kernel(int* blk_cnt, long nblk, int* cell_off, int* tile_info,
-                                                         int max_tiles, const int* indeg, int* dst_ptr,
-                                                         long num_nodes) {
+                                                         int max_tiles, int* tile_info2, int max_tiles2,
+                                                         const int* indeg, int* dst_ptr, long num_nodes) {
     __shared__ int part[1024];
     __shared__ int tilebuf[16384];
     __shared__ int cell_tot[NCELL], tile_off[NCELL + 1], coff[NCELL + 1];
     const int tid = threadIdx.x;
-    // (1) per-cell scans over blocks: 26 cells in parallel groups of threads would need a 2-D
-    //     scan; nblk <= a few thousand, so one pass per cell with the block-wide scan is enough.
+    // (1) per-cell scans over blocks (nblk is at most a few thousand: one block-wide scan per cell)
     for (int k = 0; k < NCELL; ++k) {
         int carry = 0;
         for (long t0 = 0; t0 < nblk; t0 += 1024) {
@@ -158,29 +185,18 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(int* blk_cnt, long nblk
     }
     __syncthreads();
     if (tid == 0) {
-        int off = 0, t = 0;
+        int off = 0;
         for (int k = 0; k < NCELL; ++k) {
             cell_off[k] = off;
             coff[k] = off;
-            tile_off[k] = t;
             off += cell_tot[k];
-            t += (cell_tot[k] + fpm::GBM - 1) / fpm::GBM;
         }
         cell_off[NCELL] = off;
-        tile_off[NCELL] = t;
+        coff[NCELL] = off;
     }
     __syncthreads();
-    for (int t = tid; t < max_tiles; t += 1024) {
-        int g = -1, r0 = 0;
-        if (t < tile_off[NCELL]) {
-            int k = 0;
-            while (tile_off[k + 1] <= t) ++k;
-            g = k;
-            r0 = coff[k] + (t - tile_off[k]) * fpm::GBM;
-        }
-        tile_info[2 * t] = g;
-        tile_info[2 * t + 1] = r0;
-    }
+    build_tile_table(coff, cell_tot, tile_off, fpm::GBM, tile_info, max_tiles);
+    build_tile_table(coff, cell_tot, tile_off, fpm::G2_BM, tile_info2, max_tiles2);
     // (2) exclusive scan of indeg -> dst_ptr, tiled through LDS (coalesced global reads/writes)
     constexpr int TILE = 16384, PER = TILE / 1024;
     int* buf = tilebuf;
@@ -397,8 +413,8 @@ extern "C" int fpm_spline_plan(const int* src, const int* dst, const float* pseu
     hipLaunchKernelGGL(plan_blkcount_kernel, dim3(nblocks), dim3(256), 0, st, (const int*)(w + L.mask), num_nodes,
                        (int*)(w + L.blk_cnt));
     hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, st, (int*)(w + L.blk_cnt), L.nblk,
-                       (int*)(w + L.cell_off), (int*)(w + L.tile_info), (int)L.max_tiles, (const int*)(w + L.indeg),
-                       (int*)(w + L.dst_ptr), num_nodes);
+                       (int*)(w + L.cell_off), (int*)(w + L.tile_info), (int)L.max_tiles, (int*)(w + L.tile_info2),
+                       (int)L.max_tiles2, (const int*)(w + L.indeg), (int*)(w + L.dst_ptr), num_nodes);
     hipLaunchKernelGGL(plan_rank_kernel, dim3(nblocks), dim3(256), 0, st, (const int*)(w + L.mask), num_nodes,
                        (const int*)(w + L.blk_cnt), (const int*)(w + L.cell_off), (int*)(w + L.rowid),
                        (int*)(w + L.arows));
@@ -450,8 +466,9 @@ extern "C" int fpm_spline_conv_fwd(int dtype, const void* x_op, const void* plan
         p.epi = EPI_STORE; p.ldc = D;
         if (dtype == 0) p.Cf = (float*)y_ws;
         else p.Ct = y_ws;
-        p.remap_mtiles = (int)L.max_tiles;
-        dim3 grid(remap_grid(D, (int)L.max_tiles), 1, 1);
+        p.remap_mtiles = (int)(dtype == 0 ? L.max_tiles : L.max_tiles2);
+        if (dtype == 1) p.tile_info = (const int*)(w + L.tile_info2);
+        dim3 grid(dtype == 0 ? remap_grid(D, p.remap_mtiles) : remap_grid256(D, p.remap_mtiles), 1, 1);
         ProfRec rec = {nullptr, nullptr, (int)g_prof.size()};
         if (g_prof_on && !g_prof_rows) (void)hipMalloc(&g_prof_rows, PROF_MAX * sizeof(int));
         if (g_prof_on && g_prof_rows && rec.slot < PROF_MAX) {
@@ -462,7 +479,7 @@ extern "C" int fpm_spline_conv_fwd(int dtype, const void* x_op, const void* plan
             (void)hipEventRecord(rec.a, st);
         }
         if (dtype == 0) hipLaunchKernelGGL((gemm_kernel<float, false>), grid, dim3(GTHREADS), 0, st, p);
-        else hipLaunchKernelGGL((gemm_kernel<bf16_t, false>), grid, dim3(GTHREADS), 0, st, p);
+        else hipLaunchKernelGGL(gemm256_bf16_kernel, grid, dim3(G2_THREADS), 0, st, p);
         if (g_prof_on && g_prof_rows && rec.slot < PROF_MAX) {
             (void)hipEventRecord(rec.b, st);
             g_prof.push_back(rec);

@@ -1,0 +1,94 @@
+// Micro-benchmark of the SplineConv product GEMM shapes: 128x128 register-staged kernel
+// (gemm_core.h) vs the 256x256 LDS-DMA kernel (gemm_big.h); checks the outputs are identical.
+// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I fingerprint-matching-code_amd/csrc tools/gemm_bench.hip
+#include "gemm_big.h"
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <random>
+#include <algorithm>
+#include <cstring>
+
+namespace fpm {
+void set_error(const char*, ...) {}
+int check_launch(const char*) { return 0; }
+}
+using namespace fpm;
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+
+static uint16_t h_f2bf(float f) { uint32_t u; memcpy(&u, &f, 4); u += 0x7FFF + ((u >> 16) & 1); return (uint16_t)(u >> 16); }
+
+int main(int argc, char** argv) {
+    const int Nn = 32768, D = 768, NC = 26;
+    std::mt19937 rng(1);
+    std::uniform_real_distribution<float> U(-1.f, 1.f);
+    std::vector<uint16_t> hx((size_t)Nn * D), hw((size_t)NC * D * D);
+    for (auto& v : hx) v = h_f2bf(U(rng));
+    for (auto& v : hw) v = h_f2bf(U(rng) * 0.05f);
+    // cell row sets: 9 dense cells (~97% of nodes), 8 sparse cells, root = all nodes
+    std::vector<int> arows, goff(NC + 1);
+    std::uniform_real_distribution<float> P(0.f, 1.f);
+    for (int c = 0; c < NC; ++c) {
+        goff[c] = (int)arows.size();
+        float pr = c == 25 ? 1.f : ((c % 5 >= 1 && c % 5 <= 3 && c / 5 >= 1 && c / 5 <= 3) ? 0.97f : 0.002f);
+        for (int u = 0; u < Nn; ++u) if (P(rng) < pr) arows.push_back(u);
+    }
+    goff[NC] = (int)arows.size();
+    const int rows = goff[NC];
+    auto table = [&](int tb) {
+        std::vector<int> t;
+        for (int c = 0; c < NC; ++c)
+            for (int r = goff[c]; r < goff[c + 1]; r += tb) { t.push_back(c); t.push_back(r); }
+        int real = (int)t.size() / 2;
+        int maxt = rows / tb + NC + 1;
+        for (int i = real; i < maxt; ++i) { t.push_back(-1); t.push_back(0); }
+        return t;
+    };
+    auto t128 = table(128), t256 = table(256);
+    printf("rows %d  tiles128 %zu tiles256 %zu\n", rows, t128.size() / 2, t256.size() / 2);
+    uint16_t *dx, *dw, *c1, *c2;
+    int *darows, *dgoff, *dt128, *dt256;
+    CK(hipMalloc(&dx, hx.size() * 2)); CK(hipMalloc(&dw, hw.size() * 2));
+    CK(hipMalloc(&c1, (size_t)rows * D * 2)); CK(hipMalloc(&c2, (size_t)rows * D * 2));
+    CK(hipMalloc(&darows, arows.size() * 4)); CK(hipMalloc(&dgoff, goff.size() * 4));
+    CK(hipMalloc(&dt128, t128.size() * 4)); CK(hipMalloc(&dt256, t256.size() * 4));
+    CK(hipMemcpy(dx, hx.data(), hx.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dw, hw.data(), hw.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(darows, arows.data(), arows.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dgoff, goff.data(), goff.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dt128, t128.data(), t128.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dt256, t256.data(), t256.size() * 4, hipMemcpyHostToDevice));
+    GemmParams p = {};
+    p.A = dx; p.lda = D; p.a_rows = darows; p.B = dw; p.ldb = D; p.sB_seg = (long)D * D;
+    p.M = rows; p.N = D; p.K = D; p.nseg = 1; p.group_off = dgoff; p.epi = EPI_STORE; p.ldc = D;
+    GemmParams p1 = p, p2 = p;
+    p1.tile_info = dt128; p1.Ct = c1; p1.remap_mtiles = (int)t128.size() / 2;
+    p2.tile_info = dt256; p2.Ct = c2; p2.remap_mtiles = (int)t256.size() / 2;
+    dim3 g1(remap_grid(D, p1.remap_mtiles)), g2(remap_grid256(D, p2.remap_mtiles));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    const double flops = 2.0 * rows * (double)D * D;
+    const int reps = 20;
+    for (int round = 0; round < 3; ++round) {
+        for (int v = 0; v < 2; ++v) {
+            CK(hipEventRecord(e0));
+            for (int r = 0; r < reps; ++r) {
+                if (v == 0) hipLaunchKernelGGL((gemm_kernel<bf16_t, false>), g1, dim3(GTHREADS), 0, 0, p1);
+                else hipLaunchKernelGGL(gemm256_bf16_kernel, g2, dim3(G2_THREADS), 0, 0, p2);
+            }
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+            ms /= reps;
+            printf("round %d %-10s %.4f ms  %.1f TF/s\n", round, v ? "256x256" : "128x128", ms, flops / ms / 1e9);
+        }
+    }
+    std::vector<uint16_t> h1((size_t)rows * D), h2((size_t)rows * D);
+    CK(hipMemcpy(h1.data(), c1, h1.size() * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(h2.data(), c2, h2.size() * 2, hipMemcpyDeviceToHost));
+    size_t diff = 0;
+    for (size_t i = 0; i < h1.size(); ++i) diff += h1[i] != h2[i];
+    printf("mismatching elements: %zu of %zu\n", diff, h1.size());
+    return diff != 0;
+}
