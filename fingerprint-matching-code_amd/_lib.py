@@ -30,6 +30,7 @@ SIGNATURES = {
     "fpm_spline_y_bytes": (L, [I, L, L]),
     "fpm_spline_conv_fwd": (I, [I, P, P, L, L, I, P, P, P, P, L, I, P, P, P, P, P]),
     "fpm_edge_diff": (I, [P, P, P, L, I, P, P]),
+    "fpm_edge_diff_padded": (I, [P, P, P, P, P, P, L, I, P, P]),
     "fpm_kron_gnn_layer_fwd": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, P, P]),
     "fpm_gnn_param_count": (I, [I]),
     "fpm_node_classifier": (I, [P, I, I, I, P, P, P, P]),
@@ -39,6 +40,15 @@ SIGNATURES = {
     "fpm_match_cls_ws_floats": (L, [I, I, I]),
     "fpm_match_cls_fwd": (I, [P, P, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),
     "fpm_lsa_batch_host": (I, [P, L, L, P, P, I, I, P, I]),
+    "fpm_csr_dot_csc_to_dense": (I, [I, P, P, P, P, P, P, L, L, L, P, P]),
+    "fpm_dense_dot_csc_to_dense": (I, [I, P, P, P, P, L, L, L, L, P, P]),
+    "fpm_csr_dot_diag_to_csr": (I, [I, P, P, P, P, L, L, L, P, P]),
+    "fpm_bilinear_diag": (I, [I, P, P, P, P, L, P, P, P, L, L, P, P]),
+    "fpm_csr_dot_csc_to_csr_host": (L, [I, P, P, P, P, P, P, L, L, L, P, L, P, P]),
+    "fpm_csr_dot_diag_to_csr_host": (I, [I, P, P, P, P, L, L, L, P]),
+    "fpm_bilinear_diag_host": (I, [I, P, P, P, P, L, P, P, P, L, L, P]),
+    "fpm_gconv_ws_floats": (L, [I, I, I]),
+    "fpm_gconv_fwd": (I, [P, P, I, I, I, I, P, P, I, P, P, P]),
     "fpm_profile_enable": (I, [I]),
     "fpm_profile_read": (I, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(I)]),

@@ -11,7 +11,9 @@ extern "C" int fpm_gemm(int dtype, const void* A, long lda, long sA, const int* 
     FPM_CHECK_ARG(M >= 0 && N > 0 && K > 0 && batch >= 0, "gemm: bad sizes M=%d N=%d K=%d", M, N, K);
     FPM_CHECK_ARG(K % (dtype ? 8 : 4) == 0, "gemm: K=%d must be a multiple of %d", K, dtype ? 8 : 4);
     FPM_CHECK_ARG(lda % (dtype ? 8 : 4) == 0 && ldb % (dtype ? 8 : 4) == 0, "gemm: lda/ldb must keep rows 16-B aligned");
-    FPM_CHECK_ARG(epi != EPI_AFFINITY || (n1 && n2), "gemm: affinity epilogue needs n1/n2");
+    FPM_CHECK_ARG((epi != EPI_AFFINITY && epi != EPI_HALF_AFFINITY) || (n1 && n2),
+                  "gemm: affinity epilogues need n1/n2");
+    FPM_CHECK_ARG(epi >= EPI_STORE && epi <= EPI_HALF_AFFINITY, "gemm: bad epilogue %d", epi);
     if (M == 0 || batch == 0) return 0;
     GemmParams p = {};
     p.A = A; p.lda = lda; p.sA = sA; p.a_rows = a_rows;

@@ -24,6 +24,7 @@ enum GemmEpi : int {
     EPI_RELU = 1,       // relu(v + bias)
     EPI_TANH = 2,       // tanh(v + bias)
     EPI_AFFINITY = 3,   // C[j][i] = (j < n2b && i < n1b) ? softplus(v) - 0.5 : 0  (per pair)
+    EPI_HALF_AFFINITY = 4,   // 0.5 * (softplus(v) - 0.5) on the same mask (quadratic Ke, ngm.py:289)
 };
 
 struct GemmParams {
@@ -246,7 +247,7 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_kernel(GemmParams p) {
     // epilogue
     const int epi = p.epi;
     int n1b = 0, n2b = 0;
-    if (epi == EPI_AFFINITY) { n1b = p.n1[batch]; n2b = p.n2[batch]; }
+    if (epi == EPI_AFFINITY || epi == EPI_HALF_AFFINITY) { n1b = p.n1[batch]; n2b = p.n2[batch]; }
     float* Cf = p.Cf ? p.Cf + (long)batch * p.sC : nullptr;
     T* Ct = p.Ct ? (T*)p.Ct + (long)batch * p.sC : nullptr;
 #pragma unroll
@@ -264,6 +265,7 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_kernel(GemmParams p) {
                 if (epi == EPI_RELU) v = fmaxf(v, 0.f);
                 else if (epi == EPI_TANH) v = tanhf(v);
                 else if (epi == EPI_AFFINITY) v = (r < n2b && n < n1b) ? softplus_f(v) - 0.5f : 0.f;
+                else if (epi == EPI_HALF_AFFINITY) v = (r < n2b && n < n1b) ? 0.5f * (softplus_f(v) - 0.5f) : 0.f;
                 long o = (long)r * p.ldc + n;
                 if (Cf) Cf[o] = v;
                 if (Ct) Ct[o] = from_f<T>(v);

@@ -512,7 +512,34 @@ __global__ void edge_diff_kernel(const float* __restrict__ x, const int* __restr
     const float* b = x + (long)dst[e] * D;
     for (int c = threadIdx.x; c < D; c += blockDim.x) out[e * D + c] = a[c] - b[c];
 }
+
+// Padded per-pair layout for the quadratic affinity GEMM: out[row[e]] = (x[src]-x[dst]) o c[pair[e]]
+// (Xe * coefficients, affinity_layer.py:15); rows not named by any edge are left untouched.
+__global__ void edge_diff_padded_kernel(const float* __restrict__ x, const int* __restrict__ src,
+                                        const int* __restrict__ dst, const int* __restrict__ pair,
+                                        const int* __restrict__ row, const float* __restrict__ cscale, long E, int D,
+                                        float* __restrict__ out) {
+    long e = blockIdx.x;
+    if (e >= E) return;
+    const float* a = x + (long)src[e] * D;
+    const float* b = x + (long)dst[e] * D;
+    const float* c = cscale ? cscale + (long)pair[e] * D : nullptr;
+    float* o = out + (long)row[e] * D;
+    for (int k = threadIdx.x; k < D; k += blockDim.x) {
+        float v = a[k] - b[k];
+        o[k] = c ? v * c[k] : v;
+    }
+}
 }  // namespace
+
+extern "C" int fpm_edge_diff_padded(const float* x, const int* src, const int* dst, const int* pair, const int* row,
+                                    const float* cscale, long E, int D, float* out, void* stream) {
+    if (E <= 0) return 0;
+    FPM_CHECK_ARG(pair && row && D > 0, "edge_diff_padded: pair/row maps required");
+    hipLaunchKernelGGL(edge_diff_padded_kernel, dim3((unsigned)E), dim3(256), 0, (hipStream_t)stream, x, src, dst,
+                       pair, row, cscale, E, D, out);
+    return fpm::check_launch("fpm_edge_diff_padded");
+}
 
 extern "C" int fpm_edge_diff(const float* x, const int* src, const int* dst, long E, int D, float* out, void* stream) {
     if (E <= 0) return 0;

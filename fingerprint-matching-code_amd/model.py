@@ -47,7 +47,7 @@ def _build_tree(root, sd):
 
 
 class Net(nn.Module):
-    def __init__(self, regression=False, dtype="f32", seed=0, lsa_threads=None, chunks=None):
+    def __init__(self, regression=False, dtype="f32", seed=0, lsa_threads=None, chunks=None, compute_ke=False):
         super().__init__()
         _build_tree(self, P.init_params(seed))
         self.regression = regression
@@ -60,6 +60,8 @@ class Net(nn.Module):
         self.dtype_mode = dtype
         self.lsa_threads = lsa_threads or max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16")), len(os.sched_getaffinity(0))))
         self.chunks = chunks
+        # quadratic (edge) affinity Ke (ngm.py:282-289): dead for every output, off by default
+        self.compute_ke = compute_ke
         self._pack = None
         self._pack_key = None
         self._pinned = None
@@ -97,6 +99,8 @@ class Net(nn.Module):
             d["bias%d" % l] = g(pre + ".bias")
         d["aff_w"] = g("vertex_affinity.A.weight")          # [768][1024] = N x K
         d["aff_b"] = g("vertex_affinity.A.bias")
+        d["eaff_w"] = g("edge_affinity.A.weight")
+        d["eaff_b"] = g("edge_affinity.A.bias")
         for l in range(C.GNN_LAYER):
             pre = "gnn_layer_%d" % l
             parts = [sd[pre + ".conv2.lin_l.weight"], sd[pre + ".conv2.lin_l.bias"], sd[pre + ".conv2.lin_r.weight"],
@@ -203,8 +207,35 @@ class Net(nn.Module):
             self.stage_times[name] = self.stage_times.get(name, 0.0) + (t - self._t_last)
             self._t_last = t
 
+    def _edge_affinity(self, wp, bt, gw, f1, f2):
+        """Ke[b] = 0.5 * (softplus((Xe1 o c') Xe2^T) - 0.5), Xe = x'[src] - x'[dst] from the
+        SplineConv output (ngm.py:250-289; affinity_layer.py:11-19) -> (B, E1max, E2max) fp32,
+        zero outside each pair's E1 x E2 block."""
+        dev = bt.device
+        B, D = bt.B, C.NODE_FEATURE_DIM
+        ce = torch.empty(B, D, device=dev, dtype=torch.float32)
+        ops.gemm(gw, wp["eaff_w"], B, D, C.GLOBAL_STATE_DIM, C.GLOBAL_STATE_DIM, C.GLOBAL_STATE_DIM,
+                 epi=ops.EPI_TANH, bias=wp["eaff_b"], out_f=ce)
+        xe, cnt = [], []
+        for side, f in ((0, f1), (1, f2)):
+            off = torch.as_tensor(bt.edge_off[side], dtype=torch.long)
+            c = off[1:] - off[:-1]
+            emax = max(int(c.max()), 1)
+            pair = torch.repeat_interleave(torch.arange(B), c)
+            row = pair * emax + (torch.arange(int(off[-1])) - off[pair])
+            x = ops.edge_diff_padded(f, bt.src[side], bt.dst[side], pair.to(dev, torch.int32),
+                                     row.to(dev, torch.int32), B * emax, cscale=ce if side == 0 else None)
+            xe.append((x, emax))
+            cnt.append(c.to(dev, torch.int32))
+        (x1, e1), (x2, e2) = xe
+        Ke = torch.empty(B, e1, e2, device=dev, dtype=torch.float32)
+        ops.gemm(x1, x2, e1, e2, D, D, D, batch=B, sA=e1 * D, sB=e2 * D, epi=ops.EPI_HALF_AFFINITY, out_f=Ke,
+                 ldc=e2, sC=e1 * e2, n1=cnt[1], n2=cnt[0])
+        return Ke
+
     def run_gpu_stage(self, bt, keep_feats=False, s_out=None, ss_out=None):
         """Everything up to ds_mat on the GPU.  Returns a dict of device tensors."""
+        keep_feats = keep_feats or self.compute_ke
         self._keep_feats = keep_feats
         if self._stage_timing:
             torch.cuda.synchronize()
@@ -229,6 +260,7 @@ class Net(nn.Module):
                  sA=n2max * C.NODE_FEATURE_DIM, sB=n1max * C.NODE_FEATURE_DIM, epi=ops.EPI_AFFINITY, out_f=X,
                  ldc=n1max, sC=N, n1=bt.n1, n2=bt.n2)
         Kp = X
+        Ke = self._edge_affinity(wp, bt, gw, f1, f2) if self.compute_ke else None
         self._mark("affinity")
         csr1 = ops.plan_csr(plan0, bt.E[0], B * n1max)
         csr2 = ops.plan_csr(plan1, bt.E[1], B * n2max)
@@ -249,6 +281,8 @@ class Net(nn.Module):
         out = dict(s=s, ss=ss, Kp=Kp[:, 0].transpose(1, 2), coef=coef)
         if keep_feats:
             out["feat0"], out["feat1"] = f1, f2
+        if Ke is not None:
+            out["Ke"] = Ke
         return out
 
     # ------------------------------------------------------------------------------------------
@@ -311,6 +345,8 @@ class Net(nn.Module):
         dev = bt.device
         B, n1max, n2max = bt.B, bt.n1max, bt.n2max
         K = chunks if chunks is not None else self.pipeline_chunks(B)
+        if self.compute_ke:
+            K = 1          # Ke blocks are padded to per-chunk edge maxima: keep one chunk
         parts = bt.split(K)
         t0 = time.perf_counter()
         min_pt = torch.minimum(bt.n1, bt.n2).to(torch.float32)

@@ -11,7 +11,7 @@ import torch
 from . import _lib
 
 F32, BF16 = 0, 1
-EPI_STORE, EPI_RELU, EPI_TANH, EPI_AFFINITY = 0, 1, 2, 3
+EPI_STORE, EPI_RELU, EPI_TANH, EPI_AFFINITY, EPI_HALF_AFFINITY = 0, 1, 2, 3, 4
 
 
 def _p(t):
@@ -133,6 +133,16 @@ def edge_diff(x, src, dst):
     E, D = src.numel(), x.shape[-1]
     out = torch.empty(E, D, device=x.device, dtype=torch.float32)
     _lib.call("fpm_edge_diff", _p(x), _p(src), _p(dst), E, D, _p(out), _stream(x))
+    return out
+
+
+def edge_diff_padded(x, src, dst, pair, row, nrows, cscale=None):
+    """(nrows, D) zero-padded: out[row[e]] = (x[src[e]] - x[dst[e]]) * cscale[pair[e]]."""
+    _dev(x, src, dst, pair, row)
+    E, D = src.numel(), x.shape[-1]
+    out = torch.zeros(nrows, D, device=x.device, dtype=torch.float32)
+    _lib.call("fpm_edge_diff_padded", _p(x), _p(src), _p(dst), _p(pair), _p(row), _p(cscale), E, D, _p(out),
+              _stream(x))
     return out
 
 

@@ -81,6 +81,11 @@ int fpm_spline_conv_fwd(int dtype, const void* x_op, const void* plan_ws, long E
                         const float* xres, const float* cscale, float* out_f, void* out_t, void* stream);
 /* vertex_attr_to_edge_attr (spline_conv.py:73-81): out[e] = x[src[e]] - x[dst[e]] */
 int fpm_edge_diff(const float* x, const int* src, const int* dst, long E, int D, float* out, void* stream);
+/* same, written into a padded per-pair layout and scaled: out[row[e]] = (x[src]-x[dst]) o c[pair[e]]
+ * (Xe * coefficients of the quadratic affinity, ngm.py:282-289 / affinity_layer.py:15); cscale may
+ * be NULL.  Feeds the optional Ke GEMM (fpm_gemm epilogue EPI_HALF_AFFINITY = 4). */
+int fpm_edge_diff_padded(const float* x, const int* src, const int* dst, const int* pair, const int* row,
+                         const float* cscale, long E, int D, float* out, void* stream);
 
 /* ---- association-graph GNN layer --------------------------------------------------------------
  * Replaces PYGNNLayer.forward's SAGEConv mean aggregation over the Kronecker pattern + MLPs +
@@ -113,6 +118,43 @@ int fpm_match_cls_fwd(const float* s, const float* perm, int B, int H, int W, co
                       const float* bn1_sc, const float* bn1_sh, const float* w2, const float* b2,
                       const float* bn2_sc, const float* bn2_sh, const float* fcw, const float* fcb, float* ws,
                       float* logits, float* prob, void* stream);
+
+/* ---- API parity: the reference's sparse extension ops (off the live forward path) ------------
+ * Replace src/extension/sparse_dot/sparse_dot.cpp:322-331 (csr_dot_csc_to_dense,
+ * dense_dot_csc_to_dense, csr_dot_diag_to_csr; csr_dot_csc_to_csr is CPU-only in the reference)
+ * and src/extension/bilinear_diag/bilinear_diag.cpp:324-326 (bilinear_diag).  Batched CSR/CSC in
+ * the csx_matrix.py:20-93 layout: int64 indices, int64 indptr of length B*len+1 with global
+ * offsets.  dtype: 0 f32, 2 f64, 3 f16 (device); 0 f32, 2 f64 (host).  Caller allocates outputs;
+ * the dense outputs are fully written (no pre-zeroing needed). */
+int fpm_csr_dot_csc_to_dense(int dtype, const long* t1_indices, const long* t1_indptr, const void* t1_data,
+                             const long* t2_indices, const long* t2_indptr, const void* t2_data, long batch_size,
+                             long out_h, long out_w, void* out, void* stream);
+int fpm_dense_dot_csc_to_dense(int dtype, const void* t1, const long* t2_indices, const long* t2_indptr,
+                               const void* t2_data, long batch_size, long out_h, long out_w, long t1_w, void* out,
+                               void* stream);
+int fpm_csr_dot_diag_to_csr(int dtype, const long* t1_indices, const long* t1_indptr, const void* t1_data,
+                            const void* t2, long batch_size, long out_h, long out_w, void* out_data, void* stream);
+int fpm_bilinear_diag(int dtype, const long* t1_indices, const long* t1_indptr, const void* t1_data, const void* t2,
+                      long feat_size, const long* t3_indices, const long* t3_indptr, const void* t3_data,
+                      long batch_size, long xlen, void* out, void* stream);
+/* host twins (CPU tensors, synchronous); csr_dot_csc_to_csr: call with out_indices == NULL for the
+ * nnz (out_indptr filled if given), then with buffers of capacity >= nnz.  Returns nnz or -1. */
+long fpm_csr_dot_csc_to_csr_host(int dtype, const long* t1_indices, const long* t1_indptr, const void* t1_data,
+                                 const long* t2_indices, const long* t2_indptr, const void* t2_data, long batch_size,
+                                 long out_h, long out_w, long* out_indptr, long capacity, long* out_indices,
+                                 void* out_data);
+int fpm_csr_dot_diag_to_csr_host(int dtype, const long* t1_indices, const long* t1_indptr, const void* t1_data,
+                                 const void* t2, long batch_size, long out_h, long out_w, void* out_data);
+int fpm_bilinear_diag_host(int dtype, const long* t1_indices, const long* t1_indptr, const void* t1_data,
+                           const void* t2, long feat_size, const long* t3_indices, const long* t3_indptr,
+                           const void* t3_data, long batch_size, long xlen, void* out);
+
+/* ---- Gconv (src/model/gcn.py:8-38; unused by Net) ----------------------------
+ * out = norm1(A) relu(x Wa^T + ba) + relu(x Wu^T + bu); W = [Wa; Wu] (2*dout, din), bias likewise;
+ * ws: fpm_gconv_ws_floats(B, n, dout) floats. */
+long fpm_gconv_ws_floats(int B, int n, int dout);
+int fpm_gconv_fwd(const float* A, const float* x, int B, int n, int din, int dout, const float* W, const float* bias,
+                  int norm, float* ws, float* out, void* stream);
 
 /* ---- profiling hooks: HIP-event timing of the dominant kernel (edge-message GEMM) ------------ */
 int fpm_profile_enable(int on);

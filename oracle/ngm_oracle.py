@@ -379,8 +379,14 @@ def gconv(A, x, a_w, a_b, u_w, u_b, norm=True):
 # ----------------------------------------------------------------------------------------------
 # Net.forward (ngm.py:205-491) from node features (synthetic bypass of backbone+feature_align)
 # ----------------------------------------------------------------------------------------------
+def edge_affinity(Xe1, Xe2, w, sd):
+    """Quadratic affinity (ngm.py:282-289): 0.5 * edge_affinity(Xe1, Xe2, w).  Dead for the
+    outputs (the dense K that would consume it is commented out at ngm.py:293-315)."""
+    return 0.5 * affinity(Xe1, Xe2, w, sd["edge_affinity.A.weight"], sd["edge_affinity.A.bias"])
+
+
 def forward(pairs, sd, regression=True, training=False, gt_perm=None, labels=None,
-            dtype=torch.float32, explicit_pattern=False, stages=None):
+            dtype=torch.float32, explicit_pattern=False, stages=None, compute_ke=False):
     """pairs: list of (g0, g1) dicts as produced by ``fpm.synth.make_graph`` (keys x, w,
     edge_index, pseudo, n).  Returns the data_dict keys written at ngm.py:479-487 plus the
     intermediates ``s``, ``ss``, ``Kp`` used by the parity tests."""
@@ -404,6 +410,10 @@ def forward(pairs, sd, regression=True, training=False, gt_perm=None, labels=Non
         kp = affinity(feats[0][b], feats[1][b], gw[b], sd["vertex_affinity.A.weight"],
                       sd["vertex_affinity.A.bias"])
         Kp[b, :kp.shape[0], :kp.shape[1]] = kp
+    Ke = None
+    if compute_ke:
+        Ke = [edge_affinity(edge_diff(feats[0][b], T(pairs[b][0]["edge_index"])),
+                            edge_diff(feats[1][b], T(pairs[b][1]["edge_index"])), gw[b], sd) for b in range(B)]
     emb = Kp.transpose(1, 2).contiguous().view(B, -1, 1)
     qap = []
     for b in range(B):
@@ -443,6 +453,8 @@ def forward(pairs, sd, regression=True, training=False, gt_perm=None, labels=Non
     cls_prob = torch.sigmoid(logits)
     out = dict(ds_mat=ds, perm_mat=perm, k_prob=ks, cls_prob=cls_prob, cls_logits=logits,
                s=s, ss=ss, Kp=Kp, lsa=x)
+    if Ke is not None:
+        out["Ke"] = Ke
     if labels is not None:
         out["cls_loss"] = F.binary_cross_entropy_with_logits(logits, T(labels).to(dtype).view(-1))
     else:

@@ -226,3 +226,37 @@ def test_chunked_pipeline_bitwise(sd):
     c = net.run(sub, chunks=1)
     for k in ("ds_mat", "perm_mat", "k_prob"):
         assert torch.equal(c[k], a[k][2:5]), k
+
+
+# ---------------------------------------------------------------------------------------- Ke, Gconv
+def test_edge_affinity_ke(sd):
+    """Optional quadratic affinity (ngm.py:282-289) vs the oracle, ragged edge counts."""
+    pairs = synth.make_batch(12, 3, [20, 31, 26], n2=[24, 18, 30])
+    net = fpm.Net(regression=True, compute_ke=True)
+    net.load_state_dict(sd)
+    res = net.run(DeviceBatch.from_pairs(pairs, DEV))
+    ref = O.forward(pairs, sd, regression=True, compute_ke=True)
+    Ke = res["Ke"].cpu()
+    for b in range(3):
+        e1, e2 = ref["Ke"][b].shape
+        assert (Ke[b, :e1, :e2] - ref["Ke"][b]).abs().max() < 1e-5
+        assert Ke[b, e1:].abs().max() == 0 if e1 < Ke.shape[1] else True
+        assert Ke[b, :, e2:].abs().max() == 0 if e2 < Ke.shape[2] else True
+    assert (res["ds_mat"].cpu() - ref["ds_mat"]).abs().max() < 1e-4
+
+
+def test_gconv_golden():
+    from fpm.gconv import Gconv
+    z = np.load(os.path.join(GOLDEN, "gconv.npz"))
+    gc = Gconv(6, 5)
+    with torch.no_grad():
+        gc.a_fc.weight.copy_(torch.from_numpy(z["a_w"]))
+        gc.a_fc.bias.copy_(torch.from_numpy(z["a_b"]))
+        gc.u_fc.weight.copy_(torch.from_numpy(z["u_w"]))
+        gc.u_fc.bias.copy_(torch.from_numpy(z["u_b"]))
+    A, x = torch.from_numpy(z["A"]), torch.from_numpy(z["x"])
+    y = gc(A.to(DEV), x.to(DEV)).cpu()
+    np.testing.assert_allclose(y.numpy(), z["y"], atol=1e-5, rtol=0)
+    y2 = gc(A.to(DEV), x.to(DEV), norm=False).cpu()
+    ref = O.gconv(A, x, *(torch.from_numpy(z[k]) for k in ("a_w", "a_b", "u_w", "u_b")), norm=False)
+    assert (y2 - ref).abs().max() < 1e-5
