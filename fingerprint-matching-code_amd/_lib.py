@@ -35,7 +35,7 @@ SIGNATURES = {
     "fpm_gnn_param_count": (I, [I]),
     "fpm_node_classifier": (I, [P, I, I, I, P, P, P, P]),
     "fpm_crossset_attn_fwd": (I, [I, P, L, L, I, I, I, P, P, I, P, P, P, P, P, P]),
-    "fpm_instnorm": (I, [I, P, P, I, I, I, P, P, P, P, F, P, P, P, P]),
+    "fpm_instnorm": (I, [I, P, P, I, I, I, P, P, P, P, F, P, P, I, P, P]),
     "fpm_afau_head": (I, [P, P, I, I, P, P, P, P, P, P, P, P, P, P]),
     "fpm_match_cls_ws_floats": (L, [I, I, I]),
     "fpm_match_cls_fwd": (I, [P, P, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),

@@ -26,6 +26,7 @@ SPLINE_CELLS = SPLINE_KERNEL * SPLINE_KERNEL
 PSEUDO_RESCALE = 320.0              # gmdataset.py:36,171 (max(RESCALE))
 
 AFAU_EMB = 600                      # afau.py:27
+AFAU_EMB_PAD = 640                  # bf16 operand copies of 600-wide rows, K padded to a multiple of 64
 AFAU_HEADS = 16                     # afau.py:28
 AFAU_QKV = 16                       # afau.py:29
 AFAU_FF = 256                       # afau.py:30

@@ -86,7 +86,7 @@ __global__ __launch_bounds__(256) void instnorm_kernel(const float* __restrict__
                                                        int P, int Cn, const int* __restrict__ nvalid,
                                                        const float* __restrict__ onehot_bias, const float* __restrict__ w,
                                                        const float* __restrict__ bb, float eps, float* __restrict__ out_f,
-                                                       T* __restrict__ out_t, float* __restrict__ gmax) {
+                                                       T* __restrict__ out_t, int ldt, float* __restrict__ gmax) {
     __shared__ float ps[4][64], pq[4][64];
     const int b = blockIdx.x, c = blockIdx.y * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
     const bool cv = c < Cn;
@@ -122,9 +122,12 @@ __global__ __launch_bounds__(256) void instnorm_kernel(const float* __restrict__
         else {
             long o = ((long)b * P + p) * Cn + c;
             if (out_f) out_f[o] = y;
-            if (out_t) out_t[o] = fpm::from_f<T>(y);
+            if (out_t) out_t[((long)b * P + p) * ldt + c] = fpm::from_f<T>(y);
         }
     }
+    // zero K-padding columns [Cn, ldt) of the operand copy (the next GEMM runs K = ldt)
+    if (!cv && out_t && !gmax && c < ldt)
+        for (int p = g; p < P; p += 4) out_t[((long)b * P + p) * ldt + c] = fpm::from_f<T>(0.f);
     if (gmax) {
         __syncthreads();
         ps[g][threadIdx.x & 63] = mx;
@@ -181,16 +184,19 @@ extern "C" int fpm_crossset_attn_fwd(int dtype, const float* cost, long c_sb, lo
 
 extern "C" int fpm_instnorm(int dtype, const float* in1, const float* in2, int B, int P, int Cn, const int* nvalid,
                             const float* onehot_bias, const float* w, const float* bias, float eps, float* out_f,
-                            void* out_t, float* gmax, void* stream) {
+                            void* out_t, int ldt, float* gmax, void* stream) {
     if (B == 0) return 0;
-    dim3 grid(B, (Cn + 63) / 64);
+    if (ldt <= 0) ldt = Cn;
+    FPM_CHECK_ARG(ldt >= Cn, "instnorm: ldt %d < Cn %d", ldt, Cn);
+    const int cols = ldt > Cn ? ldt : Cn;
+    dim3 grid(B, (cols + 63) / 64);
     hipStream_t st = (hipStream_t)stream;
     if (dtype == 0)
         hipLaunchKernelGGL((instnorm_kernel<float>), grid, dim3(256), 0, st, in1, in2, P, Cn, nvalid, onehot_bias, w,
-                           bias, eps, out_f, (float*)out_t, gmax);
+                           bias, eps, out_f, (float*)out_t, ldt, gmax);
     else
         hipLaunchKernelGGL((instnorm_kernel<bf16_t>), grid, dim3(256), 0, st, in1, in2, P, Cn, nvalid, onehot_bias, w,
-                           bias, eps, out_f, (bf16_t*)out_t, gmax);
+                           bias, eps, out_f, (bf16_t*)out_t, ldt, gmax);
     return fpm::check_launch("fpm_instnorm");
 }
 

@@ -1,7 +1,7 @@
 // C-ABI entry for the generic (batched, optionally row-gathered) MFMA GEMM with fused epilogues.
 // Used by: SplineConv root term, global-weight coefficient (affinity_layer.py:13), vertex
 // affinity Kp (affinity_layer.py:15-18), AFA-U projections/FFN (afau.py:99-103,188-199).
-#include "gemm_core.h"
+#include "gemm_big.h"
 
 extern "C" int fpm_gemm(int dtype, const void* A, long lda, long sA, const int* a_rows, const void* B, long ldb,
                         long sB, int M, int N, int K, int batch, int epi, const float* bias, float* Cf, void* Ct,
@@ -22,9 +22,29 @@ extern "C" int fpm_gemm(int dtype, const void* A, long lda, long sA, const int* 
     p.M = M; p.N = N; p.K = K; p.nseg = 1;
     p.tile_info = nullptr; p.group_off = nullptr;
     p.epi = epi; p.bias = bias; p.Cf = Cf; p.Ct = Ct; p.ldc = ldc; p.sC = sC; p.n1 = n1; p.n2 = n2;
+    hipStream_t st = (hipStream_t)stream;
+    // bf16 with a large M: the 256-row LDS-DMA tiles (gemm_big.h)
+    const bool big = dtype == 1 && M >= 2 * G2_BM && K % G2_BK == 0 && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
+                     !(Cf && Ct) && (Cf ? ldc % 4 == 0 : ldc % 8 == 0) && (epi == EPI_STORE || epi == EPI_RELU);
+    if (big) {
+        const int mt = (M + G2_BM - 1) / G2_BM;
+        const int BN = (N % 256 == 0 && (long)mt * (N / 256) * batch >= 512) ? 256 : 128;
+        p.remap_mtiles = mt;
+        dim3 grid(remap_grid_big(N, BN, mt), 1, batch);
+        const bool relu = epi == EPI_RELU, f32 = Cf != nullptr;
+#define FPM_BIG(BN_, R_, F_) hipLaunchKernelGGL((gemm_big_kernel<BN_, R_, F_>), grid, dim3(G2_THREADS), 0, st, p)
+        if (BN == 256) {
+            if (relu) { if (f32) FPM_BIG(256, true, true); else FPM_BIG(256, true, false); }
+            else { if (f32) FPM_BIG(256, false, true); else FPM_BIG(256, false, false); }
+        } else {
+            if (relu) { if (f32) FPM_BIG(128, true, true); else FPM_BIG(128, true, false); }
+            else { if (f32) FPM_BIG(128, false, true); else FPM_BIG(128, false, false); }
+        }
+#undef FPM_BIG
+        return check_launch("fpm_gemm");
+    }
     p.remap_mtiles = (M + GBM - 1) / GBM;
     dim3 grid(remap_grid(N, p.remap_mtiles), 1, batch);
-    hipStream_t st = (hipStream_t)stream;
     if (dtype == 0) hipLaunchKernelGGL((gemm_kernel<float, false>), grid, dim3(GTHREADS), 0, st, p);
     else hipLaunchKernelGGL((gemm_kernel<bf16_t, false>), grid, dim3(GTHREADS), 0, st, p);
     return check_launch("fpm_gemm");

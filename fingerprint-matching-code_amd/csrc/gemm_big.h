@@ -1,9 +1,10 @@
-// 256 x 256 bf16 MFMA GEMM tile for the large product GEMM of SplineConv (and any bf16 GEMM with
-// N % 256 == 0, K % 64 == 0):
+// 256-row bf16 MFMA GEMM tiles (256 x 256 and 256 x 128) for the large bf16 GEMMs: the SplineConv
+// (node, cell) product GEMM and the AFA-U projections / FFN.
 //
-//   C[r, n] = sum_k A[row(r), k] * B_g[n, k]        (bf16 operands, fp32 accumulate, bf16 out)
+//   C[r, n] = epi( sum_k A[row(r), k] * B_g[n, k] (+ bias[n]) )   bf16 operands, fp32 accumulate
 //
-// * 512 threads = 8 waves as 2 (M) x 4 (N); each wave owns 128 x 64 = 8 x 4 MFMA 16x16x32 tiles.
+// * 512 threads = 8 waves; BN = 256: 2 (M) x 4 (N) waves of 128 x 64, BN = 128: 4 x 2 waves of
+//   64 x 64, as 16x16x32 MFMA fragments.
 // * A and B K-tiles (BK = 64, 128 B per row) are staged global -> LDS with global_load_lds
 //   (16 B per lane, no VGPR round trip); the per-lane SOURCE address carries the row gather and an
 //   XOR swizzle, the LDS image stays lane-linear: LDS row r, 16-B slot s holds K-chunk
@@ -11,7 +12,11 @@
 //   touches 16 distinct 16-B slots of the 256-B bank row: conflict-free ds_read_b128.
 // * Two LDS stages: the loads of K-tile t+1 are issued before the MFMAs of tile t and retired by
 //   the barrier that ends step t.
-// * Epilogue: accumulators -> bf16 -> LDS (rows padded to 528 B) -> 16-B coalesced global stores.
+// * Epilogue through LDS (rows padded by 16 B): bf16 output in one pass, fp32 output in two
+//   128-row halves; 16-B coalesced global stores; optional bias and ReLU on the fp32 accumulator.
+// * Requirements (checked by the launchers): K % 64 == 0 (callers pad K with zeros), N % 8 == 0,
+//   lda/ldb % 8 == 0, ldc 16-B aligned rows.  Rows past M and columns past N are clamped on load
+//   and never stored.
 // * Tile order: the XCD-chunked remap of gemm_core.h; grouped mode reads a (group, row0) table
 //   built for 256-row tiles, group g selecting B + g * sB_seg.
 #pragma once
@@ -19,30 +24,53 @@
 
 namespace fpm {
 
-constexpr int G2_BM = 256, G2_BN = 256, G2_BK = 64, G2_THREADS = 512;
-constexpr int G2_TILE_BYTES = G2_BM * G2_BK * 2;          // 32 KiB per operand per stage
-constexpr int G2_EPI_ROW = G2_BN * 2 + 16;                // padded epilogue row (bytes)
-constexpr int G2_SMEM = G2_BM * G2_EPI_ROW;               // 135168 B >= 4 staging tiles (131072 B)
+constexpr int G2_BM = 256, G2_BK = 64, G2_THREADS = 512;
+constexpr int G2_A_BYTES = G2_BM * G2_BK * 2;             // 32 KiB A tile per stage
+constexpr int g2_max(int a, int b) { return a > b ? a : b; }
 
-inline unsigned remap_grid256(int N, int mtiles) {
-    long nt = N / G2_BN, chunk = 4 * nt;
+template <int BN> struct G2Cfg {
+    static constexpr int WM = BN == 256 ? 2 : 4;          // waves along M
+    static constexpr int WN = 8 / WM;                     // waves along N
+    static constexpr int FM = G2_BM / WM / 16;            // 16-row fragments per wave
+    static constexpr int FN = BN / WN / 16;               // 16-col fragments per wave (4)
+    static constexpr int B_BYTES = BN * G2_BK * 2;
+    static constexpr int STAGE = G2_A_BYTES + B_BYTES;
+    static constexpr int BPIECES = BN / 8 / 8;            // 8-row pieces of B per wave
+    // 2 stages; bf16 epilogue [256][2BN+16 B]; fp32 epilogue half [128][4BN+16 B]
+    static constexpr int SMEM = g2_max(2 * STAGE, g2_max(G2_BM * (2 * BN + 16), 128 * (4 * BN + 16)));
+};
+
+inline unsigned remap_grid_big(int N, int BN, int mtiles) {
+    long nt = (N + BN - 1) / BN, chunk = 4 * nt;
     long t = nt * mtiles;
+    if (mtiles < REMAP_MIN) return (unsigned)t;
     return (unsigned)((t + 8 * chunk - 1) / (8 * chunk) * (8 * chunk));
 }
+inline unsigned remap_grid256(int N, int mtiles) { return remap_grid_big(N, 256, mtiles); }
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
 
-__global__ __launch_bounds__(G2_THREADS, 1) void gemm256_bf16_kernel(GemmParams p) {
-    __shared__ __attribute__((aligned(16))) unsigned char smem[G2_SMEM];
+// epilogue: optional bias, optional ReLU (the only epilogues these GEMMs need; compiled per variant
+// so the unrolled 128-element epilogue stays small)
+template <bool RELU>
+__device__ __forceinline__ float g2_epi(const float* __restrict__ bias, float v, int n) {
+    if (bias) v += bias[n];
+    return RELU ? fmaxf(v, 0.f) : v;
+}
+
+template <int BN, bool RELU, bool F32OUT>
+__global__ __launch_bounds__(G2_THREADS, 1) void gemm_big_kernel(GemmParams p) {
+    using Cfg = G2Cfg<BN>;
+    constexpr int FM = Cfg::FM, FN = Cfg::FN;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[Cfg::SMEM];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave >> 2, wn = wave & 3;
+    const int wm = wave / Cfg::WN, wn = wave % Cfg::WN;
+    const int batch = blockIdx.z;
 
     // XCD-chunked tile order (see gemm_core.h)
-    const int nt = p.N / G2_BN;
-    const int chunk = 4 * nt;
-    const int bi = blockIdx.x >> 3;
-    const int q = ((bi / chunk) * 8 + (blockIdx.x & 7)) * chunk + (bi % chunk);
+    const int nt = (p.N + BN - 1) / BN;
+    const int q = remap_tile(nt, p.remap_mtiles);
     const int mtile = q / nt, ntile = q - mtile * nt;
     if (mtile >= p.remap_mtiles) return;
     int group = 0, row0, row_end;
@@ -55,50 +83,57 @@ __global__ __launch_bounds__(G2_THREADS, 1) void gemm256_bf16_kernel(GemmParams 
         row0 = mtile * G2_BM;
         row_end = p.M;
     }
-    const int n0 = ntile * G2_BN;
-    const bf16_t* A = (const bf16_t*)p.A;
-    const bf16_t* Bg = (const bf16_t*)p.B + (long)group * p.sB_seg;
+    const int n0 = ntile * BN;
+    const bf16_t* A = (const bf16_t*)p.A + (long)batch * p.sA;
+    const bf16_t* Bg = (const bf16_t*)p.B + (long)batch * p.sB + (long)group * p.sB_seg;
 
-    // staging: wave w issues pieces ci = 4w + i (i < 4) of each operand; a piece is 8 rows x 128 B.
-    // lane: row 8 ci + (lane >> 3), slot lane & 7, K-chunk slot ^ ((row >> 1) & 7)
+    // staging: a piece is 8 rows x 128 B; wave w issues A pieces 4w..4w+3 and its share of B.
+    // lane: row 8*piece + (lane >> 3), slot lane & 7, K-chunk slot ^ ((row >> 1) & 7)
     const bf16_t* asrc[4];
-    const bf16_t* bsrc[4];
+    const bf16_t* bsrc[Cfg::BPIECES];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int ci = wave * 4 + i;
-        const int r = ci * 8 + (lane >> 3);
+        const int r = (wave * 4 + i) * 8 + (lane >> 3);
         const int kc = (lane & 7) ^ ((r >> 1) & 7);
         int gr = row0 + r;
         gr = gr < row_end ? gr : row0;                    // clamp: rows past the end are never stored
         const long arow = p.a_rows ? (long)p.a_rows[gr] : (long)gr;
         asrc[i] = A + arow * p.lda + kc * 8;
-        bsrc[i] = Bg + (long)(n0 + r) * p.ldb + kc * 8;
+    }
+#pragma unroll
+    for (int i = 0; i < Cfg::BPIECES; ++i) {
+        const int r = (wave * Cfg::BPIECES + i) * 8 + (lane >> 3);
+        const int kc = (lane & 7) ^ ((r >> 1) & 7);
+        const int n = n0 + r < p.N ? n0 + r : p.N - 1;    // clamp: columns past N are never stored
+        bsrc[i] = Bg + (long)n * p.ldb + kc * 8;
     }
     auto issue = [&](int stage, int kt) {
-        unsigned char* As = smem + stage * 2 * G2_TILE_BYTES;
-        unsigned char* Bs = As + G2_TILE_BYTES;
+        unsigned char* As = smem + stage * Cfg::STAGE;
+        unsigned char* Bs = As + G2_A_BYTES;
         const int k0 = kt * G2_BK;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int ci = wave * 4 + i;
-            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(asrc[i] + k0), (lds_ptr_t)(As + ci * 1024), 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bsrc[i] + k0), (lds_ptr_t)(Bs + ci * 1024), 16, 0, 0);
-        }
+        for (int i = 0; i < 4; ++i)
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(asrc[i] + k0), (lds_ptr_t)(As + (wave * 4 + i) * 1024), 16,
+                                             0, 0);
+#pragma unroll
+        for (int i = 0; i < Cfg::BPIECES; ++i)
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bsrc[i] + k0),
+                                             (lds_ptr_t)(Bs + (wave * Cfg::BPIECES + i) * 1024), 16, 0, 0);
     };
 
     // fragment read offsets: row R = base + f*16 + (lane&15), K-chunk c = kk*4 + (lane>>4),
     // slot c ^ ((R>>1)&7) = c ^ ((lane>>1)&7)  (f*16 does not change (R>>1)&7)
     const int xr = (lane >> 1) & 7;
-    const int a_base = (wm * 128 + (lane & 15)) * 128;
-    const int b_base = (wn * 64 + (lane & 15)) * 128;
-    const int s0 = (((lane >> 4)) ^ xr) * 16;            // kk = 0
+    const int a_base = (wm * FM * 16 + (lane & 15)) * 128;
+    const int b_base = (wn * FN * 16 + (lane & 15)) * 128;
+    const int s0 = ((lane >> 4) ^ xr) * 16;              // kk = 0
     const int s1 = ((4 + (lane >> 4)) ^ xr) * 16;        // kk = 1
 
-    f32x4_t acc[8][4];
+    f32x4_t acc[FM][FN];
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
     const int ktiles = p.K / G2_BK;
     issue(0, 0);
@@ -107,47 +142,87 @@ __global__ __launch_bounds__(G2_THREADS, 1) void gemm256_bf16_kernel(GemmParams 
     for (int kt = 0; kt < ktiles; ++kt) {
         const int cur = kt & 1;
         if (kt + 1 < ktiles) issue(cur ^ 1, kt + 1);
-        const unsigned char* As = smem + cur * 2 * G2_TILE_BYTES;
-        const unsigned char* Bs = As + G2_TILE_BYTES;
+        const unsigned char* As = smem + cur * Cfg::STAGE;
+        const unsigned char* Bs = As + G2_A_BYTES;
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
             const int so = kk ? s1 : s0;
-            bf16x8_t a[8], b[4];
+            bf16x8_t a[FM], b[FN];
 #pragma unroll
-            for (int f = 0; f < 4; ++f) b[f] = *(const bf16x8_t*)(Bs + b_base + f * 2048 + so);
+            for (int f = 0; f < FN; ++f) b[f] = *(const bf16x8_t*)(Bs + b_base + f * 2048 + so);
 #pragma unroll
-            for (int f = 0; f < 8; ++f) a[f] = *(const bf16x8_t*)(As + a_base + f * 2048 + so);
+            for (int f = 0; f < FM; ++f) a[f] = *(const bf16x8_t*)(As + a_base + f * 2048 + so);
 #pragma unroll
-            for (int fm = 0; fm < 8; ++fm)
+            for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
-                for (int fn = 0; fn < 4; ++fn)
+                for (int fn = 0; fn < FN; ++fn)
                     acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[fm], b[fn], acc[fm][fn], 0, 0, 0);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
 
-    // epilogue through LDS: bf16 tile [256][256] with 528-B rows
+    // epilogue through LDS
+    if (!F32OUT) {
+        // bf16 tile [256][BN] with (2*BN + 16)-B rows
+        constexpr int ROW = BN * 2 + 16;
 #pragma unroll
-    for (int fm = 0; fm < 8; ++fm)
+        for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int r = wm * 128 + fm * 16 + (lane >> 4) * 4 + j;
+            for (int j = 0; j < 4; ++j) {
+                const int r = wm * FM * 16 + fm * 16 + (lane >> 4) * 4 + j;
 #pragma unroll
-            for (int fn = 0; fn < 4; ++fn) {
-                const int c = wn * 64 + fn * 16 + (lane & 15);
-                *(bf16_t*)(smem + r * G2_EPI_ROW + c * 2) = f2bf(acc[fm][fn][j]);
+                for (int fn = 0; fn < FN; ++fn) {
+                    const int c = wn * FN * 16 + fn * 16 + (lane & 15);
+                    const int n = n0 + c < p.N ? n0 + c : p.N - 1;
+                    *(bf16_t*)(smem + r * ROW + c * 2) = f2bf(g2_epi<RELU>(p.bias, acc[fm][fn][j], n));
+                }
+            }
+        __syncthreads();
+        bf16_t* Ct = (bf16_t*)p.Ct + (long)batch * p.sC;
+        constexpr int CH = BN / 8;                        // 16-B chunks per row
+#pragma unroll 4
+        for (int it = 0; it < G2_BM * CH / G2_THREADS; ++it) {
+            const int idx = it * G2_THREADS + tid;
+            const int r = idx / CH, ch = idx % CH;
+            if (row0 + r < row_end && n0 + ch * 8 < p.N) {
+                uint4 v = *(const uint4*)(smem + r * ROW + ch * 16);
+                *(uint4*)(Ct + (long)(row0 + r) * p.ldc + n0 + ch * 8) = v;
             }
         }
-    __syncthreads();
-    bf16_t* Ct = (bf16_t*)p.Ct;
+    } else {
+        // fp32 tile in two 128-row halves, [128][BN] with (4*BN + 16)-B rows
+        constexpr int ROW = BN * 4 + 16;
+        constexpr int WAVES_PER_HALF_M = Cfg::WM / 2;     // waves along M in each half
+        float* Cf = p.Cf + (long)batch * p.sC;
+        constexpr int CH = BN / 4;
+        for (int h = 0; h < 2; ++h) {
+            if (wm / WAVES_PER_HALF_M == h) {
+#pragma unroll
+                for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int r = wm * FM * 16 + fm * 16 + (lane >> 4) * 4 + j;   // tile row
+#pragma unroll
+                        for (int fn = 0; fn < FN; ++fn) {
+                            const int c = wn * FN * 16 + fn * 16 + (lane & 15);
+                            const int n = n0 + c < p.N ? n0 + c : p.N - 1;
+                            *(float*)(smem + (r - h * 128) * ROW + c * 4) = g2_epi<RELU>(p.bias, acc[fm][fn][j], n);
+                        }
+                    }
+            }
+            __syncthreads();
 #pragma unroll 4
-    for (int it = 0; it < (G2_BM * G2_BN / 8) / G2_THREADS; ++it) {
-        const int idx = it * G2_THREADS + tid;
-        const int r = idx >> 5, ch = idx & 31;
-        if (row0 + r < row_end) {
-            uint4 v = *(const uint4*)(smem + r * G2_EPI_ROW + ch * 16);
-            *(uint4*)(Ct + (long)(row0 + r) * p.ldc + n0 + ch * 8) = v;
+            for (int it = 0; it < 128 * CH / G2_THREADS; ++it) {
+                const int idx = it * G2_THREADS + tid;
+                const int r = idx / CH, ch = idx % CH;
+                const int gr = row0 + h * 128 + r;
+                if (gr < row_end && n0 + ch * 4 < p.N) {
+                    uint4 v = *(const uint4*)(smem + r * ROW + ch * 16);
+                    *(uint4*)(Cf + (long)gr * p.ldc + n0 + ch * 4) = v;
+                }
+            }
+            __syncthreads();
         }
     }
 }

@@ -49,10 +49,20 @@ struct GemmParams {
 
 // 1-D grid for the XCD-aware tile order: padded to whole rounds of 8 chunks so the remap is a
 // bijection (extra blocks exit).
+// Small launches (fewer than REMAP_MIN row tiles per batch) keep the plain order: dealing a
+// handful of tiles in XCD chunks would put them all on one XCD.
+constexpr int REMAP_MIN = 32;
 inline unsigned remap_grid(int N, int mtiles) {
     long nt = (N + 127) / 128, chunk = 4 * nt;
     long t = nt * mtiles;
+    if (mtiles < REMAP_MIN) return (unsigned)t;
     return (unsigned)((t + 8 * chunk - 1) / (8 * chunk) * (8 * chunk));
+}
+__device__ __forceinline__ int remap_tile(int nt, int mtiles) {
+    if (mtiles < REMAP_MIN) return blockIdx.x;
+    const int chunk = 4 * nt;
+    const int i = blockIdx.x >> 3;
+    return ((i / chunk) * 8 + (blockIdx.x & 7)) * chunk + (i % chunk);
 }
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -143,9 +153,7 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_kernel(GemmParams p) {
         // Runs are chunks of 4 row tiles x nt column tiles, dealt to the XCDs in turn, so a tail of
         // empty tiles (grouped mode over-provisions the table) stays spread over all 8 XCDs.
         const int nt = (p.N + GBN - 1) / GBN;
-        const int chunk = 4 * nt;
-        const int i = blockIdx.x >> 3;
-        const int q = ((i / chunk) * 8 + (blockIdx.x & 7)) * chunk + (i % chunk);
+        const int q = remap_tile(nt, p.remap_mtiles);
         mtile = q / nt;
         ntile = q - mtile * nt;
         if (mtile >= p.remap_mtiles) return;

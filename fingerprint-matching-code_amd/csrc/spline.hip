@@ -479,7 +479,7 @@ extern "C" int fpm_spline_conv_fwd(int dtype, const void* x_op, const void* plan
             (void)hipEventRecord(rec.a, st);
         }
         if (dtype == 0) hipLaunchKernelGGL((gemm_kernel<float, false>), grid, dim3(GTHREADS), 0, st, p);
-        else hipLaunchKernelGGL(gemm256_bf16_kernel, grid, dim3(G2_THREADS), 0, st, p);
+        else hipLaunchKernelGGL((gemm_big_kernel<256, false, false>), grid, dim3(G2_THREADS), 0, st, p);
         if (g_prof_on && g_prof_rows && rec.slot < PROF_MAX) {
             (void)hipEventRecord(rec.b, st);
             g_prof.push_back(rec);

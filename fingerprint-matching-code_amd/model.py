@@ -66,7 +66,7 @@ class Net(nn.Module):
         self._pack_key = None
         self._pinned = None
         self._stream_cache = {}
-        self.two_streams = os.environ.get("FPM_STREAMS", "2") != "1"
+        self.n_streams = max(1, int(os.environ.get("FPM_STREAMS", "2")))
         self._keep_feats = False
         self._stage_timing = os.environ.get("FPM_STAGE_TIMING", "0") == "1"
         self.stage_times = {}
@@ -119,7 +119,10 @@ class Net(nn.Module):
             d[blk + "_mix2b"] = g(pre + ".mixed_score_MHA.mix2_bias")
             d[blk + "_Wc"] = sd[pre + ".multi_head_combine.weight"].to(device).contiguous().to(op)   # (600, 256)
             d[blk + "_bc"] = g(pre + ".multi_head_combine.bias")
-            d[blk + "_W1"] = sd[pre + ".feed_forward.W1.weight"].to(device).contiguous().to(op)      # (256, 600)
+            W1 = sd[pre + ".feed_forward.W1.weight"].to(device)                                      # (256, 600)
+            if op == torch.bfloat16:      # K padded with zeros to the 256-row kernel's BK multiple
+                W1 = F.pad(W1, (0, C.AFAU_EMB_PAD - C.AFAU_EMB))
+            d[blk + "_W1"] = W1.contiguous().to(op)
             d[blk + "_b1"] = g(pre + ".feed_forward.W1.bias")
             d[blk + "_W2"] = sd[pre + ".feed_forward.W2.weight"].to(device).contiguous().to(op)      # (600, 256)
             d[blk + "_b2"] = g(pre + ".feed_forward.W2.bias")
@@ -178,15 +181,16 @@ class Net(nn.Module):
         gmax = {}
         for blk, rows, P_ in (("row", B * n1max, n1max), ("col", B * n2max, n2max)):
             o1f = torch.empty(rows, E, device=dev, dtype=torch.float32)
-            o1t = o1f if op == torch.float32 else torch.empty(rows, E, device=dev, dtype=op)
+            KE = E if op == torch.float32 else C.AFAU_EMB_PAD      # bf16 operand copy: zero-padded K
+            o1t = o1f if op == torch.float32 else torch.empty(rows, KE, device=dev, dtype=op)
             if blk == "row":
                 ops.instnorm(mh, B, P_, E, wp["row_n1w"], wp["row_n1b"], out_f=o1f,
-                             out_t=None if op == torch.float32 else o1t)
+                             out_t=None if op == torch.float32 else o1t, ldt=KE)
             else:
                 ops.instnorm(None, B, P_, E, wp["col_n1w"], wp["col_n1b"], nvalid=bt.n2, onehot_bias=wp["col_bc"],
-                             out_f=o1f, out_t=None if op == torch.float32 else o1t)
+                             out_f=o1f, out_t=None if op == torch.float32 else o1t, ldt=KE)
             hbuf = torch.empty(rows, FF, device=dev, dtype=op)
-            ops.gemm(o1t, wp[blk + "_W1"], rows, FF, E, E, E, epi=ops.EPI_RELU, bias=wp[blk + "_b1"],
+            ops.gemm(o1t, wp[blk + "_W1"], rows, FF, KE, KE, KE, epi=ops.EPI_RELU, bias=wp[blk + "_b1"],
                      out_t=hbuf if op != torch.float32 else None, out_f=hbuf if op == torch.float32 else None,
                      ldc=FF)
             ff = torch.empty(rows, E, device=dev, dtype=torch.float32)
@@ -289,13 +293,15 @@ class Net(nn.Module):
     def _streams(self, dev):
         key = str(dev)
         if key not in self._stream_cache:
-            self._stream_cache[key] = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+            self._stream_cache[key] = [torch.cuda.Stream(dev) for _ in range(self.n_streams)]
         return self._stream_cache[key]
 
     def pipeline_chunks(self, B):
         """Sub-batches per forward so the host Hungarian of chunk c overlaps the GPU work of c+1."""
         if self.chunks is not None:
             return max(1, min(self.chunks, B))
+        if os.environ.get("FPM_CHUNKS"):
+            return max(1, min(int(os.environ["FPM_CHUNKS"]), B))
         return max(1, min(8, B // 128))
 
     def _stage_a(self, part, b0, b1, o, keep_feats, gt_ks, min_pt, st):
@@ -363,7 +369,7 @@ class Net(nn.Module):
         main = torch.cuda.current_stream(dev)
         ev_start = torch.cuda.Event(enable_timing=True)
         ev_start.record(main)
-        streams = self._streams(dev) if (len(parts) > 1 and self.two_streams) else [main]
+        streams = self._streams(dev) if (len(parts) > 1 and self.n_streams > 1) else [main]
         for st in streams:
             if st is not main:
                 st.wait_event(ev_start)

@@ -166,11 +166,12 @@ def crossset_attn(cost, n2, Wv, mix1w, mix1b, mix2w, mix2b, out):
 
 
 def instnorm(in1, B, P, Cn, w, b, in2=None, nvalid=None, onehot_bias=None, out_f=None, out_t=None, gmax=None,
-             eps=1e-5):
+             eps=1e-5, ldt=0):
+    """``ldt`` > Cn: out_t rows are ldt wide and columns [Cn, ldt) are written as zeros."""
     code = _code(out_t) if out_t is not None else F32
     ref = in1 if in1 is not None else w
     _lib.call("fpm_instnorm", code, _p(in1), _p(in2), B, P, Cn, _p(nvalid), _p(onehot_bias), _p(w), _p(b),
-              float(eps), _p(out_f), _p(out_t), _p(gmax), _stream(ref))
+              float(eps), _p(out_f), _p(out_t), int(ldt), _p(gmax), _stream(ref))
 
 
 def afau_head(gr, gc, B, E, r0w, r0b, r2w, r2b, c0w, c0b, c2w, c2b, ks):

@@ -107,7 +107,7 @@ int fpm_crossset_attn_fwd(int dtype, const float* cost, long c_sb, long c_ld, in
                           const float* mix2w, const float* mix2b, void* out, void* stream);
 int fpm_instnorm(int dtype, const float* in1, const float* in2, int B, int P, int Cn, const int* nvalid,
                  const float* onehot_bias, const float* w, const float* bias, float eps, float* out_f, void* out_t,
-                 float* gmax, void* stream);
+                 int ldt, float* gmax, void* stream);
 int fpm_afau_head(const float* gr, const float* gc, int B, int E, const float* r0w, const float* r0b,
                   const float* r2w, const float* r2b, const float* c0w, const float* c0b, const float* c2w,
                   const float* c2b, float* ks, void* stream);

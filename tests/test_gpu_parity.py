@@ -260,3 +260,30 @@ def test_gconv_golden():
     y2 = gc(A.to(DEV), x.to(DEV), norm=False).cpu()
     ref = O.gconv(A, x, *(torch.from_numpy(z[k]) for k in ("a_w", "a_b", "u_w", "u_b")), norm=False)
     assert (y2 - ref).abs().max() < 1e-5
+
+
+@pytest.mark.parametrize("M,N,K,batch,epi,f32out,gather", [
+    (1000, 600, 256, 1, 1, True, False),      # AFA-U W2 / Wc shape: N tail, 256x128 tiles
+    (1000, 256, 640, 1, 1, False, False),     # FFN W1 (zero-padded K), bf16 out
+    (2048, 768, 768, 1, 0, False, True),      # gathered rows, 256x256 tiles
+    (600, 512, 128, 3, 0, True, False),       # batched
+])
+def test_gemm_big_vs_torch(M, N, K, batch, epi, f32out, gather):
+    """The 256-row LDS-DMA bf16 kernel (gemm_big.h) through fpm_gemm: bias, ReLU, fp32/bf16 out,
+    row gather, batch strides, N tails."""
+    g = torch.Generator().manual_seed(M + N)
+    A = torch.randn(batch, M + 17, K, generator=g).to(torch.bfloat16)
+    Bm = (torch.randn(batch, N, K, generator=g) * 0.1).to(torch.bfloat16)
+    bias = torch.randn(N, generator=g)
+    rows = torch.randint(0, M + 17, (M,), generator=g) if gather else None
+    Ad, Bd = A.to(DEV), Bm.to(DEV)
+    out = torch.empty(batch, M, N, device=DEV, dtype=torch.float32 if f32out else torch.bfloat16)
+    kw = dict(out_f=out) if f32out else dict(out_t=out)
+    ops.gemm(Ad, Bd, M, N, K, K, K, batch=batch, sA=(M + 17) * K, sB=N * K, sC=M * N,
+             a_rows=rows.to(DEV).int() if gather else None, epi=epi, bias=bias.to(DEV), **kw)
+    Af = A.float()[:, rows] if gather else A.float()[:, :M]
+    ref = Af @ Bm.float().transpose(1, 2) + bias
+    if epi == 1:
+        ref = torch.relu(ref)
+    tol = 2e-3 if f32out else 1e-2
+    assert ((out.float().cpu() - ref).abs().max() / ref.abs().max()) < tol
