@@ -31,9 +31,9 @@ SIGNATURES = {
     "fpm_spline_conv_fwd": (I, [I, P, P, L, L, I, P, P, P, P, L, I, P, P, P, P, P]),
     "fpm_edge_diff": (I, [P, P, P, L, I, P, P]),
     "fpm_edge_diff_padded": (I, [P, P, P, P, P, P, L, I, P, P]),
-    "fpm_kron_gnn_layer_fwd": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, P, P]),
+    "fpm_kron_gnn_layer_fwd": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P]),
     "fpm_gnn_param_count": (I, [I]),
-    "fpm_node_classifier": (I, [P, I, I, I, P, P, P, P]),
+    "fpm_node_classifier": (I, [P, I, I, I, P, P, P, P, P]),
     "fpm_crossset_attn_fwd": (I, [I, P, L, L, I, I, I, P, P, I, P, P, P, P, P, P]),
     "fpm_instnorm": (I, [I, P, P, I, I, I, P, P, P, P, F, P, P, I, P, P]),
     "fpm_afau_head": (I, [P, P, I, I, P, P, P, P, P, P, P, P, P, P]),

@@ -6,11 +6,26 @@
 //                  / ( deg1(i) deg2(d) + D[d][i] ),   D = [d*n1max + i < n1b*n2b]  (quirk A.10(ii))
 // One workgroup per (graph-2 node d, pair), one thread per graph-1 node i: the rows X[c][b][:] of
 // d's neighbours are summed (coalesced) into LDS, then each thread gathers its i's graph-1
-// neighbours from LDS and runs the node MLPs: x1 = lin_l(agg) + lin_r(x) + relu(W2 relu(W1 x + b1) + b2), z = classifier(x1).
+// neighbours from LDS and runs the node MLPs: x1 = lin_l(agg) + lin_r(x) + relu(W2 relu(W1 x + b1)
+// + b2), z = classifier(x1).  (An fp32-MFMA variant of the MLPs measured slower: the layer is bound
+// by the neighbour-row gathers, not the MLP arithmetic.)
 // Layout: X[b][c][d][i] (channel-major, i = graph-1 node fastest), p(i,d) = d*n1max + i.
+// Block order: all (d) blocks of a pair run on ONE XCD (workgroups are dealt to the 8 XCDs
+// round-robin by linear id), so the pair's 17-channel slab (4.4 MB at n = 256) is re-read from
+// that XCD's L2 by the ~6 neighbour blocks instead of from the fabric.
 #include "fpm_common.h"
 
 namespace {
+
+// linear block id -> (pair b, graph-2 node d): XCD x = id % 8 takes pairs x, x+8, ... in d order
+__device__ __forceinline__ bool pair_block(int n2max, int B, int& b, int& d) {
+    const int x = blockIdx.x & 7, k = blockIdx.x >> 3;
+    b = (k / n2max) * 8 + x;
+    d = k % n2max;
+    return b < B;
+}
+
+inline unsigned pair_grid(int n2max, int B) { return (unsigned)(((B + 7) / 8) * 8 * n2max); }
 
 // packed per-layer parameters (f32): Wl[16][C] bl[16] Wr[16][C] W1[16][C] b1[16] W2[16][16] b2[16] wc[16] bc
 template <int C>
@@ -20,12 +35,13 @@ struct GnnPack {
 };
 
 template <int C>
-__global__ __launch_bounds__(1024) void gnn_layer_kernel(const float* __restrict__ X, int n1max, int n2max,
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6, 8))) void gnn_layer_kernel(const float* __restrict__ X, int n1max, int n2max,
                                                          const int* __restrict__ ptr1, const int* __restrict__ nbr1,
                                                          const int* __restrict__ ptr2, const int* __restrict__ nbr2,
                                                          const int* __restrict__ n1, const int* __restrict__ n2,
                                                          const float* __restrict__ W, float* __restrict__ Xo,
-                                                         float* __restrict__ zbuf) {
+                                                         float* __restrict__ zbuf, float* __restrict__ vpart,
+                                                         const float* __restrict__ cls_w, int B) {
     // one thread per graph-1 node i (blockDim >= n1max): no loop, so the uniform weight loads
     // stay scalar (s_load, SGPR operands of the FMAs) instead of being hoisted into VGPRs.
     using P = GnnPack<C>;
@@ -33,7 +49,9 @@ __global__ __launch_bounds__(1024) void gnn_layer_kernel(const float* __restrict
     __shared__ int nb2[64];
     __shared__ int nnb2;
 
-    const int d = blockIdx.x, b = blockIdx.y, i = threadIdx.x;
+    int d, b;
+    if (!pair_block(n2max, B, b, d)) return;
+    const int i = threadIdx.x;
     const long N = (long)n1max * n2max;
     const float* Xb = X + (long)b * C * N;
     if (i == 0) {
@@ -92,7 +110,7 @@ __global__ __launch_bounds__(1024) void gnn_layer_kernel(const float* __restrict
         for (int c = 0; c < C; ++c) s += W[P::W1 + m * C + c] * x[c];
         h[m] = fmaxf(s, 0.f);
     }
-    float z = 0.f;
+    float z = 0.f, vp = 0.f;
     float* Xob = Xo + (long)b * 17 * N + p;
 #pragma unroll
     for (int o = 0; o < 16; ++o) {
@@ -105,23 +123,33 @@ __global__ __launch_bounds__(1024) void gnn_layer_kernel(const float* __restrict
 #pragma unroll
         for (int m = 0; m < 16; ++m) t += W[P::W2 + o * 16 + m] * h[m];
         float x1 = ((l + W[P::bl + o]) + r) + fmaxf(t + W[P::b2 + o], 0.f);
-        Xob[(long)o * N] = x1;
+        if (vpart) vp = fmaf(cls_w[o], x1, vp);      // last layer: only w[0:16] . x1 is consumed
+        else Xob[(long)o * N] = x1;
         z += W[P::wc + o] * x1;
     }
+    if (vpart) vpart[(long)b * N + p] = vp;
     zbuf[(long)b * N + p] = z + W[P::bc];
 }
 
-// v[p] = classifier(emb[p]) (ngm.py:368), written as s[b][i][j] = v[b][j*n1max + i] (ngm.py:369)
+// v[p] = classifier(emb[p]) (ngm.py:368), written as s[b][i][j] = v[b][j*n1max + i] (ngm.py:369).
+// With vpart (the last GNN layer's w[0:16] . x1, fused there) only channel 16 (its Sinkhorn) is read.
 __global__ __launch_bounds__(256) void node_classifier_kernel(const float* __restrict__ X, int n1max, int n2max,
                                                               const float* __restrict__ w, const float* __restrict__ bias,
-                                                              float* __restrict__ s) {
-    const int d = blockIdx.x, b = blockIdx.y;
+                                                              const float* __restrict__ vpart, float* __restrict__ s,
+                                                              int B) {
+    int d, b;
+    if (!pair_block(n2max, B, b, d)) return;
     const long N = (long)n1max * n2max;
     for (int i = threadIdx.x; i < n1max; i += 256) {
         const long p = (long)d * n1max + i;
-        float acc = 0.f;
+        float acc;
+        if (vpart) {
+            acc = fmaf(w[16], X[(long)b * 17 * N + 16L * N + p], vpart[(long)b * N + p]);
+        } else {
+            acc = 0.f;
 #pragma unroll
-        for (int c = 0; c < 17; ++c) acc += w[c] * X[(long)b * 17 * N + (long)c * N + p];
+            for (int c = 0; c < 17; ++c) acc += w[c] * X[(long)b * 17 * N + (long)c * N + p];
+        }
         s[(long)b * N + (long)i * n2max + d] = acc + bias[0];
     }
 }
@@ -130,29 +158,31 @@ __global__ __launch_bounds__(256) void node_classifier_kernel(const float* __res
 
 extern "C" int fpm_kron_gnn_layer_fwd(const float* X, int C, int B, int n1max, int n2max, const int* ptr1,
                                       const int* nbr1, const int* ptr2, const int* nbr2, const int* n1, const int* n2,
-                                      const float* params, float* Xout, float* zbuf, void* stream) {
+                                      const float* params, float* Xout, float* zbuf, float* vpart, const float* cls_w,
+                                      void* stream) {
     FPM_CHECK_ARG(C == 1 || C == 17, "gnn_layer: C must be 1 or 17 (got %d)", C);
+    FPM_CHECK_ARG(!vpart || cls_w, "gnn_layer: vpart needs cls_w");
     if (B == 0) return 0;
     FPM_CHECK_ARG(n1max <= 1024, "gnn_layer: n1max must be <= 1024");
-    dim3 grid(n2max, B);
-    const int threads = (n1max + 63) / 64 * 64;
+    dim3 grid(pair_grid(n2max, B));
     hipStream_t st = (hipStream_t)stream;
     const size_t sh = (size_t)C * n1max * 4;
+    const int threads = (n1max + 63) / 64 * 64;
     if (C == 1)
         hipLaunchKernelGGL((gnn_layer_kernel<1>), grid, dim3(threads), sh, st, X, n1max, n2max, ptr1, nbr1, ptr2, nbr2,
-                           n1, n2, params, Xout, zbuf);
+                           n1, n2, params, Xout, zbuf, vpart, cls_w, B);
     else
-        hipLaunchKernelGGL((gnn_layer_kernel<17>), grid, dim3(threads), sh, st, X, n1max, n2max, ptr1, nbr1, ptr2,
-                           nbr2, n1, n2, params, Xout, zbuf);
+        hipLaunchKernelGGL((gnn_layer_kernel<17>), grid, dim3(threads), sh, st, X, n1max, n2max, ptr1, nbr1, ptr2, nbr2,
+                           n1, n2, params, Xout, zbuf, vpart, cls_w, B);
     return fpm::check_launch("fpm_kron_gnn_layer_fwd");
 }
 
 extern "C" int fpm_gnn_param_count(int C) { return C == 1 ? GnnPack<1>::total : GnnPack<17>::total; }
 
 extern "C" int fpm_node_classifier(const float* X, int B, int n1max, int n2max, const float* w, const float* bias,
-                                   float* s, void* stream) {
+                                   const float* vpart, float* s, void* stream) {
     if (B == 0) return 0;
-    hipLaunchKernelGGL(node_classifier_kernel, dim3(n2max, B), dim3(256), 0, (hipStream_t)stream, X, n1max, n2max, w,
-                       bias, s);
+    hipLaunchKernelGGL(node_classifier_kernel, dim3(pair_grid(n2max, B)), dim3(256), 0, (hipStream_t)stream, X, n1max,
+                       n2max, w, bias, vpart, s, B);
     return fpm::check_launch("fpm_node_classifier");
 }

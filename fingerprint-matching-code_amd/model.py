@@ -269,17 +269,20 @@ class Net(nn.Module):
         csr1 = ops.plan_csr(plan0, bt.E[0], B * n1max)
         csr2 = ops.plan_csr(plan1, bt.E[1], B * n2max)
         zbuf = torch.empty(B, n2max, n1max, device=dev, dtype=torch.float32)
+        vpart = torch.empty(B, n2max, n1max, device=dev, dtype=torch.float32)
         Cin = 1
         for l in range(C.GNN_LAYER):
             Xn = torch.empty(B, 17, n2max, n1max, device=dev, dtype=torch.float32)
-            ops.gnn_layer(X, Cin, B, n1max, n2max, csr1, csr2, bt.n1, bt.n2, wp["gnn%d" % l], Xn, zbuf)
+            last = l == C.GNN_LAYER - 1      # fuse the final classifier's x1 part (ngm.py:368)
+            ops.gnn_layer(X, Cin, B, n1max, n2max, csr1, csr2, bt.n1, bt.n2, wp["gnn%d" % l], Xn, zbuf,
+                          vpart=vpart if last else None, cls_w=wp["cls_w"] if last else None)
             # Sinkhorn(20, tau) on Z[i][j] = z[j*n1max + i], written into channel 16 (gnn.py:217-222)
             ops.sinkhorn(zbuf.transpose(1, 2), bt.n1, bt.n2, C.GNN_SK_ITER, self.tau, True,
                          out=Xn[:, 16].transpose(1, 2))
             X, Cin = Xn, 17
             self._mark("gnn%d" % l)
         s = s_out if s_out is not None else torch.empty(B, n1max, n2max, device=dev, dtype=torch.float32)
-        ops.node_classifier(X, B, n1max, n2max, wp["cls_w"], wp["cls_b"], s)
+        ops.node_classifier(X, B, n1max, n2max, wp["cls_w"], wp["cls_b"], s, vpart=vpart)
         ss = ops.sinkhorn(s, bt.n1, bt.n2, C.SK_ITER_NUM, self.tau, True, out=ss_out)
         self._mark("final_sinkhorn")
         out = dict(s=s, ss=ss, Kp=Kp[:, 0].transpose(1, 2), coef=coef)

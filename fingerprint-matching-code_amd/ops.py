@@ -146,16 +146,16 @@ def edge_diff_padded(x, src, dst, pair, row, nrows, cscale=None):
     return out
 
 
-def gnn_layer(X, C, B, n1max, n2max, csr1, csr2, n1, n2, params, Xout, zbuf):
-    _dev(X, n1, n2, params, Xout, zbuf)
+def gnn_layer(X, C, B, n1max, n2max, csr1, csr2, n1, n2, params, Xout, zbuf, vpart=None, cls_w=None):
+    _dev(X, n1, n2, params, Xout, zbuf, vpart, cls_w)
     _lib.call("fpm_kron_gnn_layer_fwd", _p(X), C, B, n1max, n2max, ctypes.c_void_p(csr1[0]),
               ctypes.c_void_p(csr1[1]), ctypes.c_void_p(csr2[0]), ctypes.c_void_p(csr2[1]), _p(n1), _p(n2),
-              _p(params), _p(Xout), _p(zbuf), _stream(X))
+              _p(params), _p(Xout), _p(zbuf), _p(vpart), _p(cls_w), _stream(X))
 
 
-def node_classifier(X, B, n1max, n2max, w, b, out):
-    _dev(X, w, b, out)
-    _lib.call("fpm_node_classifier", _p(X), B, n1max, n2max, _p(w), _p(b), _p(out), _stream(X))
+def node_classifier(X, B, n1max, n2max, w, b, out, vpart=None):
+    _dev(X, w, b, out, vpart)
+    _lib.call("fpm_node_classifier", _p(X), B, n1max, n2max, _p(w), _p(b), _p(vpart), _p(out), _stream(X))
 
 
 def crossset_attn(cost, n2, Wv, mix1w, mix1b, mix2w, mix2b, out):

@@ -92,14 +92,17 @@ int fpm_edge_diff_padded(const float* x, const int* src, const int* dst, const i
  * classifier (src/model/gnn.py:207-218; pattern from factorize_graph_matching.py:57-95 and
  * gmdataset.py:614-642), factorised so the n1*n2 x n1*n2 pattern is never built.
  * X: (B, C, n2max, n1max) with C in {1, 17}; Xout channels 0..15 and zbuf (B, n2max, n1max)
- * are written; the caller runs fpm_sinkhorn_log_fwd(zbuf -> Xout channel 16). */
+ * are written; the caller runs fpm_sinkhorn_log_fwd(zbuf -> Xout channel 16).  Last layer: pass
+ * vpart (B, n2max, n1max) and the final classifier weights cls_w (17): vpart = cls_w[0:16] . x1
+ * is written instead of Xout channels 0..15 (fpm_node_classifier then reads vpart + channel 16). */
 int fpm_kron_gnn_layer_fwd(const float* X, int C, int B, int n1max, int n2max, const int* ptr1, const int* nbr1,
                            const int* ptr2, const int* nbr2, const int* n1, const int* n2, const float* params,
-                           float* Xout, float* zbuf, void* stream);
+                           float* Xout, float* zbuf, float* vpart, const float* cls_w, void* stream);
 int fpm_gnn_param_count(int C);
-/* final classifier (ngm.py:368-369): s[b][i][j] = w . X[b][:, j, i] + bias */
-int fpm_node_classifier(const float* X, int B, int n1max, int n2max, const float* w, const float* bias, float* s,
-                        void* stream);
+/* final classifier (ngm.py:368-369): s[b][i][j] = w . X[b][:, j, i] + bias; with vpart (NULL =
+ * all 17 channels): s = vpart + w[16] X[b][16, j, i] + bias */
+int fpm_node_classifier(const float* X, int B, int n1max, int n2max, const float* w, const float* bias,
+                        const float* vpart, float* s, void* stream);
 
 /* ---- AFA-U k regressor (ngm.py:386-412, src/model/afau.py) ------------------------------------ */
 int fpm_crossset_attn_fwd(int dtype, const float* cost, long c_sb, long c_ld, int B, int n1max, int n2max,
