@@ -29,15 +29,22 @@ class DeviceBatch:
         self.edge_off = edge_off
         self._splits = {}
 
-    def split(self, k):
-        """k contiguous sub-batches of pairs (views of x/w, renumbered edge copies); cached."""
+    def split(self, k, tail=0):
+        """k contiguous sub-batches of pairs (views of x/w, renumbered edge copies); cached.
+        ``tail`` > 0 halves the last chunk ``tail`` times (a short final chunk shortens the host
+        Hungarian that runs after the GPU has finished)."""
         if k <= 1 or self.B < 2:
             return [self]
-        if k in self._splits:
-            return self._splits[k]
+        key = (k, tail)
+        if key in self._splits:
+            return self._splits[key]
         if self.edge_off is None:
             raise ValueError("split() needs per-pair edge offsets")
         bounds = [round(i * self.B / k) for i in range(k + 1)]
+        for _ in range(tail):
+            a, b = bounds[-2], bounds[-1]
+            if b - a >= 2:
+                bounds.insert(-1, (a + b) // 2)
         parts = []
         for c in range(k):
             b0, b1 = bounds[c], bounds[c + 1]
@@ -57,7 +64,7 @@ class DeviceBatch:
                               nmax=self.nmax, edge_off=eo)
             sub.pair_range = (b0, b1)
             parts.append(sub)
-        self._splits[k] = parts
+        self._splits[key] = parts
         return parts
 
     @property

@@ -67,6 +67,7 @@ class Net(nn.Module):
         self._pinned = None
         self._stream_cache = {}
         self.n_streams = max(1, int(os.environ.get("FPM_STREAMS", "2")))
+        self.tail_splits = int(os.environ.get("FPM_TAIL", "1"))
         self._keep_feats = False
         self._stage_timing = os.environ.get("FPM_STAGE_TIMING", "0") == "1"
         self.stage_times = {}
@@ -237,8 +238,20 @@ class Net(nn.Module):
                  ldc=e2, sC=e1 * e2, n1=cnt[1], n2=cnt[0])
         return Ke
 
-    def run_gpu_stage(self, bt, keep_feats=False, s_out=None, ss_out=None):
-        """Everything up to ds_mat on the GPU.  Returns a dict of device tensors."""
+    def global_coef(self, bt):
+        """Global weights w = L2norm(cat(w1, w2)) and vertex-affinity coefficients c = tanh(A w + a)
+        for every pair of ``bt`` (ngm.py:262-268, affinity_layer.py:13); one launch per forward."""
+        wp = self.packed(bt.device)
+        gw = torch.cat([bt.w[0], bt.w[1]], dim=1)
+        gw = (gw / torch.norm(gw, dim=1, keepdim=True)).contiguous()
+        coef = torch.empty(bt.B, C.NODE_FEATURE_DIM, device=bt.device, dtype=torch.float32)
+        ops.gemm(gw, wp["aff_w"], bt.B, C.NODE_FEATURE_DIM, C.GLOBAL_STATE_DIM, C.GLOBAL_STATE_DIM,
+                 C.GLOBAL_STATE_DIM, epi=ops.EPI_TANH, bias=wp["aff_b"], out_f=coef)
+        return gw, coef
+
+    def run_gpu_stage(self, bt, keep_feats=False, s_out=None, ss_out=None, gc=None):
+        """Everything up to ds_mat on the GPU.  Returns a dict of device tensors.  ``gc``: this
+        batch's rows of global_coef() when computed for a parent batch."""
         keep_feats = keep_feats or self.compute_ke
         self._keep_feats = keep_feats
         if self._stage_timing:
@@ -248,12 +261,7 @@ class Net(nn.Module):
         dev = bt.device
         B, n1max, n2max = bt.B, bt.n1max, bt.n2max
         N = n1max * n2max
-        # global weights + vertex-affinity coefficients c_b = tanh(A w_b + a)  (ngm.py:262-268, affinity_layer.py:13)
-        gw = torch.cat([bt.w[0], bt.w[1]], dim=1)
-        gw = (gw / torch.norm(gw, dim=1, keepdim=True)).contiguous()
-        coef = torch.empty(B, C.NODE_FEATURE_DIM, device=dev, dtype=torch.float32)
-        ops.gemm(gw, wp["aff_w"], B, C.NODE_FEATURE_DIM, C.GLOBAL_STATE_DIM, C.GLOBAL_STATE_DIM, C.GLOBAL_STATE_DIM,
-                 epi=ops.EPI_TANH, bias=wp["aff_b"], out_f=coef)
+        gw, coef = gc if gc is not None else self.global_coef(bt)
         self._mark("coef")
         plan0, x1c, f1 = self._spline_side(wp, bt, 0, coef)
         plan1, x2, f2 = self._spline_side(wp, bt, 1, None)
@@ -307,10 +315,11 @@ class Net(nn.Module):
             return max(1, min(int(os.environ["FPM_CHUNKS"]), B))
         return max(1, min(8, B // 128))
 
-    def _stage_a(self, part, b0, b1, o, keep_feats, gt_ks, min_pt, st):
+    def _stage_a(self, part, b0, b1, o, keep_feats, gt_ks, min_pt, st, gc):
         """GPU stage of one chunk (on its stream): everything up to ds_mat, then its D2H copy."""
         dev = part.device
-        r = self.run_gpu_stage(part, keep_feats, s_out=o["s"][b0:b1], ss_out=o["ss"][b0:b1])
+        r = self.run_gpu_stage(part, keep_feats, s_out=o["s"][b0:b1], ss_out=o["ss"][b0:b1],
+                               gc=(gc[0][b0:b1], gc[1][b0:b1]))
         ks = o["k_prob"][b0:b1]
         if self.regression:
             ks.copy_(self._afau(self.packed(dev), o["ss"][b0:b1], part))
@@ -356,7 +365,7 @@ class Net(nn.Module):
         K = chunks if chunks is not None else self.pipeline_chunks(B)
         if self.compute_ke:
             K = 1          # Ke blocks are padded to per-chunk edge maxima: keep one chunk
-        parts = bt.split(K)
+        parts = bt.split(K, self.tail_splits if K > 1 else 0)
         t0 = time.perf_counter()
         min_pt = torch.minimum(bt.n1, bt.n2).to(torch.float32)
         if gt_perm is None:
@@ -372,16 +381,19 @@ class Net(nn.Module):
         main = torch.cuda.current_stream(dev)
         ev_start = torch.cuda.Event(enable_timing=True)
         ev_start.record(main)
+        gc = self.global_coef(bt)
+        ev_coef = torch.cuda.Event()
+        ev_coef.record(main)
         streams = self._streams(dev) if (len(parts) > 1 and self.n_streams > 1) else [main]
         for st in streams:
             if st is not main:
-                st.wait_event(ev_start)
+                st.wait_event(ev_coef)
         outs, events = [], []
         for c, part in enumerate(parts):
             st = streams[c % len(streams)]
             b0, b1 = getattr(part, "pair_range", (0, B))
             with torch.cuda.stream(st):
-                r, ev = self._stage_a(part, b0, b1, o, keep_feats, gt_ks, min_pt, st)
+                r, ev = self._stage_a(part, b0, b1, o, keep_feats, gt_ks, min_pt, st, gc)
             outs.append(r)
             events.append(ev)
         t_lsa, t_first = 0.0, None
