@@ -46,7 +46,7 @@ class DeviceBatch:
             if b - a >= 2:
                 bounds.insert(-1, (a + b) // 2)
         parts = []
-        for c in range(k):
+        for c in range(len(bounds) - 1):
             b0, b1 = bounds[c], bounds[c + 1]
             if b1 <= b0:
                 continue

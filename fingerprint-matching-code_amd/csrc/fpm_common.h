@@ -53,6 +53,12 @@ __device__ __forceinline__ void store4(bf16_t* p, const float (&v)[4]) {
     *(uint2*)p = o;
 }
 
+// native base-2 transcendental (v_exp_f32 / v_log_f32, ~1 ulp): the log-domain kernels keep their
+// values in log2 units so each exp is one instruction instead of expf's range-reduced sequence
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float fast_log2(float x) { return __builtin_amdgcn_logf(x); }
+constexpr float LOG2E_F = 1.4426950408889634f;
+
 __device__ __forceinline__ float warp_max(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));

@@ -8,6 +8,7 @@
 // only per-iteration state is u, v.  Semantics kept: row step first, per-pair valid block
 // [:n1, :n2], n1 > n2 handled on the transpose, dummy rows (value -100 in log space) when
 // dummy_row and rows < cols, output exp(L) on the block and 0 in the padding.
+// Arithmetic runs in log2 units (L2 = L log2 e): every exp/log is one native v_exp_f32 / v_log_f32.
 #include "fpm_common.h"
 
 namespace {
@@ -29,7 +30,7 @@ struct SinkArgs {
 __device__ __forceinline__ void lse_combine(float& m, float& s, float mo, float so) {
     float mn = fmaxf(m, mo);
     if (mn == -INFINITY) { m = mn; s = 0.f; return; }
-    s = s * expf(m - mn) + so * expf(mo - mn);
+    s = s * fpm::fast_exp2(m - mn) + so * fpm::fast_exp2(mo - mn);
     m = mn;
 }
 
@@ -61,7 +62,7 @@ __global__ __launch_bounds__(1024) void sinkhorn_reg_kernel(SinkArgs a) {
     const int R = transposed ? n2b : n1b;   // algorithmic rows
     const int C = transposed ? n1b : n2b;   // algorithmic cols
     const int nd = (a.dummy_row && C > R) ? (C - R) : 0;
-    const float lognd = nd > 0 ? logf((float)nd) : 0.f;
+    const float lognd = nd > 0 ? fpm::fast_log2((float)nd) : 0.f;
     // physical dims: pc (lanes) = unit-stride dim
     const int limPR = a.contig_j ? n1b : n2b;
     const int limPC = a.contig_j ? n2b : n1b;
@@ -84,7 +85,7 @@ __global__ __launch_bounds__(1024) void sinkhorn_reg_kernel(SinkArgs a) {
         for (int f = 0; f < EC; ++f) {
             const int pc = tc + 32 * f;
             float v = -INFINITY;
-            if (pr < limPR && pc < limPC) v = in[pr * spr + pc * spc] / a.tau;
+            if (pr < limPR && pc < limPC) v = (in[pr * spr + pc * spc] / a.tau) * fpm::LOG2E_F;
             M[e][f] = v;
         }
     }
@@ -92,6 +93,7 @@ __global__ __launch_bounds__(1024) void sinkhorn_reg_kernel(SinkArgs a) {
     for (int f = 0; f < EC; ++f) pC[f] = 0.f;
 
     float ud = 0.f;  // potential of the (identical) dummy rows
+    const float DUMMY = -100.f * fpm::LOG2E_F;   // the dummy rows' log value, in log2 units
 
     // potR[e] = lse_f(M - pC) (+ dummy term)
     auto update_R = [&](bool add_dummy) {
@@ -101,16 +103,16 @@ __global__ __launch_bounds__(1024) void sinkhorn_reg_kernel(SinkArgs a) {
 #pragma unroll
             for (int f = 0; f < EC; ++f) m = fmaxf(m, M[e][f] - pC[f]);
             m = lane32_max(m);
-            float dv = -100.f - ud;
+            float dv = DUMMY - ud;
             if (add_dummy) m = fmaxf(m, dv);
             float s = 0.f;
             if (m != -INFINITY) {
 #pragma unroll
-                for (int f = 0; f < EC; ++f) s += expf(M[e][f] - pC[f] - m);
+                for (int f = 0; f < EC; ++f) s += fpm::fast_exp2(M[e][f] - pC[f] - m);
             }
             s = lane32_sum(s);
-            if (add_dummy && m != -INFINITY) s += (float)nd * expf(dv - m);
-            pR[e] = (m == -INFINITY) ? 0.f : m + logf(s);
+            if (add_dummy && m != -INFINITY) s += (float)nd * fpm::fast_exp2(dv - m);
+            pR[e] = (m == -INFINITY) ? 0.f : m + fpm::fast_log2(s);
         }
     };
     // potC[f] = lse_e(M - pR) (+ dummy term): across the 32 thread-rows via LDS
@@ -123,7 +125,7 @@ __global__ __launch_bounds__(1024) void sinkhorn_reg_kernel(SinkArgs a) {
             float s = 0.f;
             if (m != -INFINITY) {
 #pragma unroll
-                for (int e = 0; e < ER; ++e) s += expf(M[e][f] - pR[e] - m);
+                for (int e = 0; e < ER; ++e) s += fpm::fast_exp2(M[e][f] - pR[e] - m);
             }
             float mo = __shfl_xor(m, 32), so = __shfl_xor(s, 32);
             lse_combine(m, s, mo, so);
@@ -136,8 +138,8 @@ __global__ __launch_bounds__(1024) void sinkhorn_reg_kernel(SinkArgs a) {
         if (tid < NCOL) {
             float m = red_m[0][tid], s = red_s[0][tid];
             for (int w = 1; w < 16; ++w) lse_combine(m, s, red_m[w][tid], red_s[w][tid]);
-            if (add_dummy) lse_combine(m, s, -100.f - ud, (float)nd);
-            fin[tid] = (m == -INFINITY) ? 0.f : m + logf(s);
+            if (add_dummy) lse_combine(m, s, DUMMY - ud, (float)nd);
+            fin[tid] = (m == -INFINITY) ? 0.f : m + fpm::fast_log2(s);
         }
         __syncthreads();
 #pragma unroll
@@ -149,21 +151,21 @@ __global__ __launch_bounds__(1024) void sinkhorn_reg_kernel(SinkArgs a) {
         if (u_on_R) {  // v on the pc side
 #pragma unroll
             for (int f = 0; f < EC; ++f)
-                if (tc + 32 * f < limPC) m = fmaxf(m, -100.f - pC[f]);
+                if (tc + 32 * f < limPC) m = fmaxf(m, DUMMY - pC[f]);
             m = lane32_max(m);
 #pragma unroll
             for (int f = 0; f < EC; ++f)
-                if (tc + 32 * f < limPC) s += expf(-100.f - pC[f] - m);
+                if (tc + 32 * f < limPC) s += fpm::fast_exp2(DUMMY - pC[f] - m);
             s = lane32_sum(s);
-            ud = m + logf(s);
+            ud = m + fpm::fast_log2(s);
         } else {       // v on the pr side: block reduction over threads with tc == 0
             if (tc == 0) {
 #pragma unroll
                 for (int e = 0; e < ER; ++e)
-                    if (tr + 32 * e < limPR) m = fmaxf(m, -100.f - pR[e]);
+                    if (tr + 32 * e < limPR) m = fmaxf(m, DUMMY - pR[e]);
 #pragma unroll
                 for (int e = 0; e < ER; ++e)
-                    if (tr + 32 * e < limPR) s += expf(-100.f - pR[e] - m);
+                    if (tr + 32 * e < limPR) s += fpm::fast_exp2(DUMMY - pR[e] - m);
             }
             float mo = __shfl_xor(m, 32), so = __shfl_xor(s, 32);
             lse_combine(m, s, mo, so);
@@ -171,7 +173,7 @@ __global__ __launch_bounds__(1024) void sinkhorn_reg_kernel(SinkArgs a) {
             __syncthreads();
             m = blk_m[0]; s = blk_s[0];
             for (int w = 1; w < 16; ++w) lse_combine(m, s, blk_m[w], blk_s[w]);
-            ud = m + logf(s);
+            ud = m + fpm::fast_log2(s);
             __syncthreads();
         }
     };
@@ -198,7 +200,7 @@ __global__ __launch_bounds__(1024) void sinkhorn_reg_kernel(SinkArgs a) {
             const int pc = tc + 32 * f;
             if (pc >= boxPC) continue;
             float v = 0.f;
-            if (pr < limPR && pc < limPC) v = expf(M[e][f] - pR[e] - pC[f]);
+            if (pr < limPR && pc < limPC) v = fpm::fast_exp2(M[e][f] - pR[e] - pC[f]);
             out[pr * opr + pc * opc] = v;
         }
     }
