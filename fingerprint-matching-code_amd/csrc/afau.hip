@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256) void afau_row_attn_kernel(const float* __restr
             mx = fpm::warp_max(mx);
             float sum = 0.f;
             for (int j = lane; j < n2max; j += 64) {
-                float e = expf(Pm[lr * n2max + j] - mx);
+                float e = fpm::fast_exp2((Pm[lr * n2max + j] - mx) * fpm::LOG2E_F);
                 Pm[lr * n2max + j] = e;
                 sum += e;
             }

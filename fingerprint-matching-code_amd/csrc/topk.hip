@@ -7,14 +7,18 @@
 // function of the column potentials seen at the last row step (vu), so the state is four
 // scalars and one pass over q per column step is a whole iteration.  The reference's
 // data-dependent ``while any(L > 0)`` continuation is kept (bounded at 64 extra steps).
+// Values are kept in log2 units (L2 = L log2 e; the test L > 0 is unit-free), so each exp/log is
+// one native v_exp_f32 / v_log_f32.
 #include "fpm_common.h"
 
 namespace {
 
+// log2-unit logsumexp of a row's two entries (one term is exp2(0) = 1 exactly, so u >= max and
+// L = a - u <= 0 after a row step, as in the reference)
 __device__ __forceinline__ float urow(float a0, float a1) {
     float m = fmaxf(a0, a1);
     if (m == -INFINITY) return INFINITY;
-    return m + logf(expf(a0 - m) + expf(a1 - m));
+    return m + fpm::fast_log2(fpm::fast_exp2(a0 - m) + fpm::fast_exp2(a1 - m));
 }
 
 template <int NQ>
@@ -60,7 +64,7 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
 
     // dist_mat = -|s - anchor| (soft_topk.py:28-29), then Sinkhorn_m divides by tau (:180);
     // recomputed from s on every pass (keeps 64 values per thread resident instead of 128)
-    const float rtau = tau;
+    const float dscale = fpm::LOG2E_F / tau;   // distances / tau, in log2 units
     // visit every q of this thread: register-resident values (unrolled), then LDS-resident ones
     // (runtime loop: bounded code size and register pressure)
     auto forq = [&](auto&& f) {
@@ -71,8 +75,8 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
             if (tid + 1024 * k < N) f(k, sl[(k - NQR) * 1024 + tid]);
     };
     const float kk = kvec[b];
-    const float lcp0 = logf((float)N - kk);   // log(col_prob[:,0]) = log(n1*n2 - k)
-    const float lcp1 = logf(kk);              // log(col_prob[:,1]) = log(k)
+    const float lcp0 = fpm::fast_log2((float)N - kk);   // log(col_prob[:,0]) = log(n1*n2 - k)
+    const float lcp1 = fpm::fast_log2(kk);              // log(col_prob[:,1]) = log(k)
     // state: L_c(q) = a_c - u(q) [after a row step]  or  ((a_c - u) - lse_c) + lcp_c [after a
     // column step], a_c = D_c - vu_c, u = lse(a_0, a_1).  The last two steps are evaluated with the
     // reference's own operation order, so "L <= 0 after a row step" holds exactly as it does there.
@@ -87,7 +91,7 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
         asm volatile("" : "+v"(lo), "+v"(hi));
     };
     auto Lpair = [&](float sv, float mnl, float mxl, float& L0, float& L1) {
-        float a0 = ((-fabsf(sv - mnl)) / rtau) - vu0, a1 = ((-fabsf(sv - mxl)) / rtau) - vu1;
+        float a0 = (-fabsf(sv - mnl)) * dscale - vu0, a1 = (-fabsf(sv - mxl)) * dscale - vu1;
         float u = urow(a0, a1);
         L0 = a0 - u;
         L1 = a1 - u;
@@ -128,8 +132,8 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
         forq([&](int k, float sv) {
             float L0, L1;
             Lpair(sv, mnl, mxl, L0, L1);
-            if (m0 != -INFINITY) a0 += expf(L0 - m0);
-            if (m1 != -INFINITY) a1 += expf(L1 - m1);
+            if (m0 != -INFINITY) a0 += fpm::fast_exp2(L0 - m0);
+            if (m1 != -INFINITY) a1 += fpm::fast_exp2(L1 - m1);
         });
         a0 = fpm::warp_sum(a0);
         a1 = fpm::warp_sum(a1);
@@ -138,8 +142,8 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
         a0 = 0.f; a1 = 0.f;
         for (int w = 0; w < 16; ++w) { a0 += sa[w]; a1 += sb_[w]; }
         __syncthreads();
-        lse0 = (m0 == -INFINITY) ? -INFINITY : m0 + logf(a0);
-        lse1 = (m1 == -INFINITY) ? -INFINITY : m1 + logf(a1);
+        lse0 = (m0 == -INFINITY) ? -INFINITY : m0 + fpm::fast_log2(a0);
+        lse1 = (m1 == -INFINITY) ? -INFINITY : m1 + fpm::fast_log2(a1);
         last = 2;
     };
     auto any_pos = [&]() -> bool {
@@ -186,7 +190,7 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
         int i = q / n2o, j = q - i * n2o;
         float L0, L1;
         Lpair(sv, mnl, mxl, L0, L1);
-        O[i * old_ + j] = expf(L1);
+        O[i * old_ + j] = fpm::fast_exp2(L1);
     });
 #undef SVAL
 }
