@@ -25,9 +25,15 @@ def _gen(args):
     return (synth.make_graph(seed, p, 0, n), synth.make_graph(seed, p, 1, n))
 
 
+def _under_profiler():
+    """rocprofv3 preloads its tool library and initialises HSA before main: forked workers of such
+    a process can hang, so graph generation stays in-process there."""
+    return "rocprof" in os.environ.get("LD_PRELOAD", "") or any(k.startswith("ROCPROF") for k in os.environ)
+
+
 def make_pairs(seed, first, B, n, workers):
     ids = [(seed, first + b, n) for b in range(B)]
-    if workers <= 1 or B < 8:
+    if workers <= 1 or B < 8 or _under_profiler():
         return [_gen(a) for a in ids]
     import multiprocessing as mp
     with mp.get_context("fork").Pool(workers) as pool:
@@ -132,6 +138,19 @@ def main():
     cnt = ctypes.c_int()
     _lib.call("fpm_profile_read", ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(cnt))
     elapsed = t1 - t0
+    # the same kernel without the second stream's kernels sharing the CUs (one extra, untimed
+    # forward on one stream): its isolated rate, reported beside the in-pipeline one
+    iso_ms = ctypes.c_double()
+    iso_fl = ctypes.c_double()
+    iso_cnt = ctypes.c_int()
+    saved_streams = net.n_streams
+    net.n_streams = 1
+    lib.fpm_profile_enable(1)
+    net.run(bt)
+    torch.cuda.synchronize()
+    lib.fpm_profile_enable(0)
+    net.n_streams = saved_streams
+    _lib.call("fpm_profile_read", ctypes.byref(iso_ms), ctypes.byref(iso_fl), ctypes.byref(iso_cnt))
     if world > 1:
         t = torch.tensor([elapsed, gpu_s, lsa_s], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -167,11 +186,13 @@ def main():
                        "edges_per_graph": E_tot / (2.0 * args.batch), "parallelism": "pair-sharded x%d" % world},
             "gpu_stage_pairs_per_s": args.batch * world * args.steps / gpu_s,
             "host_lsa_ms_per_step": lsa_s / args.steps * 1e3,
-            "roofline": {"kernel": "spline (node, cell) product GEMM (%s, grouped by cell)" % ("gemm256_bf16_kernel" if args.dtype == "bf16" else "gemm_kernel<f32>"),
+            "roofline": {"kernel": "spline (node, cell) product GEMM (%s, grouped by cell)" % ("gemm_big_kernel<256>" if args.dtype == "bf16" else "gemm_kernel<f32>"),
                          "bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak, "traffic": None,
                          "launches": cnt.value, "avg_launch_ms": ms.value / max(cnt.value, 1),
-                         "algorithmic_flops_per_launch": fl.value / max(cnt.value, 1)},
+                         "algorithmic_flops_per_launch": fl.value / max(cnt.value, 1),
+                         "isolated_achieved": (iso_fl.value / (iso_ms.value / 1e3)) / 1e12 if iso_ms.value > 0 else 0.0,
+                         "isolated_avg_launch_ms": iso_ms.value / max(iso_cnt.value, 1)},
             "cpu_baseline": cpu,
             "input_gen_s": t_gen,
         }

@@ -1,8 +1,9 @@
 // MatchClassifier (reference ngm.py:75-106) on matched_sim = s * perm_mat (ngm.py:451-455):
 //   [conv3x3(1->16,pad 1) -> ReLU -> BN(eval) -> MaxPool2] -> [conv3x3(16->32) -> ReLU -> BN -> MaxPool2]
 //   -> global average pool -> Linear(32->1) -> logit (sigmoid applied for cls_prob).
-// Direct convolutions in fp32; stage 1 fuses the s*perm product, stage 2 fuses the average pool
-// into per-block partial sums (deterministic, reduced by the head kernel).
+// fp32 throughout; stage 1 (direct conv) fuses the s*perm product, stage 2 runs conv2 as an
+// implicit GEMM on the fp32 matrix cores and fuses the average pool into per-block partial sums
+// (deterministic, reduced by the head kernel).
 #include "fpm_common.h"
 
 namespace {
@@ -55,78 +56,105 @@ __global__ __launch_bounds__(256) void cls_stage1_kernel(const float* __restrict
     }
 }
 
-// conv2 + ReLU + BN + MaxPool2, then partial sums of the pooled map per channel.
-// thread = (pooled pixel, channel group of 8); block sums written to part[b][blk][32]
+// conv2 (16 -> 32, 3x3, pad 1) + ReLU + BN + MaxPool2 + partial sums of the pooled map per channel,
+// as an implicit GEMM on the fp32 matrix cores (v_mfma_f32_16x16x4_f32: exact fp32 products):
+// out^T[oc][pos] = W2[oc][k] . im2col[k][pos], k = ci*9 + ky*3 + kx (144 = 36 K-steps of 4).
+// Block = one pair, a 16 x 32 tile of pre-pool positions (8 x 16 pooled pixels); the 16-channel
+// input tile with its 1-pixel halo is staged in LDS.  Wave w owns pre-pool rows 4w..4w+3: two
+// row pairs x two 16-column halves; each lane holds the B operand (one im2col entry) per K-step.
+constexpr int C2_TY = 16, C2_TX = 32, C2_LY = C2_TY + 2, C2_LX = C2_TX + 2;
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
 __global__ __launch_bounds__(256) void cls_stage2_kernel(const float* __restrict__ P1, int H1, int W1,
                                                          const float* __restrict__ w2, const float* __restrict__ b2,
                                                          const float* __restrict__ bn_sc, const float* __restrict__ bn_sh,
                                                          float* __restrict__ part) {
-    __shared__ float wsh[32 * 16 * 9];
-    __shared__ float red[256][8];
-    for (int k = threadIdx.x; k < 32 * 144; k += 256) wsh[k] = w2[k];
-    __syncthreads();
+    __shared__ float tin[16 * C2_LY * C2_LX];
+    __shared__ float red[4][32];
     const int H2 = H1 / 2, W2 = W1 / 2;
+    const int tiles_x = (2 * W2 + C2_TX - 1) / C2_TX;
     const int b = blockIdx.y;
-    const int cg = threadIdx.x & 3;         // channels 8*cg .. 8*cg+7
-    const long pix = (long)blockIdx.x * 64 + (threadIdx.x >> 2);
-    float sums[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) sums[k] = 0.f;
-    if (pix < (long)H2 * W2) {
-        const int ph = (int)(pix / W2), pw = (int)(pix - (long)ph * W2);
-        float acc[8][4];
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) acc[k][q] = 0.f;
-        for (int ci = 0; ci < 16; ++ci) {
-            float in[4][4];
-            const float* src = P1 + ((long)b * 16 + ci) * H1 * W1;
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    int y = 2 * ph - 1 + r, x = 2 * pw - 1 + c;
-                    in[r][c] = (y >= 0 && y < H1 && x >= 0 && x < W1) ? src[(long)y * W1 + x] : 0.f;
-                }
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const float* wk = wsh + ((cg * 8 + k) * 16 + ci) * 9;
-#pragma unroll
-                for (int dy = 0; dy < 2; ++dy)
-#pragma unroll
-                    for (int dx = 0; dx < 2; ++dx) {
-                        float a = acc[k][dy * 2 + dx];
-#pragma unroll
-                        for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-                            for (int kx = 0; kx < 3; ++kx) a += wk[ky * 3 + kx] * in[dy + ky][dx + kx];
-                        acc[k][dy * 2 + dx] = a;
-                    }
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int ch = cg * 8 + k;
-            float mx = -INFINITY;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                float v = fmaxf(acc[k][q] + b2[ch], 0.f);
-                v = v * bn_sc[ch] + bn_sh[ch];
-                mx = fmaxf(mx, v);
-            }
-            sums[k] = mx;
-        }
+    const int ty = blockIdx.x / tiles_x, tx = blockIdx.x - ty * tiles_x;
+    const int y0 = ty * C2_TY, x0 = tx * C2_TX;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int g = lane >> 4, col = lane & 15;
+    const float* src = P1 + (long)b * 16 * H1 * W1;
+    for (int k = tid; k < 16 * C2_LY * C2_LX; k += 256) {
+        const int ci = k / (C2_LY * C2_LX), rem = k - ci * (C2_LY * C2_LX);
+        const int yy = rem / C2_LX, xx = rem - yy * C2_LX;
+        const int y = y0 - 1 + yy, x = x0 - 1 + xx;
+        tin[k] = (y >= 0 && y < H1 && x >= 0 && x < W1) ? src[((long)ci * H1 + y) * W1 + x] : 0.f;
     }
+    // A operands: W2[16 mt + col][4 s + g]
+    float wa[2][36];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) red[threadIdx.x][k] = sums[k];
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int s = 0; s < 36; ++s) wa[mt][s] = w2[(16 * mt + col) * 144 + 4 * s + g];
+    float bsh[2][4], bsc[2][4], bsf[2][4];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int oc = 16 * mt + 4 * g + r;
+            bsh[mt][r] = b2[oc];
+            bsc[mt][r] = bn_sc[oc];
+            bsf[mt][r] = bn_sh[oc];
+        }
     __syncthreads();
-    if (threadIdx.x < 32) {
-        const int ch = threadIdx.x, g = ch >> 3, k = ch & 7;
-        float s = 0.f;
-        for (int t = g; t < 256; t += 4) s += red[t][k];
-        part[((long)b * gridDim.x + blockIdx.x) * 32 + ch] = s;
+    float sums[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int rp = 0; rp < 2; ++rp) {
+        const int r0 = wave * 4 + rp * 2;                 // tile row of the pair's first row
+#pragma unroll
+        for (int xh = 0; xh < 2; ++xh) {
+            f32x4_t acc[2][2];                            // [mt][row of the pair]
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int q = 0; q < 2; ++q) acc[mt][q] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+            const int xl = xh * 16 + col;                 // tile column of this lane's position
+#pragma unroll
+            for (int s = 0; s < 36; ++s) {
+                const int k = 4 * s + g, ci = k / 9, t = k - ci * 9, ky = t / 3, kx = t - ky * 3;
+                const float* base = tin + (ci * C2_LY + r0 + ky) * C2_LX + xl + kx;
+                const float v0 = base[0], v1 = base[C2_LX];
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt) {
+                    acc[mt][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[mt][s], v0, acc[mt][0], 0, 0, 0);
+                    acc[mt][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[mt][s], v1, acc[mt][1], 0, 0, 0);
+                }
+            }
+            // ReLU -> BN -> 2x2 max (rows in acc[.][0/1], columns in lanes col, col ^ 1)
+            const int py = (y0 + r0) / 2, px = (x0 + xl) / 2;
+            const bool ok = ((col & 1) == 0) && py < H2 && px < W2;
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float a = fmaxf(acc[mt][0][r] + bsh[mt][r], 0.f) * bsc[mt][r] + bsf[mt][r];
+                    float c = fmaxf(acc[mt][1][r] + bsh[mt][r], 0.f) * bsc[mt][r] + bsf[mt][r];
+                    float m = fmaxf(a, c);
+                    m = fmaxf(m, __shfl_xor(m, 1));
+                    if (ok) sums[mt][r] += m;
+                }
+        }
     }
+    // per-channel block sums: over the 16 columns of each row group, then the 4 waves
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float v = sums[mt][r];
+            v += __shfl_xor(v, 1);
+            v += __shfl_xor(v, 2);
+            v += __shfl_xor(v, 4);
+            v += __shfl_xor(v, 8);
+            if (col == 0) red[wave][16 * mt + 4 * g + r] = v;
+        }
+    __syncthreads();
+    if (tid < 32)
+        part[((long)b * gridDim.x + blockIdx.x) * 32 + tid] = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
 }
 
 __global__ __launch_bounds__(64) void cls_head_kernel(const float* __restrict__ part, int nblk, long npix,
@@ -149,10 +177,14 @@ __global__ __launch_bounds__(64) void cls_head_kernel(const float* __restrict__ 
 
 }  // namespace
 
+static long cls2_blocks(int H1, int W1) {
+    const long H2 = H1 / 2, W2 = W1 / 2;
+    return ((2 * H2 + C2_TY - 1) / C2_TY) * ((2 * W2 + C2_TX - 1) / C2_TX);
+}
+
 extern "C" long fpm_match_cls_ws_floats(int B, int H, int W) {
-    long H1 = H / 2, W1 = W / 2, H2 = H1 / 2, W2 = W1 / 2;
-    long nblk = (H2 * W2 + 63) / 64;
-    return (long)B * 16 * H1 * W1 + (long)B * nblk * 32;
+    long H1 = H / 2, W1 = W / 2;
+    return (long)B * 16 * H1 * W1 + (long)B * cls2_blocks((int)H1, (int)W1) * 32;
 }
 
 // bn*_sc = gamma / sqrt(running_var + eps), bn*_sh = beta - running_mean * bn*_sc (host-folded)
@@ -165,7 +197,7 @@ extern "C" int fpm_match_cls_fwd(const float* s, const float* perm, int B, int H
     hipStream_t st = (hipStream_t)stream;
     const int H1 = H / 2, W1 = W / 2, H2 = H1 / 2, W2 = W1 / 2;
     float* P1 = ws;
-    const long nblk = ((long)H2 * W2 + 63) / 64;
+    const long nblk = cls2_blocks(H1, W1);
     float* part = ws + (long)B * 16 * H1 * W1;
     hipLaunchKernelGGL(cls_stage1_kernel, dim3((unsigned)(((long)H1 * W1 + 255) / 256), B), dim3(256), 0, st, s, perm,
                        H, W, w1, b1, bn1_sc, bn1_sh, P1);
