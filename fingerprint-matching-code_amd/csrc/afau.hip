@@ -21,17 +21,18 @@ __global__ __launch_bounds__(256) void afau_row_attn_kernel(const float* __restr
                                                             const float* __restrict__ mix1b,
                                                             const float* __restrict__ mix2w,
                                                             const float* __restrict__ mix2b, T* __restrict__ out) {
+    constexpr int VS = 20;                // V row stride (floats): float4-aligned, spreads the LDS banks
     extern __shared__ float sh[];
-    float* V = sh;                        // [n2max][16]
-    float* Pm = sh + n2max * 16;          // [16 rows][n2max]
+    float* V = sh;                        // [n2max][VS]
+    float* Pm = sh + n2max * VS;          // [16 rows][n2max]
     const int b = blockIdx.x, i0 = blockIdx.y * 16, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int n2b = n2[b];
     const float* Cb = cost + (long)b * c_sb;
     for (int h = 0; h < 16; ++h) {
         __syncthreads();
-        for (int k = tid; k < n2max * 16; k += 256) {
-            int j = k >> 4, dd = k & 15;
-            V[k] = j < n2b ? Wv[(long)(h * 16 + dd) * emb + j] : 0.f;
+        for (int k = tid; k < n2max * 16; k += 256) {      // coalesced along j
+            const int dd = k / n2max, j = k - dd * n2max;
+            V[j * VS + dd] = j < n2b ? Wv[(long)(h * 16 + dd) * emb + j] : 0.f;
         }
         float w1[16], b1[16], w2[16];
 #pragma unroll
@@ -66,13 +67,31 @@ __global__ __launch_bounds__(256) void afau_row_attn_kernel(const float* __restr
             for (int j = lane; j < n2max; j += 64) Pm[lr * n2max + j] *= inv;
         }
         __syncthreads();
-        // out[i][h*16 + d] for the 16 rows: thread = (row, d)
+        // out[i][h*16 + d] for the 16 rows: thread = (row, 4 d's, j residue mod 4), float4 V reads
         {
-            const int lr = tid >> 4, dd = tid & 15, i = i0 + lr;
-            if (i < n1max) {
-                float acc = 0.f;
-                for (int j = 0; j < n2max; ++j) acc += Pm[lr * n2max + j] * V[j * 16 + dd];
-                out[((long)b * n1max + i) * 256 + h * 16 + dd] = fpm::from_f<T>(acc);
+            const int lr = tid >> 4, dq = (tid >> 2) & 3, jp = tid & 3, i = i0 + lr;
+            float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int j = jp; j < n2max; j += 4) {
+                const float pj = Pm[lr * n2max + j];
+                const float4 v = *(const float4*)(V + j * VS + dq * 4);
+                acc.x = fmaf(pj, v.x, acc.x);
+                acc.y = fmaf(pj, v.y, acc.y);
+                acc.z = fmaf(pj, v.z, acc.z);
+                acc.w = fmaf(pj, v.w, acc.w);
+            }
+#pragma unroll
+            for (int o = 1; o <= 2; o <<= 1) {
+                acc.x += __shfl_xor(acc.x, o);
+                acc.y += __shfl_xor(acc.y, o);
+                acc.z += __shfl_xor(acc.z, o);
+                acc.w += __shfl_xor(acc.w, o);
+            }
+            if (i < n1max && jp == 0) {
+                T* o = out + ((long)b * n1max + i) * 256 + h * 16 + dq * 4;
+                o[0] = fpm::from_f<T>(acc.x);
+                o[1] = fpm::from_f<T>(acc.y);
+                o[2] = fpm::from_f<T>(acc.z);
+                o[3] = fpm::from_f<T>(acc.w);
             }
         }
     }
@@ -171,7 +190,7 @@ extern "C" int fpm_crossset_attn_fwd(int dtype, const float* cost, long c_sb, lo
     FPM_CHECK_ARG(n2max <= emb, "crossset_attn: n2max > embedding dim");
     if (B == 0) return 0;
     dim3 grid(B, (n1max + 15) / 16);
-    size_t sh = (size_t)(n2max * 16 + 16 * n2max) * 4;
+    size_t sh = (size_t)(n2max * 20 + 16 * n2max) * 4;
     hipStream_t st = (hipStream_t)stream;
     if (dtype == 0)
         hipLaunchKernelGGL((afau_row_attn_kernel<float>), grid, dim3(256), sh, st, cost, c_sb, c_ld, n1max, n2max, n2,
