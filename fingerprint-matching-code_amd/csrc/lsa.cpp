@@ -311,18 +311,122 @@ __attribute__((target("avx2"))) int lsap_solve_dense(int nr, int nc, const doubl
     return 0;
 }
 
-bool use_avx2() {
-#if defined(__x86_64__)
-    static int ok = -1;
-    if (ok < 0) {
-        const char* e = getenv("FPM_LSA_SCALAR");
-        ok = (e && e[0] == '1') ? 0 : (__builtin_cpu_supports("avx2") ? 1 : 0);
+// Same solver with 8-wide AVX-512 vectors and mask registers (Zen 4/5, Sapphire Rapids hosts).
+__attribute__((target("avx512f,avx512dq"))) int lsap_solve_dense512(int nr, int nc, const double* cost,
+                                                                   std::vector<int>& col4row) {
+    const int ncp = (nc + 7) & ~7;
+    std::vector<double> u(nr, 0.0), v(ncp, 0.0), spc(ncp);
+    std::vector<long long> rem(ncp);
+    std::vector<long long> path(ncp, -1);
+    std::vector<int> row4col(nc, -1), remaining(nc), pos(nc);
+    std::vector<char> SR(nr), SC(nc);
+    std::vector<int> ties;
+    std::vector<double> crow_pad;
+    const bool pad = ncp != nc;
+    if (pad) crow_pad.assign(ncp, 0.0);
+    col4row.assign(nr, -1);
+    const __m512d vinf = _mm512_set1_pd(INFINITY);
+    const __m512i zero = _mm512_setzero_si512();
+    for (int cur = 0; cur < nr; ++cur) {
+        double minVal = 0.0;
+        int i = cur;
+        int num = nc;
+        for (int it = 0; it < nc; ++it) {
+            remaining[it] = nc - it - 1;
+            pos[nc - it - 1] = it;
+        }
+        for (int j = 0; j < ncp; ++j) {
+            rem[j] = j < nc ? -1LL : 0LL;
+            spc[j] = INFINITY;
+        }
+        std::fill(SR.begin(), SR.end(), 0);
+        std::fill(SC.begin(), SC.end(), 0);
+        int sink = -1;
+        while (sink == -1) {
+            SR[i] = 1;
+            const double* crow = cost + (long)i * nc;
+            if (pad) {
+                std::copy(crow, crow + nc, crow_pad.begin());
+                crow = crow_pad.data();
+            }
+            const __m512d vmv = _mm512_set1_pd(minVal), vui = _mm512_set1_pd(u[i]);
+            const __m512i vi = _mm512_set1_epi64(i);
+            __m512d vlow = vinf;
+            for (int j = 0; j < ncp; j += 8) {
+                const __mmask8 m = _mm512_cmpneq_epi64_mask(_mm512_loadu_si512(&rem[j]), zero);
+                const __m512d r = _mm512_sub_pd(_mm512_sub_pd(_mm512_add_pd(vmv, _mm512_loadu_pd(crow + j)), vui),
+                                                _mm512_loadu_pd(&v[j]));
+                __m512d sv = _mm512_loadu_pd(&spc[j]);
+                const __mmask8 lt = _mm512_mask_cmp_pd_mask(m, r, sv, _CMP_LT_OQ);
+                sv = _mm512_mask_blend_pd(lt, sv, r);
+                _mm512_storeu_pd(&spc[j], sv);
+                _mm512_mask_storeu_epi64(&path[j], lt, vi);
+                vlow = _mm512_mask_min_pd(vlow, m, vlow, sv);
+            }
+            const double lowest = _mm512_reduce_min_pd(vlow);
+            if (lowest == INFINITY) return -1;
+            ties.clear();
+            const __m512d vl = _mm512_set1_pd(lowest);
+            for (int j = 0; j < ncp; j += 8) {
+                const __mmask8 m = _mm512_cmpneq_epi64_mask(_mm512_loadu_si512(&rem[j]), zero);
+                unsigned mk = _mm512_mask_cmp_pd_mask(m, _mm512_loadu_pd(&spc[j]), vl, _CMP_EQ_OQ);
+                while (mk) {
+                    const int q = __builtin_ctz(mk);
+                    ties.push_back(j + q);
+                    mk &= mk - 1;
+                }
+            }
+            int j = ties[0];
+            if (ties.size() > 1) {
+                int first = -1, lastu = -1, fpos = nc, upos = -1;
+                for (int t : ties) {
+                    if (pos[t] < fpos) { fpos = pos[t]; first = t; }
+                    if (row4col[t] == -1 && pos[t] > upos) { upos = pos[t]; lastu = t; }
+                }
+                j = lastu >= 0 ? lastu : first;
+            }
+            minVal = lowest;
+            rem[j] = 0;
+            const int p = pos[j], last = remaining[--num];
+            remaining[p] = last;
+            pos[last] = p;
+            if (row4col[j] == -1) sink = j;
+            else i = row4col[j];
+            SC[j] = 1;
+        }
+        u[cur] += minVal;
+        for (int r = 0; r < nr; ++r)
+            if (SR[r] && r != cur) u[r] += minVal - spc[col4row[r]];
+        for (int c = 0; c < nc; ++c)
+            if (SC[c]) v[c] -= minVal - spc[c];
+        int j = sink;
+        while (true) {
+            const int r = (int)path[j];
+            row4col[j] = r;
+            std::swap(col4row[r], j);
+            if (r == cur) break;
+        }
     }
-    return ok == 1;
+    return 0;
+}
+
+// 0 scalar, 1 AVX2, 2 AVX-512 (FPM_LSA_SCALAR=1 / FPM_LSA_AVX2=1 force the narrower paths)
+int lsa_isa() {
+#if defined(__x86_64__)
+    static int isa = -1;
+    if (isa < 0) {
+        const char* e = getenv("FPM_LSA_SCALAR");
+        const char* a = getenv("FPM_LSA_AVX2");
+        if (e && e[0] == '1') isa = 0;
+        else if (__builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512dq") && !(a && a[0] == '1')) isa = 2;
+        else isa = __builtin_cpu_supports("avx2") ? 1 : 0;
+    }
+    return isa;
 #else
-    return false;
+    return 0;
 #endif
 }
+
 
 // one pair: s (ld stride) block [n1 x n2], maximise s  ->  assign[r] = col or -1
 int lsa_pair(const float* s, long ld, int n1, int n2, int* assign, int n1max) {
@@ -342,7 +446,10 @@ int lsa_pair(const float* s, long ld, int n1, int n2, int* assign, int n1max) {
         if (cost[k] != cost[k] || cost[k] == -INFINITY) return -2;   // invalid (scipy raises)
     std::vector<int> c4r;
 #if defined(__x86_64__)
-    int rc = use_avx2() ? lsap_solve_dense(nr, nc, cost.data(), c4r) : lsap_solve(nr, nc, cost.data(), c4r);
+    const int isa = lsa_isa();
+    int rc = isa == 2   ? lsap_solve_dense512(nr, nc, cost.data(), c4r)
+             : isa == 1 ? lsap_solve_dense(nr, nc, cost.data(), c4r)
+                        : lsap_solve(nr, nc, cost.data(), c4r);
 #else
     int rc = lsap_solve(nr, nc, cost.data(), c4r);
 #endif
