@@ -191,7 +191,14 @@ extern "C" int fpm_crossset_attn_fwd(int dtype, const float* cost, long c_sb, lo
     if (B == 0) return 0;
     dim3 grid(B, (n1max + 15) / 16);
     size_t sh = (size_t)(n2max * 20 + 16 * n2max) * 4;
+    FPM_CHECK_ARG(sh <= 160 * 1024, "crossset_attn: n2max %d needs %zu B of LDS", n2max, sh);
     hipStream_t st = (hipStream_t)stream;
+    if (sh > 64 * 1024) {   // n2max > 455: opt in to the larger LDS allocation of gfx950
+        (void)hipFuncSetAttribute((const void*)afau_row_attn_kernel<float>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
+        (void)hipFuncSetAttribute((const void*)afau_row_attn_kernel<bf16_t>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
+    }
     if (dtype == 0)
         hipLaunchKernelGGL((afau_row_attn_kernel<float>), grid, dim3(256), sh, st, cost, c_sb, c_ld, n1max, n2max, n2,
                            Wv, emb, mix1w, mix1b, mix2w, mix2b, (float*)out);

@@ -206,6 +206,118 @@ __global__ __launch_bounds__(1024) void sinkhorn_reg_kernel(SinkArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Large blocks (max(n1max, n2max) > 256, e.g. n = 512): the block no longer fits the register file,
+// so every half-iteration streams the pair's block from L2 / HBM (1 MB at n = 512) while the
+// potentials stay in LDS.  Same algorithm and semantics as sinkhorn_reg_kernel; the per-thread
+// logsumexps are single-pass (online max rescaling).
+// Physical axes: "a" = the strided axis, "c" = the unit-stride axis of the input.
+constexpr int SK_MAXN = 2048;
+
+__device__ __forceinline__ void lse_push(float& m, float& s, float x) {
+    if (x > m) {
+        s = s * fpm::fast_exp2(m - x) + 1.f;
+        m = x;
+    } else {
+        s += fpm::fast_exp2(x - m);
+    }
+}
+
+__global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
+    __shared__ float potA[SK_MAXN], potC[SK_MAXN];
+    __shared__ float red_m[1024], red_s[1024];
+    __shared__ float ud_sh;
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int n1b = a.n1[b], n2b = a.n2[b];
+    const bool transposed = n1b > n2b;
+    const int R = transposed ? n2b : n1b, C = transposed ? n1b : n2b;
+    const int nd = (a.dummy_row && C > R) ? (C - R) : 0;
+    const float DUMMY = -100.f * fpm::LOG2E_F;
+    const float scale = fpm::LOG2E_F / a.tau;
+    const int limA = a.contig_j ? n1b : n2b, limC = a.contig_j ? n2b : n1b;
+    const int boxA = a.contig_j ? a.n1max : a.n2max, boxC = a.contig_j ? a.n2max : a.n1max;
+    const bool u_on_A = (a.contig_j != 0) == (!transposed);
+    const float* in = a.in + (long)b * a.in_sb;
+    const long sA = a.contig_j ? a.in_si : a.in_sj, sC = a.contig_j ? a.in_sj : a.in_si;
+    auto val = [&](int ia, int ic) { return (in[ia * sA + ic * sC] / a.tau) * fpm::LOG2E_F; };
+    (void)scale;
+    for (int k = tid; k < SK_MAXN; k += 1024) { potA[k] = 0.f; potC[k] = 0.f; }
+    if (tid == 0) ud_sh = 0.f;
+    __syncthreads();
+
+    // potA[ia] = lse_c(val - potC[c]) (+ nd * exp(DUMMY - ud)): one wave per ia, lanes along c
+    auto along_c = [&](bool add_dummy) {
+        const float ud = ud_sh;
+        for (int ia = wv; ia < limA; ia += 16) {
+            float m = -INFINITY, s = 0.f;
+            for (int ic = lane; ic < limC; ic += 64) lse_push(m, s, val(ia, ic) - potC[ic]);
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                float mo = __shfl_xor(m, o), so = __shfl_xor(s, o);
+                lse_combine(m, s, mo, so);
+            }
+            if (add_dummy) lse_combine(m, s, DUMMY - ud, (float)nd);
+            if (lane == 0) potA[ia] = (m == -INFINITY) ? 0.f : m + fpm::fast_log2(s);
+        }
+        __syncthreads();
+    };
+    // potC[ic] = lse_a(val - potA[a]) (+ dummy): thread groups along a, threads along c (coalesced)
+    auto along_a = [&](bool add_dummy) {
+        const float ud = ud_sh;
+        const int cpad = (limC + 63) / 64 * 64;
+        const int groups = cpad >= 1024 ? 1 : 1024 / cpad;
+        for (int c0 = 0; c0 < limC; c0 += 1024) {
+            const int ic = c0 + (groups == 1 ? tid : tid % cpad), grp = groups == 1 ? 0 : tid / cpad;
+            float m = -INFINITY, s = 0.f;
+            if (ic < limC && grp < groups)
+                for (int ia = grp; ia < limA; ia += groups) lse_push(m, s, val(ia, ic) - potA[ia]);
+            red_m[tid] = m;
+            red_s[tid] = s;
+            __syncthreads();
+            if (grp == 0 && ic < limC) {
+                for (int g = 1; g < groups; ++g) lse_combine(m, s, red_m[tid + g * cpad], red_s[tid + g * cpad]);
+                if (add_dummy) lse_combine(m, s, DUMMY - ud, (float)nd);
+                potC[ic] = (m == -INFINITY) ? 0.f : m + fpm::fast_log2(s);
+            }
+            __syncthreads();
+        }
+    };
+    // ud = lse over the valid algorithmic columns of (DUMMY - v)
+    auto update_dummy = [&]() {
+        const float* v = u_on_A ? potC : potA;
+        const int lim = u_on_A ? limC : limA;
+        float m = -INFINITY, s = 0.f;
+        for (int k = tid; k < lim; k += 1024) lse_push(m, s, DUMMY - v[k]);
+        red_m[tid] = m;
+        red_s[tid] = s;
+        __syncthreads();
+        if (tid == 0) {
+            float mm = red_m[0], ss = red_s[0];
+            for (int k = 1; k < 1024; ++k) lse_combine(mm, ss, red_m[k], red_s[k]);
+            ud_sh = mm + fpm::fast_log2(ss);
+        }
+        __syncthreads();
+    };
+
+    for (int it = 0; it < a.iters; ++it) {
+        if ((it & 1) == 0) {           // row normalisation: update u
+            if (u_on_A) along_c(false); else along_a(false);
+            if (nd > 0) update_dummy();
+        } else {                       // column normalisation: update v
+            if (u_on_A) along_a(nd > 0); else along_c(nd > 0);
+        }
+    }
+
+    float* out = a.out + (long)b * a.out_sb;
+    const long oA = a.contig_j ? a.out_si : a.out_sj, oC = a.contig_j ? a.out_sj : a.out_si;
+    for (int ia = wv; ia < boxA; ia += 16)
+        for (int ic = lane; ic < boxC; ic += 64) {
+            float v = 0.f;
+            if (ia < limA && ic < limC) v = fpm::fast_exp2(val(ia, ic) - potA[ia] - potC[ic]);
+            out[ia * oA + ic * oC] = v;
+        }
+}
+
 }  // namespace
 
 extern "C" int fpm_sinkhorn_log_fwd(const float* s, long s_sb, long s_si, long s_sj, float* out,
@@ -213,8 +325,8 @@ extern "C" int fpm_sinkhorn_log_fwd(const float* s, long s_sb, long s_si, long s
                                     int B, int n1max, int n2max, int iters, float tau, int dummy_row,
                                     void* stream) {
     FPM_CHECK_ARG(B >= 0 && n1max > 0 && n2max > 0, "sinkhorn: bad sizes");
-    FPM_CHECK_ARG(n1max <= 256 && n2max <= 256, "sinkhorn: n1max/n2max > 256 not supported yet (%d,%d)",
-                  n1max, n2max);
+    FPM_CHECK_ARG(n1max <= SK_MAXN && n2max <= SK_MAXN, "sinkhorn: n1max/n2max > %d not supported (%d,%d)",
+                  SK_MAXN, n1max, n2max);
     if (B == 0) return 0;
     SinkArgs a;
     a.in = s; a.in_sb = s_sb; a.in_si = s_si; a.in_sj = s_sj;
@@ -222,6 +334,7 @@ extern "C" int fpm_sinkhorn_log_fwd(const float* s, long s_sb, long s_si, long s
     a.n1 = n1; a.n2 = n2; a.n1max = n1max; a.n2max = n2max;
     a.iters = iters; a.tau = tau; a.dummy_row = dummy_row;
     a.contig_j = (s_sj == 1) ? 1 : 0;
+    FPM_CHECK_ARG(s_sj == 1 || s_si == 1, "sinkhorn: one of the input's row/column strides must be 1");
     int nmax = n1max > n2max ? n1max : n2max;
     hipStream_t st = (hipStream_t)stream;
     if (nmax <= 32)
@@ -230,7 +343,9 @@ extern "C" int fpm_sinkhorn_log_fwd(const float* s, long s_sb, long s_si, long s
         hipLaunchKernelGGL((sinkhorn_reg_kernel<2, 2>), dim3(B), dim3(1024), 0, st, a);
     else if (nmax <= 128)
         hipLaunchKernelGGL((sinkhorn_reg_kernel<4, 4>), dim3(B), dim3(1024), 0, st, a);
-    else
+    else if (nmax <= 256)
         hipLaunchKernelGGL((sinkhorn_reg_kernel<8, 8>), dim3(B), dim3(1024), 0, st, a);
+    else
+        hipLaunchKernelGGL(sinkhorn_stream_kernel, dim3(B), dim3(1024), 0, st, a);
     return fpm::check_launch("fpm_sinkhorn_log_fwd");
 }

@@ -21,7 +21,9 @@ __device__ __forceinline__ float urow(float a0, float a1) {
     return m + fpm::fast_log2(fpm::fast_exp2(a0 - m) + fpm::fast_exp2(a1 - m));
 }
 
-template <int NQ>
+// STREAM: blocks beyond 64 values per thread (n1*n2 > 65536, e.g. n = 512) re-read ss from
+// L2 / HBM on every pass instead of holding it on chip.
+template <int NQ, bool STREAM>
 __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict__ ss, long sb, long ld,
                                                          const int* __restrict__ n1, const int* __restrict__ n2,
                                                          const float* __restrict__ kvec, float* __restrict__ out,
@@ -35,24 +37,34 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
     const float* S = ss + (long)b * sb;
 
     // values k < NQR stay in VGPRs, the rest in LDS (keeps the 1024-thread block under 128 VGPRs)
-    constexpr int NQR = NQ < 32 ? NQ : 32;
-    constexpr int NQL = NQ - NQR;
+    constexpr int NQR = STREAM ? 1 : (NQ < 32 ? NQ : 32);
+    constexpr int NQL = STREAM ? 0 : NQ - NQR;
     __shared__ float sl[NQL > 0 ? NQL * 1024 : 1];
     float sr[NQR];
 #define SVAL(k) ((k) < NQR ? sr[(k) < NQR ? (k) : 0] : sl[((k) >= NQR ? (k) - NQR : 0) * 1024 + tid])
     float mn = INFINITY, mx = -INFINITY;
-#pragma unroll
-    for (int k = 0; k < NQ; ++k) {
-        int q = tid + 1024 * k;
-        float v = 0.f;
-        if (q < N) {
-            int i = q / n2b, j = q - i * n2b;
-            v = S[i * ld + j];
+    if (STREAM) {
+        sr[0] = 0.f;
+        for (int q = tid; q < N; q += 1024) {
+            const int i = q / n2b, j = q - i * n2b;
+            const float v = S[i * ld + j];
             mn = fminf(mn, v);
             mx = fmaxf(mx, v);
         }
-        if (k < NQR) sr[k < NQR ? k : 0] = v;
-        else sl[(k >= NQR ? k - NQR : 0) * 1024 + tid] = v;
+    } else {
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) {
+            int q = tid + 1024 * k;
+            float v = 0.f;
+            if (q < N) {
+                int i = q / n2b, j = q - i * n2b;
+                v = S[i * ld + j];
+                mn = fminf(mn, v);
+                mx = fmaxf(mx, v);
+            }
+            if (k < NQR) sr[k < NQR ? k : 0] = v;
+            else sl[(k >= NQR ? k - NQR : 0) * 1024 + tid] = v;
+        }
     }
     mn = -fpm::warp_max(-mn);
     mx = fpm::warp_max(mx);
@@ -68,6 +80,13 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
     // visit every q of this thread: register-resident values (unrolled), then LDS-resident ones
     // (runtime loop: bounded code size and register pressure)
     auto forq = [&](auto&& f) {
+        if (STREAM) {
+            for (int k = 0; tid + 1024 * k < N; ++k) {
+                const int q = tid + 1024 * k, i = q / n2b, j = q - i * n2b;
+                f(k, S[i * ld + j]);
+            }
+            return;
+        }
 #pragma unroll
         for (int k = 0; k < NQR; ++k)
             if (tid + 1024 * k < N) f(k, sr[k]);
@@ -289,15 +308,16 @@ extern "C" int fpm_soft_topk_fwd(const float* ss, long s_sb, long s_ld, const in
                                  float* out, long o_sb, long o_ld, int* steps_out, void* stream) {
     FPM_CHECK_ARG(B >= 0 && n1max > 0 && n2max > 0, "soft_topk: bad sizes");
     long nn = (long)n1max * n2max;
-    FPM_CHECK_ARG(nn <= 65536, "soft_topk: n1max*n2max=%ld > 65536 not supported yet", nn);
+    FPM_CHECK_ARG(nn <= (1L << 24), "soft_topk: n1max*n2max=%ld too large", nn);
     if (B == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
-#define LAUNCH(NQ) hipLaunchKernelGGL((soft_topk_kernel<NQ>), dim3(B), dim3(1024), 0, st, ss, s_sb, s_ld, n1, n2, \
-                                       k, out, o_sb, o_ld, n1max, n2max, iters, tau, steps_out)
-    if (nn <= 1024) LAUNCH(1);
-    else if (nn <= 4096) LAUNCH(4);
-    else if (nn <= 16384) LAUNCH(16);
-    else LAUNCH(64);
+#define LAUNCH(NQ, ST) hipLaunchKernelGGL((soft_topk_kernel<NQ, ST>), dim3(B), dim3(1024), 0, st, ss, s_sb, s_ld, \
+                                           n1, n2, k, out, o_sb, o_ld, n1max, n2max, iters, tau, steps_out)
+    if (nn <= 1024) LAUNCH(1, false);
+    else if (nn <= 4096) LAUNCH(4, false);
+    else if (nn <= 16384) LAUNCH(16, false);
+    else if (nn <= 65536) LAUNCH(64, false);
+    else LAUNCH(1, true);
 #undef LAUNCH
     return fpm::check_launch("fpm_soft_topk_fwd");
 }

@@ -287,3 +287,37 @@ def test_gemm_big_vs_torch(M, N, K, batch, epi, f32out, gather):
         ref = torch.relu(ref)
     tol = 2e-3 if f32out else 1e-2
     assert ((out.float().cpu() - ref).abs().max() / ref.abs().max()) < tol
+
+
+# ---------------------------------------------------------------------------------------- large n (C5)
+def test_sinkhorn_stream_vs_oracle():
+    """n > 256: the L2-streaming Sinkhorn (dummy rows, transposed pair, strided views)."""
+    g = torch.Generator().manual_seed(21)
+    n1s, n2s = (512, 300, 512), (512, 512, 400)
+    B, n1max, n2max = 3, 512, 512
+    s = torch.randn(B, n1max, n2max, generator=g) * 0.3
+    ref = O.pygm_sinkhorn(s.double(), n1s, n2s, dummy_row=True, max_iter=10, tau=0.01)
+    out = ops.sinkhorn(s.to(DEV), _i32(n1s), _i32(n2s), 10, 0.01, True).cpu()
+    assert (out.double() - ref).abs().max() < 1e-4
+    sT = s.transpose(1, 2).contiguous().to(DEV).transpose(1, 2)
+    o2 = torch.zeros(B, n2max, n1max, device=DEV).transpose(1, 2)
+    ops.sinkhorn(sT, _i32(n1s), _i32(n2s), 10, 0.01, True, out=o2)
+    assert (o2.cpu().double() - ref).abs().max() < 1e-4
+
+
+def test_soft_topk_stream_vs_oracle():
+    g = torch.Generator().manual_seed(22)
+    B, n = 2, 512
+    ss = torch.rand(B, n, n, generator=g) ** 6
+    k = torch.tensor([100.5, 400.0])
+    ref = O.soft_topk(ss, k, [n] * B, [n] * B, 10, 0.01)
+    out = ops.soft_topk(ss.to(DEV), _i32([n] * B), _i32([n] * B), k.to(DEV), 10, 0.01).cpu()
+    assert (out - ref).abs().max() < 1e-4
+
+
+@pytest.mark.slow
+def test_forward_n512_parity(sd):
+    """C5 graph size (n = 512) end to end at a batch the CPU oracle finishes in tens of seconds."""
+    d = _compare_forward(synth.make_batch(31, 1, 512), sd)
+    assert d["ss"] < 1e-4 and d["ds_mat"] < 1e-4 and d["k_prob"] < 1e-4, d
+    assert d["perm_equal"], d
