@@ -31,6 +31,21 @@ def _under_profiler():
     return "rocprof" in os.environ.get("LD_PRELOAD", "") or any(k.startswith("ROCPROF") for k in os.environ)
 
 
+def _gen_gallery(args):
+    seed, g, n = args
+    from fpm import synth
+    return synth.make_graph(seed, g, 1, n)
+
+
+def make_gallery(seed, first, G, n, workers):
+    ids = [(seed, first + g, n) for g in range(G)]
+    if workers <= 1 or G < 8 or _under_profiler():
+        return [_gen_gallery(a) for a in ids]
+    import multiprocessing as mp
+    with mp.get_context("fork").Pool(workers) as pool:
+        return pool.map(_gen_gallery, ids, chunksize=max(1, G // (workers * 4)))
+
+
 def make_pairs(seed, first, B, n, workers):
     ids = [(seed, first + b, n) for b in range(B)]
     if workers <= 1 or B < 8 or _under_profiler():
@@ -76,7 +91,18 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--lsa-threads", type=int, default=0)
     ap.add_argument("--gen-workers", type=int, default=16)
+    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4", "c5"],
+                    help="SURVEY §8 configs: c3 = the headline (n=256, 1024 pairs/GPU, bf16); c2 = n=128, "
+                         "256 pairs/GPU, fp32; c4 = 1 probe x --gallery graphs (n=128) sharded over ranks, probe "
+                         "stage shared; c5 = n=512, 1024 pairs/GPU")
+    ap.add_argument("--gallery", type=int, default=10000, help="c4: gallery size over all ranks")
     args = ap.parse_args()
+    if args.config == "c2":
+        args.n, args.batch, args.dtype = 128, 256, "f32"
+    elif args.config == "c5":
+        args.n = 512
+    elif args.config == "c4":
+        args.n = 128
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -86,7 +112,17 @@ def main():
 
     # inputs first (forked workers must not inherit a GPU context)
     t_gen = time.perf_counter()
-    pairs = make_pairs(args.seed, rank * args.batch, args.batch, args.n, args.gen_workers)
+    if args.config == "c4":
+        # contiguous gallery shard per rank; the probe is replicated
+        share = (args.gallery + world - 1) // world
+        g0 = rank * share
+        args.batch = max(0, min(share, args.gallery - g0))
+        from fpm import synth
+        probe = synth.make_graph(args.seed, 0, 0, args.n)
+        gallery = make_gallery(args.seed, 1 + g0, args.batch, args.n, args.gen_workers)
+        pairs = None
+    else:
+        pairs = make_pairs(args.seed, rank * args.batch, args.batch, args.n, args.gen_workers)
     t_gen = time.perf_counter() - t_gen
     log("generated %d pairs in %.1fs" % (args.batch, t_gen))
 
@@ -103,9 +139,13 @@ def main():
     sd = params.init_params(args.seed)
     net = fpm.Net(regression=True, dtype=args.dtype, lsa_threads=args.lsa_threads or None)
     net.load_state_dict(sd)
-    bt = DeviceBatch.from_pairs(pairs, dev)
+    if args.config == "c4":
+        bt = DeviceBatch.from_probe_gallery(probe, gallery, dev)
+        del gallery
+    else:
+        bt = DeviceBatch.from_pairs(pairs, dev)
+        del pairs
     E_tot = bt.E[0] + bt.E[1]
-    del pairs
 
     def barrier():
         if world > 1:
@@ -155,7 +195,7 @@ def main():
         t = torch.tensor([elapsed, gpu_s, lsa_s], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, gpu_s, lsa_s = t.tolist()
-    pairs_total = args.batch * world * args.steps
+    pairs_total = (args.gallery if args.config == "c4" else args.batch * world) * args.steps
     value = pairs_total / elapsed
     peak = 2500.0 if args.dtype == "bf16" else 157.3
     achieved = (fl.value / (ms.value / 1e3)) / 1e12 if ms.value > 0 else 0.0
@@ -175,14 +215,20 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.config == "c4" else "weak",
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic (seeded Delaunay keypoint graphs, random node/global features, random-init weights)",
-            "config": {"workload": "batch=%d pairs/GPU, n=%d keypoints, Delaunay edges, factorized Kronecker "
-                                   "affinity, %s MFMA; full Net.forward incl. AFA-U, soft top-k, host Hungarian, "
-                                   "greedy top-k, MatchClassifier" % (args.batch, args.n, args.dtype),
-                       "global_batch": args.batch * world, "n_keypoints": args.n,
+            "config": {"workload": ("1 probe x %d gallery graphs (%d per GPU), n=%d keypoints, probe SplineConv "
+                                    "once per pipeline chunk (accounting: shared probe stage), %s MFMA; full "
+                                    "Net.forward per pair" % (args.gallery, args.batch, args.n, args.dtype))
+                       if args.config == "c4" else
+                       ("batch=%d pairs/GPU, n=%d keypoints, Delaunay edges, factorized Kronecker "
+                        "affinity, %s MFMA; full Net.forward incl. AFA-U, soft top-k, host Hungarian, "
+                        "greedy top-k, MatchClassifier" % (args.batch, args.n, args.dtype)),
+                       "survey_config": args.config,
+                       "global_batch": args.gallery if args.config == "c4" else args.batch * world,
+                       "n_keypoints": args.n,
                        "edges_per_graph": E_tot / (2.0 * args.batch), "parallelism": "pair-sharded x%d" % world},
             "gpu_stage_pairs_per_s": args.batch * world * args.steps / gpu_s,
             "host_lsa_ms_per_step": lsa_s / args.steps * 1e3,

@@ -16,8 +16,11 @@ from . import config as C
 
 
 class DeviceBatch:
-    def __init__(self, B, n1, n2, x, w, src, dst, pseudo, device, nmax=None, edge_off=None):
+    def __init__(self, B, n1, n2, x, w, src, dst, pseudo, device, nmax=None, edge_off=None, shared0=False):
         self.B = B
+        # probe x gallery (C4): every pair's side-0 graph is the same probe; its per-graph stage
+        # (SplineConv) is computed once per (sub-)batch and broadcast
+        self.shared0 = shared0
         self.device = device
         self.n_host = [torch.as_tensor(n1, dtype=torch.int32), torch.as_tensor(n2, dtype=torch.int32)]
         self.n = [t.to(device) for t in self.n_host]
@@ -61,7 +64,7 @@ class DeviceBatch:
                 ps.append(self.pseudo[side][e0:e1])
             eo = [self.edge_off[side][b0:b1 + 1] - self.edge_off[side][b0] for side in range(2)]
             sub = DeviceBatch(b1 - b0, self.n_host[0][b0:b1], self.n_host[1][b0:b1], xs, ws, ss, ds, ps, self.device,
-                              nmax=self.nmax, edge_off=eo)
+                              nmax=self.nmax, edge_off=eo, shared0=self.shared0)
             sub.pair_range = (b0, b1)
             parts.append(sub)
         self._splits[key] = parts
@@ -110,6 +113,14 @@ class DeviceBatch:
             dsts.append(torch.from_numpy(np.concatenate(d_l).astype(np.int32)).to(device))
             pss.append(torch.from_numpy(np.concatenate(p_l).astype(np.float32)).to(device).contiguous())
         return DeviceBatch(B, ns[0], ns[1], xs, ws, srcs, dsts, pss, device, edge_off=eoffs)
+
+    @staticmethod
+    def from_probe_gallery(probe, gallery, device):
+        """One probe graph against a gallery (C4): pairs (probe, g) with the probe's
+        per-graph stage shared.  Inputs are staged per pair (simple layout); compute is not."""
+        bt = DeviceBatch.from_pairs([(probe, g) for g in gallery], device)
+        bt.shared0 = True
+        return bt
 
     @staticmethod
     def from_data_dict(data_dict, device):

@@ -547,6 +547,38 @@ extern "C" int fpm_edge_diff(const float* x, const int* src, const int* dst, lon
     return fpm::check_launch("fpm_edge_diff");
 }
 
+// Probe x gallery batches (C4): the shared side-0 graph's SplineConv output y (rows x 768, fp32) is
+// computed once and broadcast to the B pairs, scaled per pair like the combine epilogue does
+// (out_t[b] = T(y o c[b]), the X1 o c operand of the vertex affinity, affinity_layer.py:15), so
+// results equal the per-pair path bit for bit.
+namespace {
+template <typename T>
+__global__ void rows_bcast_scale_kernel(const float* __restrict__ y, long rows, int B, const float* __restrict__ coef,
+                                        float* __restrict__ out_f, T* __restrict__ out_t) {
+    const long n = rows * 768;
+    const int b = blockIdx.y;
+    for (long k = (long)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (long)gridDim.x * blockDim.x) {
+        const float v = y[k];
+        if (out_f) out_f[(long)b * n + k] = v;
+        if (out_t) out_t[(long)b * n + k] = fpm::from_f<T>(coef ? v * coef[(long)b * 768 + (k % 768)] : v);
+    }
+}
+}  // namespace
+
+extern "C" int fpm_rows_bcast_scale(int dtype, const float* y, long rows, int B, const float* coef, float* out_f,
+                                    void* out_t, void* stream) {
+    FPM_CHECK_ARG(dtype == 0 || dtype == 1, "rows_bcast_scale: bad dtype");
+    if (B == 0 || rows == 0) return 0;
+    dim3 grid((unsigned)((rows * 768 + 255) / 256 < 1024 ? (rows * 768 + 255) / 256 : 1024), (unsigned)B);
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == 0)
+        hipLaunchKernelGGL(rows_bcast_scale_kernel<float>, grid, dim3(256), 0, st, y, rows, B, coef, out_f, (float*)out_t);
+    else
+        hipLaunchKernelGGL(rows_bcast_scale_kernel<bf16_t>, grid, dim3(256), 0, st, y, rows, B, coef, out_f,
+                           (bf16_t*)out_t);
+    return fpm::check_launch("fpm_rows_bcast_scale");
+}
+
 extern "C" int fpm_profile_enable(int on) {
     g_prof_on = on != 0;
     return 0;

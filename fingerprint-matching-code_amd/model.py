@@ -155,6 +155,8 @@ class Net(nn.Module):
         nn_ = bt.B * bt.nmax[side]
         E = bt.E[side]
         plan = ops.spline_plan(bt.src[side], bt.dst[side], bt.pseudo[side], nn_, bt.nmax[side])
+        if side == 0 and bt.shared0 and bt.B > 1:
+            return (plan,) + self._spline_shared(wp, bt, cscale)
         x0 = bt.x[side]
         x_op = ops.cast_bf16(x0) if op == torch.bfloat16 else x0
         yws = ops.spline_y_ws(ops.BF16 if op == torch.bfloat16 else ops.F32, E, nn_, dev)
@@ -165,6 +167,28 @@ class Net(nn.Module):
         ops.spline_conv(h, plan, E, nn_, bt.nmax[side], bt.n[side], wp["W1"], wp["bias1"], yws, 1, xres=x0,
                         cscale=cscale, out_f=outf, out_t=out)
         return plan, out, outf
+
+    def _spline_shared(self, wp, bt, cscale):
+        """Probe x gallery: the shared side-0 graph's two SplineConv layers once (pair 0's slice),
+        then broadcast to all pairs with the per-pair coefficient scaling (fpm_rows_bcast_scale)."""
+        dev = bt.device
+        op = torch.bfloat16 if self.dtype_mode == "bf16" else torch.float32
+        nm = bt.nmax[0]
+        e0 = int(bt.edge_off[0][1])
+        src, dst, ps = bt.src[0][:e0], bt.dst[0][:e0], bt.pseudo[0][:e0]
+        plan = ops.spline_plan(src, dst, ps, nm, nm)
+        x0 = bt.x[0][:nm]
+        nv = bt.n[0][:1]
+        x_op = ops.cast_bf16(x0) if op == torch.bfloat16 else x0
+        yws = ops.spline_y_ws(ops.BF16 if op == torch.bfloat16 else ops.F32, e0, nm, dev)
+        h = torch.empty(nm, C.NODE_FEATURE_DIM, device=dev, dtype=op)
+        ops.spline_conv(x_op, plan, e0, nm, nm, nv, wp["W0"], wp["bias0"], yws, 0, out_t=h)
+        y = torch.empty(nm, C.NODE_FEATURE_DIM, device=dev, dtype=torch.float32)
+        ops.spline_conv(h, plan, e0, nm, nm, nv, wp["W1"], wp["bias1"], yws, 1, xres=x0, out_f=y)
+        out = torch.empty(bt.B * nm, C.NODE_FEATURE_DIM, device=dev, dtype=op)
+        outf = torch.empty(bt.B * nm, C.NODE_FEATURE_DIM, device=dev, dtype=torch.float32) if self._keep_feats else None
+        ops.rows_bcast_scale(y, bt.B, coef=cscale, out_f=outf, out_t=out)
+        return out, outf
 
     def _afau(self, wp, ss, bt):
         """AFA-U k regression (ngm.py:386-412) -> ks (B,)."""

@@ -79,6 +79,11 @@ int fpm_spline_plan_csr(void* ws, long E, long num_nodes, int** dst_ptr, int** n
 int fpm_spline_conv_fwd(int dtype, const void* x_op, const void* plan_ws, long E, long num_nodes, int nmax,
                         const int* nvalid, const void* W, const float* bias, void* y_ws, long y_ws_bytes, int mode,
                         const float* xres, const float* cscale, float* out_f, void* out_t, void* stream);
+/* probe x gallery (C4): broadcast the shared source graph's SplineConv output y (rows x 768 fp32)
+ * to B pairs: out_f[b] = y, out_t[b] = dtype(y o coef[b]) (coef may be NULL) -- the same values the
+ * per-pair path's fused epilogue writes. */
+int fpm_rows_bcast_scale(int dtype, const float* y, long rows, int B, const float* coef, float* out_f, void* out_t,
+                         void* stream);
 /* vertex_attr_to_edge_attr (spline_conv.py:73-81): out[e] = x[src[e]] - x[dst[e]] */
 int fpm_edge_diff(const float* x, const int* src, const int* dst, long E, int D, float* out, void* stream);
 /* same, written into a padded per-pair layout and scaled: out[row[e]] = (x[src]-x[dst]) o c[pair[e]]

@@ -32,9 +32,11 @@ def test_header_symbols_exported():
 
 def test_error_channel():
     lib = _lib.load()
-    with pytest.raises(_lib.FpmError, match="n1max/n2max > 256"):
-        _lib.call("fpm_sinkhorn_log_fwd", None, 0, 0, 0, None, 0, 0, 0, None, None, 1, 300, 300, 10, 0.01, 1, None)
-    assert b"256" in lib.fpm_last_error()
+    with pytest.raises(_lib.FpmError, match="n1max/n2max > 2048"):
+        _lib.call("fpm_sinkhorn_log_fwd", None, 0, 0, 1, None, 0, 0, 1, None, None, 1, 3000, 300, 10, 0.01, 1, None)
+    assert b"2048" in lib.fpm_last_error()
+    with pytest.raises(_lib.FpmError, match="strides"):
+        _lib.call("fpm_sinkhorn_log_fwd", None, 0, 2, 2, None, 0, 0, 1, None, None, 1, 30, 30, 10, 0.01, 1, None)
 
 
 def test_cpu_tensor_rejected():

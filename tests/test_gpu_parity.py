@@ -321,3 +321,20 @@ def test_forward_n512_parity(sd):
     d = _compare_forward(synth.make_batch(31, 1, 512), sd)
     assert d["ss"] < 1e-4 and d["ds_mat"] < 1e-4 and d["k_prob"] < 1e-4, d
     assert d["perm_equal"], d
+
+
+# ---------------------------------------------------------------------------------------- probe x gallery (C4)
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_probe_gallery_shared_equals_per_pair(sd, dtype):
+    """Computing the shared probe's SplineConv once and broadcasting it gives the per-pair results
+    bit for bit (the per-graph stage does not depend on the partner)."""
+    probe = synth.make_graph(40, 0, 0, 48)
+    gallery = [synth.make_graph(40, p, 1, n) for p, n in enumerate([48, 40, 45, 48, 37, 48])]
+    net = fpm.Net(regression=True, dtype=dtype)
+    net.load_state_dict(sd)
+    shared = DeviceBatch.from_probe_gallery(probe, gallery, DEV)
+    plain = DeviceBatch.from_pairs([(probe, g) for g in gallery], DEV)
+    a = net.run(shared, chunks=2)
+    b = net.run(plain, chunks=2)
+    for k in ("s", "ss", "ds_mat", "perm_mat", "k_prob", "cls_prob"):
+        assert torch.equal(a[k], b[k]), k
