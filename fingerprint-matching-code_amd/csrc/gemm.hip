@@ -24,21 +24,25 @@ extern "C" int fpm_gemm(int dtype, const void* A, long lda, long sA, const int* 
     p.epi = epi; p.bias = bias; p.Cf = Cf; p.Ct = Ct; p.ldc = ldc; p.sC = sC; p.n1 = n1; p.n2 = n2;
     hipStream_t st = (hipStream_t)stream;
     // bf16 with a large M: the 256-row LDS-DMA tiles (gemm_big.h)
-    const bool big = dtype == 1 && M >= 2 * G2_BM && K % G2_BK == 0 && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
-                     !(Cf && Ct) && (Cf ? ldc % 4 == 0 : ldc % 8 == 0) && (epi == EPI_STORE || epi == EPI_RELU);
+    const int mt = (M + G2_BM - 1) / G2_BM;
+    const bool epi_ok = epi == EPI_STORE || epi == EPI_RELU || (epi == EPI_AFFINITY && Cf && !Ct);
+    const bool big = dtype == 1 && M >= G2_BM && K % G2_BK == 0 && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
+                     !(Cf && Ct) && (Cf ? ldc % 4 == 0 : ldc % 8 == 0) && epi_ok &&
+                     (long)mt * ((N + 127) / 128) * batch >= 128;
     if (big) {
-        const int mt = (M + G2_BM - 1) / G2_BM;
         const int BN = (N % 256 == 0 && (long)mt * (N / 256) * batch >= 512) ? 256 : 128;
         p.remap_mtiles = mt;
         dim3 grid(remap_grid_big(N, BN, mt), 1, batch);
-        const bool relu = epi == EPI_RELU, f32 = Cf != nullptr;
-#define FPM_BIG(BN_, R_, F_) hipLaunchKernelGGL((gemm_big_kernel<BN_, R_, F_>), grid, dim3(G2_THREADS), 0, st, p)
-        if (BN == 256) {
-            if (relu) { if (f32) FPM_BIG(256, true, true); else FPM_BIG(256, true, false); }
-            else { if (f32) FPM_BIG(256, false, true); else FPM_BIG(256, false, false); }
+        const bool f32 = Cf != nullptr;
+#define FPM_BIG(BN_, E_, F_) hipLaunchKernelGGL((gemm_big_kernel<BN_, E_, F_>), grid, dim3(G2_THREADS), 0, st, p)
+        if (epi == EPI_AFFINITY) {
+            if (BN == 256) FPM_BIG(256, EPI_AFFINITY, true); else FPM_BIG(128, EPI_AFFINITY, true);
+        } else if (BN == 256) {
+            if (epi == EPI_RELU) { if (f32) FPM_BIG(256, EPI_RELU, true); else FPM_BIG(256, EPI_RELU, false); }
+            else { if (f32) FPM_BIG(256, EPI_STORE, true); else FPM_BIG(256, EPI_STORE, false); }
         } else {
-            if (relu) { if (f32) FPM_BIG(128, true, true); else FPM_BIG(128, true, false); }
-            else { if (f32) FPM_BIG(128, false, true); else FPM_BIG(128, false, false); }
+            if (epi == EPI_RELU) { if (f32) FPM_BIG(128, EPI_RELU, true); else FPM_BIG(128, EPI_RELU, false); }
+            else { if (f32) FPM_BIG(128, EPI_STORE, true); else FPM_BIG(128, EPI_STORE, false); }
         }
 #undef FPM_BIG
         return check_launch("fpm_gemm");

@@ -13,7 +13,8 @@
 // * Two LDS stages: the loads of K-tile t+1 are issued before the MFMAs of tile t and retired by
 //   the barrier that ends step t.
 // * Epilogue through LDS (rows padded by 16 B): bf16 output in one pass, fp32 output in two
-//   128-row halves; 16-B coalesced global stores; optional bias and ReLU on the fp32 accumulator.
+//   128-row halves; 16-B coalesced global stores; optional bias, then ReLU or the per-pair
+//   affinity mask + softplus on the fp32 accumulator.
 // * Requirements (checked by the launchers): K % 64 == 0 (callers pad K with zeros), N % 8 == 0,
 //   lda/ldb % 8 == 0, ldc 16-B aligned rows.  Rows past M and columns past N are clamped on load
 //   and never stored.
@@ -51,15 +52,17 @@ inline unsigned remap_grid256(int N, int mtiles) { return remap_grid_big(N, 256,
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
 
-// epilogue: optional bias, optional ReLU (the only epilogues these GEMMs need; compiled per variant
-// so the unrolled 128-element epilogue stays small)
-template <bool RELU>
-__device__ __forceinline__ float g2_epi(const float* __restrict__ bias, float v, int n) {
+// epilogue: optional bias, then store / ReLU / the vertex-affinity mask + softplus (compiled per
+// variant so the unrolled 128-element epilogue stays small)
+template <int EPI>
+__device__ __forceinline__ float g2_epi(const float* __restrict__ bias, float v, int r, int n, int n1b, int n2b) {
     if (bias) v += bias[n];
-    return RELU ? fmaxf(v, 0.f) : v;
+    if (EPI == EPI_RELU) return fmaxf(v, 0.f);
+    if (EPI == EPI_AFFINITY) return (r < n2b && n < n1b) ? softplus_f(v) - 0.5f : 0.f;
+    return v;
 }
 
-template <int BN, bool RELU, bool F32OUT>
+template <int BN, int EPI, bool F32OUT>
 __global__ __launch_bounds__(G2_THREADS, 1) void gemm_big_kernel(GemmParams p) {
     using Cfg = G2Cfg<BN>;
     constexpr int FM = Cfg::FM, FN = Cfg::FN;
@@ -163,6 +166,8 @@ __global__ __launch_bounds__(G2_THREADS, 1) void gemm_big_kernel(GemmParams p) {
     }
 
     // epilogue through LDS
+    int n1b = 0, n2b = 0;
+    if (EPI == EPI_AFFINITY) { n1b = p.n1[batch]; n2b = p.n2[batch]; }
     if (!F32OUT) {
         // bf16 tile [256][BN] with (2*BN + 16)-B rows
         constexpr int ROW = BN * 2 + 16;
@@ -175,7 +180,7 @@ __global__ __launch_bounds__(G2_THREADS, 1) void gemm_big_kernel(GemmParams p) {
                 for (int fn = 0; fn < FN; ++fn) {
                     const int c = wn * FN * 16 + fn * 16 + (lane & 15);
                     const int n = n0 + c < p.N ? n0 + c : p.N - 1;
-                    *(bf16_t*)(smem + r * ROW + c * 2) = f2bf(g2_epi<RELU>(p.bias, acc[fm][fn][j], n));
+                    *(bf16_t*)(smem + r * ROW + c * 2) = f2bf(g2_epi<EPI>(p.bias, acc[fm][fn][j], row0 + r, n, n1b, n2b));
                 }
             }
         __syncthreads();
@@ -207,7 +212,8 @@ __global__ __launch_bounds__(G2_THREADS, 1) void gemm_big_kernel(GemmParams p) {
                         for (int fn = 0; fn < FN; ++fn) {
                             const int c = wn * FN * 16 + fn * 16 + (lane & 15);
                             const int n = n0 + c < p.N ? n0 + c : p.N - 1;
-                            *(float*)(smem + (r - h * 128) * ROW + c * 4) = g2_epi<RELU>(p.bias, acc[fm][fn][j], n);
+                            *(float*)(smem + (r - h * 128) * ROW + c * 4) =
+                                g2_epi<EPI>(p.bias, acc[fm][fn][j], row0 + r, n, n1b, n2b);
                         }
                     }
             }

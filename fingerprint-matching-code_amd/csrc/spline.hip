@@ -163,25 +163,26 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(int* blk_cnt, long nblk
     __shared__ int tilebuf[16384];
     __shared__ int cell_tot[NCELL], tile_off[NCELL + 1], coff[NCELL + 1];
     const int tid = threadIdx.x;
-    // (1) per-cell scans over blocks (nblk is at most a few thousand: one block-wide scan per cell)
-    for (int k = 0; k < NCELL; ++k) {
-        int carry = 0;
-        for (long t0 = 0; t0 < nblk; t0 += 1024) {
-            long i = t0 + tid;
-            int v = i < nblk ? blk_cnt[i * NCELL + k] : 0;
-            part[tid] = v;
-            __syncthreads();
-            for (int o = 1; o < 1024; o <<= 1) {
-                int w = tid >= o ? part[tid - o] : 0;
-                __syncthreads();
-                part[tid] += w;
-                __syncthreads();
+    // (1) per-cell exclusive scans over blocks: one wave per cell, 64 entries per step via shuffles
+    //     (no block-wide barriers on this serial path)
+    {
+        const int lane = tid & 63, wv = tid >> 6;
+        for (int k = wv; k < NCELL; k += 16) {
+            int carry = 0;
+            for (long t0 = 0; t0 < nblk; t0 += 64) {
+                const long i = t0 + lane;
+                const int v = i < nblk ? blk_cnt[i * NCELL + k] : 0;
+                int incl = v;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int y = __shfl_up(incl, o);
+                    if (lane >= o) incl += y;
+                }
+                if (i < nblk) blk_cnt[i * NCELL + k] = carry + incl - v;
+                carry += __shfl(incl, 63);
             }
-            if (i < nblk) blk_cnt[i * NCELL + k] = carry + part[tid] - v;
-            carry += part[1023];
-            __syncthreads();
+            if (lane == 0) cell_tot[k] = carry;
         }
-        if (tid == 0) cell_tot[k] = carry;
     }
     __syncthreads();
     if (tid == 0) {
@@ -479,7 +480,7 @@ extern "C" int fpm_spline_conv_fwd(int dtype, const void* x_op, const void* plan
             (void)hipEventRecord(rec.a, st);
         }
         if (dtype == 0) hipLaunchKernelGGL((gemm_kernel<float, false>), grid, dim3(GTHREADS), 0, st, p);
-        else hipLaunchKernelGGL((gemm_big_kernel<256, false, false>), grid, dim3(G2_THREADS), 0, st, p);
+        else hipLaunchKernelGGL((gemm_big_kernel<256, EPI_STORE, false>), grid, dim3(G2_THREADS), 0, st, p);
         if (g_prof_on && g_prof_rows && rec.slot < PROF_MAX) {
             (void)hipEventRecord(rec.b, st);
             g_prof.push_back(rec);

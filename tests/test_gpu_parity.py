@@ -338,3 +338,22 @@ def test_probe_gallery_shared_equals_per_pair(sd, dtype):
     b = net.run(plain, chunks=2)
     for k in ("s", "ss", "ds_mat", "perm_mat", "k_prob", "cls_prob"):
         assert torch.equal(a[k], b[k]), k
+
+
+def test_gemm_big_affinity_epilogue():
+    """Vertex-affinity epilogue on the 256-row kernel (batched Kp^T: rows = graph-2 nodes)."""
+    g = torch.Generator().manual_seed(9)
+    B, M, N, K = 4, 256, 256, 768
+    A = (torch.randn(B, M, K, generator=g) * 0.05).to(torch.bfloat16)
+    Bm = (torch.randn(B, N, K, generator=g) * 0.05).to(torch.bfloat16)
+    n1 = torch.tensor([256, 200, 131, 256], dtype=torch.int32)
+    n2 = torch.tensor([256, 256, 99, 180], dtype=torch.int32)
+    out = torch.empty(B, M, N, device=DEV)
+    ops.gemm(A.to(DEV), Bm.to(DEV), M, N, K, K, K, batch=B, sA=M * K, sB=N * K, sC=M * N, epi=ops.EPI_AFFINITY,
+             out_f=out, n1=n1.to(DEV), n2=n2.to(DEV))
+    ref = torch.nn.functional.softplus(A.float() @ Bm.float().transpose(1, 2)) - 0.5
+    for b in range(B):
+        r, c = int(n2[b]), int(n1[b])
+        assert (out[b, :r, :c].cpu() - ref[b, :r, :c]).abs().max() < 1e-4
+        assert out[b, r:].abs().max().item() == 0 if r < M else True
+        assert out[b, :, c:].abs().max().item() == 0 if c < N else True

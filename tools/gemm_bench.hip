@@ -75,7 +75,7 @@ int main(int argc, char** argv) {
             CK(hipEventRecord(e0));
             for (int r = 0; r < reps; ++r) {
                 if (v == 0) hipLaunchKernelGGL((gemm_kernel<bf16_t, false>), g1, dim3(GTHREADS), 0, 0, p1);
-                else hipLaunchKernelGGL((gemm_big_kernel<256, false, false>), g2, dim3(G2_THREADS), 0, 0, p2);
+                else hipLaunchKernelGGL((gemm_big_kernel<256, EPI_STORE, false>), g2, dim3(G2_THREADS), 0, 0, p2);
             }
             CK(hipEventRecord(e1));
             CK(hipEventSynchronize(e1));
