@@ -100,60 +100,84 @@ __global__ __launch_bounds__(256) void afau_row_attn_kernel(const float* __restr
 // InstanceNorm1d over positions (afau.py:145-176) of x = in1 (+ in2), or of the synthesised col
 // input C0 + bias (onehot mode).  Writes out_f / out_t, or (gmax != null) only the max over
 // positions of the normalised values (MaxPool1d over the -inf padded 600 positions, ngm.py:402-405).
-template <typename T>
-__global__ __launch_bounds__(256) void instnorm_kernel(const float* __restrict__ in1, const float* __restrict__ in2,
-                                                       int P, int Cn, const int* __restrict__ nvalid,
-                                                       const float* __restrict__ onehot_bias, const float* __restrict__ w,
-                                                       const float* __restrict__ bb, float eps, float* __restrict__ out_f,
-                                                       T* __restrict__ out_t, int ldt, float* __restrict__ gmax) {
-    __shared__ float ps[4][64], pq[4][64];
-    const int b = blockIdx.x, c = blockIdx.y * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
+// 1024 threads = 16 position groups x 64 channels; each thread keeps its <= NV values in registers,
+// so x is read once (mean, variance and output from registers).
+template <typename T, int NV>
+__global__ __launch_bounds__(1024) void instnorm_kernel(const float* __restrict__ in1, const float* __restrict__ in2,
+                                                        int P, int Cn, const int* __restrict__ nvalid,
+                                                        const float* __restrict__ onehot_bias, const float* __restrict__ w,
+                                                        const float* __restrict__ bb, float eps, float* __restrict__ out_f,
+                                                        T* __restrict__ out_t, int ldt, float* __restrict__ gmax) {
+    __shared__ float red[16][64];
+    const int b = blockIdx.x, cl = threadIdx.x & 63, c = blockIdx.y * 64 + cl, g = threadIdx.x >> 6;
     const bool cv = c < Cn;
     const int nb = onehot_bias ? nvalid[b] : 0;
-    auto val = [&](int p) -> float {
-        if (onehot_bias) return ((p == c && p < nb) ? 1.f : 0.f) + onehot_bias[c];
-        long o = ((long)b * P + p) * Cn + c;
-        return in2 ? in1[o] + in2[o] : in1[o];
-    };
-    float s = 0.f;
-    if (cv)
-        for (int p = g; p < P; p += 4) s += val(p);
-    ps[g][threadIdx.x & 63] = s;
-    __syncthreads();
-    const float mean = (ps[0][threadIdx.x & 63] + ps[1][threadIdx.x & 63] + ps[2][threadIdx.x & 63] +
-                        ps[3][threadIdx.x & 63]) / (float)P;
-    float q = 0.f;
-    if (cv)
-        for (int p = g; p < P; p += 4) {
-            float d = val(p) - mean;
-            q += d * d;
+    float v[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        const int p = g + 16 * k;
+        float x = 0.f;
+        if (cv && p < P) {
+            if (onehot_bias) {
+                x = ((p == c && p < nb) ? 1.f : 0.f) + onehot_bias[c];
+            } else {
+                const long o = ((long)b * P + p) * Cn + c;
+                x = in2 ? in1[o] + in2[o] : in1[o];
+            }
         }
-    pq[g][threadIdx.x & 63] = q;
+        v[k] = x;
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) s += v[k];
+    red[g][cl] = s;
     __syncthreads();
-    const float var = (pq[0][threadIdx.x & 63] + pq[1][threadIdx.x & 63] + pq[2][threadIdx.x & 63] +
-                       pq[3][threadIdx.x & 63]) / (float)P;
+    float tot = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) tot += red[q][cl];
+    const float mean = tot / (float)P;
+    __syncthreads();
+    float sq = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        const int p = g + 16 * k;
+        const float d = v[k] - mean;
+        if (p < P) sq += d * d;
+    }
+    red[g][cl] = sq;
+    __syncthreads();
+    float var = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) var += red[q][cl];
+    var /= (float)P;
     const float rstd = 1.f / sqrtf(var + eps);
     const float ww = cv ? w[c] : 0.f, bv = cv ? bb[c] : 0.f;
     float mx = -INFINITY;
-    for (int p = g; cv && p < P; p += 4) {
-        float y = (val(p) - mean) * rstd * ww + bv;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        const int p = g + 16 * k;
+        if (!cv || p >= P) continue;
+        const float y = (v[k] - mean) * rstd * ww + bv;
         if (gmax) mx = fmaxf(mx, y);
         else {
-            long o = ((long)b * P + p) * Cn + c;
+            const long o = ((long)b * P + p) * Cn + c;
             if (out_f) out_f[o] = y;
             if (out_t) out_t[((long)b * P + p) * ldt + c] = fpm::from_f<T>(y);
         }
     }
     // zero K-padding columns [Cn, ldt) of the operand copy (the next GEMM runs K = ldt)
     if (!cv && out_t && !gmax && c < ldt)
-        for (int p = g; p < P; p += 4) out_t[((long)b * P + p) * ldt + c] = fpm::from_f<T>(0.f);
+        for (int p = g; p < P; p += 16) out_t[((long)b * P + p) * ldt + c] = fpm::from_f<T>(0.f);
     if (gmax) {
         __syncthreads();
-        ps[g][threadIdx.x & 63] = mx;
+        red[g][cl] = mx;
         __syncthreads();
-        if (g == 0 && cv)
-            gmax[(long)b * Cn + c] = fmaxf(fmaxf(ps[0][threadIdx.x & 63], ps[1][threadIdx.x & 63]),
-                                           fmaxf(ps[2][threadIdx.x & 63], ps[3][threadIdx.x & 63]));
+        if (g == 0 && cv) {
+            float m = red[0][cl];
+#pragma unroll
+            for (int q = 1; q < 16; ++q) m = fmaxf(m, red[q][cl]);
+            gmax[(long)b * Cn + c] = m;
+        }
     }
 }
 
@@ -216,13 +240,14 @@ extern "C" int fpm_instnorm(int dtype, const float* in1, const float* in2, int B
     FPM_CHECK_ARG(ldt >= Cn, "instnorm: ldt %d < Cn %d", ldt, Cn);
     const int cols = ldt > Cn ? ldt : Cn;
     dim3 grid(B, (cols + 63) / 64);
+    FPM_CHECK_ARG(P <= 640, "instnorm: P=%d > 640 positions", P);
     hipStream_t st = (hipStream_t)stream;
-    if (dtype == 0)
-        hipLaunchKernelGGL((instnorm_kernel<float>), grid, dim3(256), 0, st, in1, in2, P, Cn, nvalid, onehot_bias, w,
-                           bias, eps, out_f, (float*)out_t, ldt, gmax);
-    else
-        hipLaunchKernelGGL((instnorm_kernel<bf16_t>), grid, dim3(256), 0, st, in1, in2, P, Cn, nvalid, onehot_bias, w,
-                           bias, eps, out_f, (bf16_t*)out_t, ldt, gmax);
+#define FPM_IN(TT, NV)                                                                                     \
+    hipLaunchKernelGGL((instnorm_kernel<TT, NV>), grid, dim3(1024), 0, st, in1, in2, P, Cn, nvalid, onehot_bias, w, \
+                       bias, eps, out_f, (TT*)out_t, ldt, gmax)
+    if (dtype == 0) { if (P <= 256) FPM_IN(float, 16); else FPM_IN(float, 40); }
+    else { if (P <= 256) FPM_IN(bf16_t, 16); else FPM_IN(bf16_t, 40); }
+#undef FPM_IN
     return fpm::check_launch("fpm_instnorm");
 }
 

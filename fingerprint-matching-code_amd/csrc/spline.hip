@@ -326,9 +326,14 @@ __global__ __launch_bounds__(256) void combine_kernel(const T* __restrict__ Y, c
                                                       const float* __restrict__ xres, const float* __restrict__ cscale,
                                                       float* __restrict__ out_f, T* __restrict__ out_t) {
     const int lane = threadIdx.x & 63;
-    const long v = (long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (v >= num_nodes) return;
-    const int b = (int)(v / nmax), loc = (int)(v - (long)b * nmax);
+    // graph-per-XCD block order: XCD x = blockIdx % 8 takes graphs x, x+8, ... so a graph's product
+    // rows (~3.7 MB at n = 256, each read ~2.4 times by its in-edges) stay in one L2
+    const int bpg = (nmax + 3) / 4;
+    const int xk = blockIdx.x >> 3;
+    const int b = (xk / bpg) * 8 + (blockIdx.x & 7);
+    const int loc = (xk % bpg) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (loc >= nmax || (long)b * nmax >= num_nodes) return;
+    const long v = (long)b * nmax + loc;
     const bool valid = loc < nvalid[b];
     const int beg = dst_ptr[v], end = dst_ptr[v + 1];
     const long root_row = (long)cell_off[25] + v;
@@ -487,7 +492,8 @@ extern "C" int fpm_spline_conv_fwd(int dtype, const void* x_op, const void* plan
         }
     }
     {
-        dim3 grid((unsigned)((num_nodes + 3) / 4));
+        const long graphs = (num_nodes + nmax - 1) / nmax;
+        dim3 grid((unsigned)(((graphs + 7) / 8) * 8 * ((nmax + 3) / 4)));
         if (dtype == 0)
             hipLaunchKernelGGL((combine_kernel<float>), grid, dim3(256), 0, st, (const float*)y_ws,
                                (const int*)(w + L.cell_off), bias, (const int*)(w + L.dst_ptr),
