@@ -168,7 +168,9 @@ def main():
         net.run(bt)
         gpu_s += net.last_timing["gpu_stage_s"]
         lsa_s += net.last_timing["lsa_s"]
-        log("step: gpu-stage %.3fs lsa %.3fs" % (net.last_timing["gpu_stage_s"], net.last_timing["lsa_s"]))
+        lt = net.last_timing
+        log("step: gpu-stage %.3fs lsa %.3fs enqueue %.3fs first-chunk %.3fs total %.3fs" % (
+            lt["gpu_stage_s"], lt["lsa_s"], lt["enqueue_s"], lt["first_chunk_wait_s"], lt["total_s"]))
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier()

@@ -420,6 +420,7 @@ class Net(nn.Module):
                 r, ev = self._stage_a(part, b0, b1, o, keep_feats, gt_ks, min_pt, st, gc)
             outs.append(r)
             events.append(ev)
+        t_enq = time.perf_counter()
         t_lsa, t_first = 0.0, None
         for c, (part, ev) in enumerate(zip(parts, events)):
             b0, b1 = getattr(part, "pair_range", (0, B))
@@ -448,7 +449,8 @@ class Net(nn.Module):
             res["ks_error"] = 0.0
         # GPU time of the stages before the Hungarian (all chunks), from events on the streams
         self.last_timing = dict(gpu_stage_s=ev_start.elapsed_time(events[-1]) / 1e3, lsa_s=t_lsa,
-                                first_chunk_wait_s=(t_first or t0) - t0, chunks=len(parts))
+                                first_chunk_wait_s=(t_first or t0) - t0, chunks=len(parts),
+                                enqueue_s=t_enq - t0, total_s=time.perf_counter() - t0)
         return res
 
     def forward(self, data_dict, regression=True):
