@@ -202,6 +202,14 @@ def main():
     peak = 2500.0 if args.dtype == "bf16" else 157.3
     achieved = (fl.value / (ms.value / 1e3)) / 1e12 if ms.value > 0 else 0.0
 
+    # HBM bytes per launch of the same kernel from the committed rocprofv3 PMC pass (FETCH_SIZE x2 +
+    # WRITE_SIZE, separate passes; tools/pmc_gemm.sh -> profiles/r01_pmc_product_gemm.json)
+    traffic = None
+    pmc_file = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_pmc_product_gemm.json")
+    if args.dtype == "bf16" and args.config in ("c3", "c5") and os.path.exists(pmc_file):
+        with open(pmc_file) as f:
+            traffic = json.load(f).get("traffic_bytes_per_launch")
+
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -236,7 +244,8 @@ def main():
             "host_lsa_ms_per_step": lsa_s / args.steps * 1e3,
             "roofline": {"kernel": "spline (node, cell) product GEMM (%s, grouped by cell)" % ("gemm_big_kernel<256>" if args.dtype == "bf16" else "gemm_kernel<f32>"),
                          "bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                         "frac": achieved / peak, "traffic": None,
+                         "frac": achieved / peak, "traffic": traffic,
+                         "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, profiles/r01_pmc_product_gemm.json)",
                          "launches": cnt.value, "avg_launch_ms": ms.value / max(cnt.value, 1),
                          "algorithmic_flops_per_launch": fl.value / max(cnt.value, 1),
                          "isolated_achieved": (iso_fl.value / (iso_ms.value / 1e3)) / 1e12 if iso_ms.value > 0 else 0.0,

@@ -1,0 +1,8 @@
+#!/bin/bash
+# PMC HBM-traffic passes (FETCH_SIZE, WRITE_SIZE: separate passes) on the product GEMM of a short
+# bench run; per-dispatch values land in gpurun_out/pmc_gemm/{fetch,write}/run_counter_collection.csv
+set -o pipefail
+export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT"; O=gpurun_out/pmc_gemm; mkdir -p $O
+p() { local n=$1; shift; timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-include-regex "gemm_big_kernel<256" -d $O/$n -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline > $O/$n.log 2>&1; }
+p fetch FETCH_SIZE && p write WRITE_SIZE
