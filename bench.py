@@ -46,6 +46,27 @@ def make_gallery(seed, first, G, n, workers):
         return pool.map(_gen_gallery, ids, chunksize=max(1, G // (workers * 4)))
 
 
+def shard(config, rank, world, batch, gallery):
+    """(first pair id, pairs on this rank).  c4: contiguous gallery shard (strong scaling, probe
+    replicated); otherwise ``batch`` pairs per rank (weak scaling).  No data-path collective."""
+    if config == "c4":
+        share = (gallery + world - 1) // world
+        first = rank * share
+        return first, max(0, min(share, gallery - first))
+    return rank * batch, batch
+
+
+def reduce_max(values, world):
+    """Max over ranks of per-rank timings (gloo all_reduce; identity on one rank)."""
+    if world <= 1:
+        return list(values)
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(values, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.tolist()
+
+
 def make_pairs(seed, first, B, n, workers):
     ids = [(seed, first + b, n) for b in range(B)]
     if workers <= 1 or B < 8 or _under_profiler():
@@ -112,17 +133,16 @@ def main():
 
     # inputs first (forked workers must not inherit a GPU context)
     t_gen = time.perf_counter()
+    first, args.batch = shard(args.config, rank, world, args.batch, args.gallery)
     if args.config == "c4":
         # contiguous gallery shard per rank; the probe is replicated
-        share = (args.gallery + world - 1) // world
-        g0 = rank * share
-        args.batch = max(0, min(share, args.gallery - g0))
+        g0 = first
         from fpm import synth
         probe = synth.make_graph(args.seed, 0, 0, args.n)
         gallery = make_gallery(args.seed, 1 + g0, args.batch, args.n, args.gen_workers)
         pairs = None
     else:
-        pairs = make_pairs(args.seed, rank * args.batch, args.batch, args.n, args.gen_workers)
+        pairs = make_pairs(args.seed, first, args.batch, args.n, args.gen_workers)
     t_gen = time.perf_counter() - t_gen
     log("generated %d pairs in %.1fs" % (args.batch, t_gen))
 
@@ -193,10 +213,7 @@ def main():
     lib.fpm_profile_enable(0)
     net.n_streams = saved_streams
     _lib.call("fpm_profile_read", ctypes.byref(iso_ms), ctypes.byref(iso_fl), ctypes.byref(iso_cnt))
-    if world > 1:
-        t = torch.tensor([elapsed, gpu_s, lsa_s], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, gpu_s, lsa_s = t.tolist()
+    elapsed, gpu_s, lsa_s = reduce_max([elapsed, gpu_s, lsa_s], world)
     pairs_total = (args.gallery if args.config == "c4" else args.batch * world) * args.steps
     value = pairs_total / elapsed
     peak = 2500.0 if args.dtype == "bf16" else 157.3
@@ -206,7 +223,7 @@ def main():
     # WRITE_SIZE, separate passes; tools/pmc_gemm.sh -> profiles/r01_pmc_product_gemm.json)
     traffic = None
     pmc_file = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_pmc_product_gemm.json")
-    if args.dtype == "bf16" and args.config in ("c3", "c5") and os.path.exists(pmc_file):
+    if args.dtype == "bf16" and args.config == "c3" and os.path.exists(pmc_file):
         with open(pmc_file) as f:
             traffic = json.load(f).get("traffic_bytes_per_launch")
 

@@ -1,0 +1,75 @@
+"""World-size-2 gloo run of the multi-GPU bench path's host logic (CPU): pair / gallery sharding
+covers every pair exactly once, per-rank host Hungarian on its shard equals the single-process
+result, and the max-over-ranks timing reduction.  (The device path is covered by the GPU shard
+test: a shard computed alone equals its slice of the full batch bit for bit.)"""
+import json
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import REPO
+
+sys.path.insert(0, REPO)
+import bench  # noqa: E402
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _mats(n_pairs, n):
+    g = torch.Generator().manual_seed(3)
+    s = torch.rand(n_pairs, n, n, generator=g)
+    s[:, :, :3] = 0.5                              # ties
+    return s
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from fpm import ops
+    res = {}
+    for cfg, batch, gallery in (("c3", 6, 0), ("c4", 0, 13)):
+        first, cnt = bench.shard(cfg, rank, world, batch, gallery)
+        total = batch * world if cfg == "c3" else gallery
+        s = _mats(total, 12)[first:first + cnt]
+        n = torch.full((cnt,), 12, dtype=torch.int32)
+        a = ops.lsa_batch_host(s, n, n, 2) if cnt else torch.empty(0, 12, dtype=torch.int32)
+        parts = [None] * world
+        dist.all_gather_object(parts, (first, cnt, a.tolist()))
+        res[cfg] = parts
+    t = bench.reduce_max([float(rank + 1), 10.0 - rank], world)
+    if rank == 0:
+        with open(os.path.join(out_dir, "res.json"), "w") as f:
+            json.dump({"res": res, "t": t}, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_sharding(tmp_path):
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    with open(os.path.join(tmp_path, "res.json")) as f:
+        d = json.load(f)
+    res, t = d["res"], d["t"]
+    assert t == [2.0, 10.0]
+    from fpm import ops
+    for cfg, total in (("c3", 12), ("c4", 13)):
+        parts = sorted(res[cfg], key=lambda p: p[0])
+        assert parts[0][0] == 0 and sum(p[1] for p in parts) == total
+        assert all(a[0] + a[1] == b[0] for a, b in zip(parts, parts[1:]))
+        got = np.concatenate([np.array(p[2], dtype=np.int32) for p in parts if p[1]])
+        n = torch.full((total,), 12, dtype=torch.int32)
+        ref = ops.lsa_batch_host(_mats(total, 12), n, n, 1).numpy()
+        np.testing.assert_array_equal(got, ref)
