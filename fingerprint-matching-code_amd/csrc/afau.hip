@@ -12,8 +12,10 @@
 
 namespace {
 
-// one workgroup per (pair, 16-row tile); 4 waves x 4 rows; heads looped
-template <typename T>
+// one workgroup per (pair, 16-row tile); 4 waves x 4 rows; heads looped.  The tile's costs stay
+// in registers across the 16 heads (lane j-slots: j = lane + 64 jj, jj < NJ); scores stay in
+// registers through max / exp / sum, and only the normalised probabilities go to LDS for AV.
+template <typename T, int NJ>
 __global__ __launch_bounds__(256) void afau_row_attn_kernel(const float* __restrict__ cost, long c_sb, long c_ld,
                                                             int n1max, int n2max, const int* __restrict__ n2,
                                                             const float* __restrict__ Wv, int emb,
@@ -28,6 +30,16 @@ __global__ __launch_bounds__(256) void afau_row_attn_kernel(const float* __restr
     const int b = blockIdx.x, i0 = blockIdx.y * 16, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int n2b = n2[b];
     const float* Cb = cost + (long)b * c_sb;
+    float creg[4][NJ];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+        const int i = i0 + wv * 4 + rr;
+#pragma unroll
+        for (int jj = 0; jj < NJ; ++jj) {
+            const int j = lane + 64 * jj;
+            creg[rr][jj] = (i < n1max && j < n2max) ? Cb[(long)i * c_ld + j] : 0.f;
+        }
+    }
     for (int h = 0; h < 16; ++h) {
         __syncthreads();
         for (int k = tid; k < n2max * 16; k += 256) {      // coalesced along j
@@ -42,29 +54,37 @@ __global__ __launch_bounds__(256) void afau_row_attn_kernel(const float* __restr
             w2[m] = mix2w[h * 16 + m];
         }
         const float b2 = mix2b[h];
+#pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
             const int lr = wv * 4 + rr, i = i0 + lr;
             if (i >= n1max) break;
+            float sv[NJ];
             float mx = -INFINITY;
-            for (int j = lane; j < n2max; j += 64) {
-                float c = Cb[(long)i * c_ld + j];
-                float s = 0.f;
 #pragma unroll
-                for (int m = 0; m < 16; ++m) s += fmaxf(c * w1[m] + b1[m], 0.f) * w2[m];
-                s += b2;
-                Pm[lr * n2max + j] = s;
-                mx = fmaxf(mx, s);
+            for (int jj = 0; jj < NJ; ++jj) {
+                const float c = creg[rr][jj];
+                float sc = 0.f;
+#pragma unroll
+                for (int m = 0; m < 16; ++m) sc += fmaxf(c * w1[m] + b1[m], 0.f) * w2[m];
+                sc += b2;
+                sv[jj] = sc;
+                if (lane + 64 * jj < n2max) mx = fmaxf(mx, sc);
             }
             mx = fpm::warp_max(mx);
             float sum = 0.f;
-            for (int j = lane; j < n2max; j += 64) {
-                float e = fpm::fast_exp2((Pm[lr * n2max + j] - mx) * fpm::LOG2E_F);
-                Pm[lr * n2max + j] = e;
-                sum += e;
+#pragma unroll
+            for (int jj = 0; jj < NJ; ++jj) {
+                const float e = fpm::fast_exp2((sv[jj] - mx) * fpm::LOG2E_F);
+                sv[jj] = e;
+                if (lane + 64 * jj < n2max) sum += e;
             }
             sum = fpm::warp_sum(sum);
-            float inv = 1.f / sum;
-            for (int j = lane; j < n2max; j += 64) Pm[lr * n2max + j] *= inv;
+            const float inv = 1.f / sum;
+#pragma unroll
+            for (int jj = 0; jj < NJ; ++jj) {
+                const int j = lane + 64 * jj;
+                if (j < n2max) Pm[lr * n2max + j] = sv[jj] * inv;
+            }
         }
         __syncthreads();
         // out[i][h*16 + d] for the 16 rows: thread = (row, 4 d's, j residue mod 4), float4 V reads
@@ -217,18 +237,18 @@ extern "C" int fpm_crossset_attn_fwd(int dtype, const float* cost, long c_sb, lo
     size_t sh = (size_t)(n2max * 20 + 16 * n2max) * 4;
     FPM_CHECK_ARG(sh <= 160 * 1024, "crossset_attn: n2max %d needs %zu B of LDS", n2max, sh);
     hipStream_t st = (hipStream_t)stream;
-    if (sh > 64 * 1024) {   // n2max > 455: opt in to the larger LDS allocation of gfx950
-        (void)hipFuncSetAttribute((const void*)afau_row_attn_kernel<float>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
-        (void)hipFuncSetAttribute((const void*)afau_row_attn_kernel<bf16_t>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
-    }
-    if (dtype == 0)
-        hipLaunchKernelGGL((afau_row_attn_kernel<float>), grid, dim3(256), sh, st, cost, c_sb, c_ld, n1max, n2max, n2,
-                           Wv, emb, mix1w, mix1b, mix2w, mix2b, (float*)out);
-    else
-        hipLaunchKernelGGL((afau_row_attn_kernel<bf16_t>), grid, dim3(256), sh, st, cost, c_sb, c_ld, n1max, n2max,
-                           n2, Wv, emb, mix1w, mix1b, mix2w, mix2b, (bf16_t*)out);
+    FPM_CHECK_ARG(n2max <= 640, "crossset_attn: n2max %d > 640", n2max);
+#define FPM_ATT(TT, NJ)                                                                                      \
+    do {                                                                                                     \
+        if (sh > 64 * 1024)                                                                                  \
+            (void)hipFuncSetAttribute((const void*)afau_row_attn_kernel<TT, NJ>,                             \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);                   \
+        hipLaunchKernelGGL((afau_row_attn_kernel<TT, NJ>), grid, dim3(256), sh, st, cost, c_sb, c_ld, n1max, n2max, \
+                           n2, Wv, emb, mix1w, mix1b, mix2w, mix2b, (TT*)out);                               \
+    } while (0)
+    if (dtype == 0) { if (n2max <= 256) FPM_ATT(float, 4); else FPM_ATT(float, 10); }
+    else { if (n2max <= 256) FPM_ATT(bf16_t, 4); else FPM_ATT(bf16_t, 10); }
+#undef FPM_ATT
     return fpm::check_launch("fpm_crossset_attn_fwd");
 }
 
