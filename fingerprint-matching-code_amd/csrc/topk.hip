@@ -28,7 +28,8 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
                                                          const int* __restrict__ n1, const int* __restrict__ n2,
                                                          const float* __restrict__ kvec, float* __restrict__ out,
                                                          long ob, long old_, int n1max, int n2max, int iters,
-                                                         float tau, int* __restrict__ steps_out) {
+                                                         float tau, int* __restrict__ steps_out,
+                                                         float* __restrict__ out2, long ob2, long old2) {
     __shared__ float sa[16], sb_[16];
     __shared__ int sflag[16];
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -196,11 +197,15 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
 
     // ds_mat[i][j] = exp(L[q(i,j), 1]) on the valid block, 0 elsewhere
     float* O = out + (long)b * ob;
+    float* O2 = out2 ? out2 + (long)b * ob2 : nullptr;   // optional second copy (host-mapped pinned memory)
     float mnl, mxl;
     anchors(mnl, mxl);
     for (int idx = tid; idx < n1max * n2max; idx += 1024) {
         int i = idx / n2max, j = idx - i * n2max;
-        if (i >= n1b || j >= n2b) O[i * old_ + j] = 0.f;
+        if (i >= n1b || j >= n2b) {
+            O[i * old_ + j] = 0.f;
+            if (O2) O2[i * old2 + j] = 0.f;
+        }
     }
     int n2o = n2b;
     asm volatile("" : "+v"(n2o));   // recompute (i, j) here rather than keep NQ addresses live
@@ -209,7 +214,9 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
         int i = q / n2o, j = q - i * n2o;
         float L0, L1;
         Lpair(sv, mnl, mxl, L0, L1);
-        O[i * old_ + j] = fpm::fast_exp2(L1);
+        const float v = fpm::fast_exp2(L1);
+        O[i * old_ + j] = v;
+        if (O2) O2[i * old2 + j] = v;
     });
 #undef SVAL
 }
@@ -305,14 +312,16 @@ __global__ __launch_bounds__(256) void topk_select_kernel(const float* __restric
 
 extern "C" int fpm_soft_topk_fwd(const float* ss, long s_sb, long s_ld, const int* n1, const int* n2,
                                  const float* k, int B, int n1max, int n2max, int iters, float tau,
-                                 float* out, long o_sb, long o_ld, int* steps_out, void* stream) {
+                                 float* out, long o_sb, long o_ld, int* steps_out, float* out2, long o2_sb,
+                                 long o2_ld, void* stream) {
     FPM_CHECK_ARG(B >= 0 && n1max > 0 && n2max > 0, "soft_topk: bad sizes");
     long nn = (long)n1max * n2max;
     FPM_CHECK_ARG(nn <= (1L << 24), "soft_topk: n1max*n2max=%ld too large", nn);
     if (B == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
 #define LAUNCH(NQ, ST) hipLaunchKernelGGL((soft_topk_kernel<NQ, ST>), dim3(B), dim3(1024), 0, st, ss, s_sb, s_ld, \
-                                           n1, n2, k, out, o_sb, o_ld, n1max, n2max, iters, tau, steps_out)
+                                           n1, n2, k, out, o_sb, o_ld, n1max, n2max, iters, tau, steps_out, \
+                                           out2, o2_sb, o2_ld)
     if (nn <= 1024) LAUNCH(1, false);
     else if (nn <= 4096) LAUNCH(4, false);
     else if (nn <= 16384) LAUNCH(16, false);

@@ -68,6 +68,10 @@ class Net(nn.Module):
         self._stream_cache = {}
         self.n_streams = max(1, int(os.environ.get("FPM_STREAMS", "2")))
         self.tail_splits = int(os.environ.get("FPM_TAIL", "1"))
+        # FPM_ZERO_COPY=1: soft_topk writes ds_mat straight into pinned host memory instead of a
+        # stream copy.  Measured slower (21.2K -> 19.7K pairs/s: the kernel stalls on PCIe writes
+        # on the critical path), so off by default.
+        self.zero_copy = os.environ.get("FPM_ZERO_COPY", "0") == "1"
         self._keep_feats = False
         self._stage_timing = os.environ.get("FPM_STAGE_TIMING", "0") == "1"
         self.stage_times = {}
@@ -352,10 +356,12 @@ class Net(nn.Module):
         self._mark("afau")
         k_used = gt_ks[b0:b1] if self.training else ks * min_pt[b0:b1]
         ops.soft_topk(o["ss"][b0:b1], part.n1, part.n2, k_used.contiguous(), C.SK_ITER_NUM, self.tau,
-                      out=o["ds_mat"][b0:b1], steps=o["sk_steps"][b0:b1])
+                      out=o["ds_mat"][b0:b1], steps=o["sk_steps"][b0:b1],
+                      out_host=self._pinned[b0:b1] if self.zero_copy else None)
         o["_kk"][b0:b1].copy_(ks * min_pt[b0:b1])
         self._mark("soft_topk")
-        self._pinned[b0:b1].copy_(o["ds_mat"][b0:b1], non_blocking=True)
+        if not self.zero_copy:
+            self._pinned[b0:b1].copy_(o["ds_mat"][b0:b1], non_blocking=True)
         ev = torch.cuda.Event(enable_timing=True)
         ev.record(st)
         return r, ev

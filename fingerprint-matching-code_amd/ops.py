@@ -52,13 +52,19 @@ def sinkhorn(s, n1, n2, iters, tau, dummy_row=True, out=None, n1max=None, n2max=
     return out
 
 
-def soft_topk(ss, n1, n2, k, iters=10, tau=0.01, out=None, steps=None):
+def soft_topk(ss, n1, n2, k, iters=10, tau=0.01, out=None, steps=None, out_host=None):
+    """``out_host``: optional pinned host tensor written by the kernel as well (zero-copy D2H of
+    ds_mat for the host Hungarian)."""
     _dev(ss, n1, n2, k)
     B, n1max, n2max = ss.shape
     if out is None:
         out = torch.empty(B, n1max, n2max, device=ss.device, dtype=torch.float32)
+    if out_host is not None and (out_host.is_cuda or not out_host.is_pinned() or tuple(out_host.shape) != (B, n1max, n2max)):
+        raise _lib.FpmError("soft_topk: out_host must be a pinned host tensor of shape (B, n1max, n2max)")
     _lib.call("fpm_soft_topk_fwd", _p(ss), ss.stride(0), ss.stride(1), _p(n1), _p(n2), _p(k), B, n1max, n2max,
-              int(iters), float(tau), _p(out), out.stride(0), out.stride(1), _p(steps), _stream(ss))
+              int(iters), float(tau), _p(out), out.stride(0), out.stride(1), _p(steps), _p(out_host),
+              out_host.stride(0) if out_host is not None else 0, out_host.stride(1) if out_host is not None else 0,
+              _stream(ss))
     return out
 
 

@@ -42,7 +42,7 @@ int fpm_sinkhorn_log_fwd(const float* s, long s_sb, long s_si, long s_sj, float*
  * steps_out (optional, int32[B]) receives the number of normalisation steps run. */
 int fpm_soft_topk_fwd(const float* ss, long s_sb, long s_ld, const int* n1, const int* n2, const float* k, int B,
                       int n1max, int n2max, int iters, float tau, float* out, long o_sb, long o_ld, int* steps_out,
-                      void* stream);
+                      float* out2, long o2_sb, long o2_ld, void* stream);
 
 /* ---- greedy top-k selection -------------------------------------------------------------------
  * Replaces argsort(x * ss_out) + greedy_perm (ngm.py:445-449, soft_topk.py:56-77).

@@ -75,6 +75,23 @@ def test_soft_topk_vs_oracle_large():
     assert (out - ref).abs().max() < 1e-4
 
 
+def test_soft_topk_host_mapped_output():
+    """The kernel's optional second output (pinned host memory, written over PCIe) equals the
+    device output bit for bit, zero padding included."""
+    g = torch.Generator().manual_seed(6)
+    B, n = 3, 40
+    ss = (torch.rand(B, n, n, generator=g) ** 4).to(DEV)
+    n1, n2 = _i32([40, 31, 17]), _i32([40, 25, 33])
+    k = torch.tensor([10.0, 12.5, 3.0]).to(DEV)
+    host = torch.full((B, n, n), 7.0, pin_memory=True)
+    out = ops.soft_topk(ss, n1, n2, k, 10, 0.01, out_host=host)
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu(), host)
+    assert (host[1, 31:, :] == 0).all() and (host[2, :, 33:] == 0).all()
+    with pytest.raises(fpm._lib.FpmError):
+        ops.soft_topk(ss, n1, n2, k, 10, 0.01, out_host=torch.empty(B, n, n))
+
+
 # ---------------------------------------------------------------------------------------- top-k select
 def test_topk_select_golden():
     z = np.load(os.path.join(GOLDEN, "hungarian_greedy.npz"))
