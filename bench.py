@@ -259,7 +259,7 @@ def main():
                        "edges_per_graph": E_tot / (2.0 * args.batch), "parallelism": "pair-sharded x%d" % world},
             "gpu_stage_pairs_per_s": args.batch * world * args.steps / gpu_s,
             "host_lsa_ms_per_step": lsa_s / args.steps * 1e3,
-            "roofline": {"kernel": "spline (node, cell) product GEMM (%s, grouped by cell)" % ("gemm_big_kernel<256>" if args.dtype == "bf16" else "gemm_kernel<f32>"),
+            "roofline": {"kernel": "spline (node, cell) product GEMM (%s, grouped by cell)" % (("gemm_phase_kernel 256x256" if os.environ.get("FPM_GEMM_PHASE", "1") != "0" else "gemm_big_kernel<256>") if args.dtype == "bf16" else "gemm_kernel<f32>"),
                          "bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak, "traffic": traffic,
                          "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, profiles/r01_pmc_product_gemm.json)",

@@ -1,7 +1,8 @@
 // C-ABI entry for the generic (batched, optionally row-gathered) MFMA GEMM with fused epilogues.
 // Used by: SplineConv root term, global-weight coefficient (affinity_layer.py:13), vertex
 // affinity Kp (affinity_layer.py:15-18), AFA-U projections/FFN (afau.py:99-103,188-199).
-#include "gemm_big.h"
+#include "gemm_phase.h"
+#include <cstdlib>
 
 extern "C" int fpm_gemm(int dtype, const void* A, long lda, long sA, const int* a_rows, const void* B, long ldb,
                         long sB, int M, int N, int K, int batch, int epi, const float* bias, float* Cf, void* Ct,
@@ -34,7 +35,12 @@ extern "C" int fpm_gemm(int dtype, const void* A, long lda, long sA, const int* 
         p.remap_mtiles = mt;
         dim3 grid(remap_grid_big(N, BN, mt), 1, batch);
         const bool f32 = Cf != nullptr;
-#define FPM_BIG(BN_, E_, F_) hipLaunchKernelGGL((gemm_big_kernel<BN_, E_, F_>), grid, dim3(G2_THREADS), 0, st, p)
+        const bool phase = BN == 256 && use_gemm_phase(K);
+#define FPM_BIG(BN_, E_, F_)                                                                            \
+    do {                                                                                               \
+        if (BN_ == 256 && phase) hipLaunchKernelGGL((gemm_phase_kernel<E_, F_>), grid, dim3(G2_THREADS), 0, st, p); \
+        else hipLaunchKernelGGL((gemm_big_kernel<BN_, E_, F_>), grid, dim3(G2_THREADS), 0, st, p);      \
+    } while (0)
         if (epi == EPI_AFFINITY) {
             if (BN == 256) FPM_BIG(256, EPI_AFFINITY, true); else FPM_BIG(128, EPI_AFFINITY, true);
         } else if (BN == 256) {
@@ -52,6 +58,22 @@ extern "C" int fpm_gemm(int dtype, const void* A, long lda, long sA, const int* 
     if (dtype == 0) hipLaunchKernelGGL((gemm_kernel<float, false>), grid, dim3(GTHREADS), 0, st, p);
     else hipLaunchKernelGGL((gemm_kernel<bf16_t, false>), grid, dim3(GTHREADS), 0, st, p);
     return check_launch("fpm_gemm");
+}
+
+namespace fpm {
+int& gemm_phase_flag() {
+    static int on = [] {
+        const char* e = getenv("FPM_GEMM_PHASE");
+        return e ? atoi(e) : 1;
+    }();
+    return on;
+}
+}  // namespace fpm
+
+extern "C" int fpm_set_gemm_phase(int on) {
+    const int prev = fpm::gemm_phase_flag();
+    fpm::gemm_phase_flag() = on;
+    return prev;
 }
 
 // f32 -> bf16 conversion (operand copies for the bf16 MFMA path)

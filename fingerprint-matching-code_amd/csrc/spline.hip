@@ -13,7 +13,7 @@
 // and fuses root + bias + ReLU or the Siamese residual.  That is ~2.5x fewer MFMA flops than the
 // per-edge GEMM, and the message tensor is never materialised.  The plan (dst CSR included) is
 // built on device once per side and shared by both layers and the GNN layers.
-#include "gemm_big.h"
+#include "gemm_phase.h"
 
 #include <vector>
 
@@ -485,6 +485,7 @@ extern "C" int fpm_spline_conv_fwd(int dtype, const void* x_op, const void* plan
             (void)hipEventRecord(rec.a, st);
         }
         if (dtype == 0) hipLaunchKernelGGL((gemm_kernel<float, false>), grid, dim3(GTHREADS), 0, st, p);
+        else if (use_gemm_phase(D)) hipLaunchKernelGGL((gemm_phase_kernel<EPI_STORE, false>), grid, dim3(G2_THREADS), 0, st, p);
         else hipLaunchKernelGGL((gemm_big_kernel<256, EPI_STORE, false>), grid, dim3(G2_THREADS), 0, st, p);
         if (g_prof_on && g_prof_rows && rec.slot < PROF_MAX) {
             (void)hipEventRecord(rec.b, st);

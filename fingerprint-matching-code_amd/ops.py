@@ -79,6 +79,12 @@ def topk_select(ds, assign, k, lsa_out=None, out=None):
     return perm
 
 
+def set_gemm_phase(on):
+    """Select the 256x256 bf16 GEMM schedule (1: phase-pipelined, 0: two-stage; bit-identical).
+    Returns the previous setting."""
+    return int(_lib.load().fpm_set_gemm_phase(int(on)))
+
+
 def gemm(A, B, M, N, K, lda, ldb, batch=1, sA=0, sB=0, a_rows=None, epi=EPI_STORE, bias=None, out_f=None,
          out_t=None, ldc=None, sC=0, n1=None, n2=None):
     """C = epi(A @ B^T (+bias)); A: rows of length >= K (lda), B: N x K (ldb)."""

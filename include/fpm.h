@@ -62,6 +62,11 @@ int fpm_gemm(int dtype, const void* A, long lda, long sA, const int* a_rows, con
              const int* n1, const int* n2, void* stream);
 int fpm_cast_bf16(const float* x, void* y, long n, void* stream);
 
+/* Selects the 256x256 bf16 GEMM tile schedule: 1 (default, or env FPM_GEMM_PHASE) = the
+ * phase-pipelined kernel, 0 = the two-stage kernel.  Both give bit-identical results; returns the
+ * previous setting.  Tuning / A-B switch only, no reference counterpart. */
+int fpm_set_gemm_phase(int on);
+
 /* ---- SplineConv message passing ---------------------------------------------------------------
  * Replaces PyG 1.6.3 SplineConv(768, 768, dim=2, kernel_size=5, aggr='max') inside SConv /
  * SiameseSConvOnNodes (src/model/spline_conv.py:17, 28-57).

@@ -306,6 +306,50 @@ def test_gemm_big_vs_torch(M, N, K, batch, epi, f32out, gather):
     assert ((out.float().cpu() - ref).abs().max() / ref.abs().max()) < tol
 
 
+@pytest.mark.parametrize("M,N,K,batch,epi,f32out,gather", [
+    (46080 + 37, 768, 768, 1, 0, False, True),   # SplineConv product shape: gathered rows, row tail
+    (40000, 512, 128, 1, 1, True, False),        # 2 K-tiles (shortest pipeline), ReLU, fp32 out
+    (33000, 1024, 192, 1, 0, False, False),      # 3 K-tiles
+    (256, 256, 256, 520, 3, True, False),        # batched affinity epilogue
+])
+def test_gemm_phase_bit_identical(M, N, K, batch, epi, f32out, gather):
+    """The phase-pipelined 256x256 kernel (gemm_phase.h) against the two-stage kernel: same
+    accumulation order, so bit-identical outputs; and both against torch."""
+    g = torch.Generator().manual_seed(M + K)
+    A = (torch.randn(batch, M + 17, K, generator=g) * 0.1).to(torch.bfloat16).to(DEV)
+    Bm = (torch.randn(batch, N, K, generator=g) * 0.1).to(torch.bfloat16).to(DEV)
+    bias = torch.randn(N, generator=g).to(DEV) if epi != 3 else None
+    rows = torch.randint(0, M + 17, (M,), generator=g).to(DEV).int() if gather else None
+    n1 = torch.randint(1, 257, (batch,), generator=g).int().to(DEV) if epi == 3 else None
+    n2 = torch.randint(1, 257, (batch,), generator=g).int().to(DEV) if epi == 3 else None
+    outs = []
+    for phase in (1, 0):
+        prev = ops.set_gemm_phase(phase)
+        try:
+            out = torch.full((batch, M, N), 3.0, device=DEV, dtype=torch.float32 if f32out else torch.bfloat16)
+            kw = dict(out_f=out) if f32out else dict(out_t=out)
+            ops.gemm(A, Bm, M, N, K, K, K, batch=batch, sA=(M + 17) * K, sB=N * K, sC=M * N, a_rows=rows,
+                     epi=epi, bias=bias, n1=n1, n2=n2, **kw)
+            torch.cuda.synchronize()
+        finally:
+            ops.set_gemm_phase(prev)
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1])
+    Af = A.float()[:, rows.long()] if gather else A.float()[:, :M]
+    ref = Af @ Bm.float().transpose(1, 2)
+    if bias is not None:
+        ref = ref + bias
+    if epi == 1:
+        ref = torch.relu(ref)
+    if epi == 3:
+        ref = torch.nn.functional.softplus(ref) - 0.5
+        r = torch.arange(M, device=DEV)[None, :, None] < n2[:, None, None]
+        c = torch.arange(N, device=DEV)[None, None, :] < n1[:, None, None]
+        ref = torch.where(r & c, ref, torch.zeros_like(ref))
+    tol = 2e-3 if f32out else 1e-2
+    assert ((outs[0].float() - ref).abs().max() / ref.abs().max()).item() < tol
+
+
 # ---------------------------------------------------------------------------------------- large n (C5)
 def test_sinkhorn_stream_vs_oracle():
     """n > 256: the L2-streaming Sinkhorn (dummy rows, transposed pair, strided views)."""

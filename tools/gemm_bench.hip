@@ -1,7 +1,7 @@
 // Micro-benchmark of the SplineConv product GEMM shapes: 128x128 register-staged kernel
 // (gemm_core.h) vs the 256x256 LDS-DMA kernel (gemm_big.h); checks the outputs are identical.
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I fingerprint-matching-code_amd/csrc tools/gemm_bench.hip
-#include "gemm_big.h"
+#include "gemm_phase.h"
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -19,7 +19,56 @@ using namespace fpm;
 
 static uint16_t h_f2bf(float f) { uint32_t u; memcpy(&u, &f, 4); u += 0x7FFF + ((u >> 16) & 1); return (uint16_t)(u >> 16); }
 
+// dense C[M][N] = A[M][K] . B[N][K]^T with both 256x256 kernels (no gather, no groups)
+static int dense(int M, int N, int K) {
+    std::mt19937 rng(2);
+    std::uniform_real_distribution<float> U(-1.f, 1.f);
+    std::vector<uint16_t> ha((size_t)M * K), hb((size_t)N * K);
+    for (auto& v : ha) v = h_f2bf(U(rng));
+    for (auto& v : hb) v = h_f2bf(U(rng));
+    uint16_t *da, *db, *c2, *c3;
+    CK(hipMalloc(&da, ha.size() * 2)); CK(hipMalloc(&db, hb.size() * 2));
+    CK(hipMalloc(&c2, (size_t)M * N * 2)); CK(hipMalloc(&c3, (size_t)M * N * 2));
+    CK(hipMemcpy(da, ha.data(), ha.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(db, hb.data(), hb.size() * 2, hipMemcpyHostToDevice));
+    GemmParams p = {};
+    p.A = da; p.lda = K; p.B = db; p.ldb = K; p.M = M; p.N = N; p.K = K; p.nseg = 1; p.epi = EPI_STORE; p.ldc = N;
+    p.remap_mtiles = (M + 255) / 256;
+    GemmParams p3 = p;
+    p.Ct = c2; p3.Ct = c3;
+    dim3 g(remap_grid256(N, p.remap_mtiles));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    const double flops = 2.0 * M * (double)N * K;
+    for (int round = 0; round < 3; ++round)
+        for (int v = 1; v < 3; ++v) {
+            CK(hipEventRecord(e0));
+            for (int r = 0; r < 10; ++r) {
+                if (v == 1) hipLaunchKernelGGL((gemm_big_kernel<256, EPI_STORE, false>), g, dim3(G2_THREADS), 0, 0, p);
+                else hipLaunchKernelGGL((gemm_phase_kernel<EPI_STORE, false>), g, dim3(G2_THREADS), 0, 0, p3);
+            }
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+            ms /= 10;
+            printf("dense %dx%dx%d round %d %-9s %.4f ms  %.1f TF/s\n", M, N, K, round, v == 2 ? "phase256" : "256x256", ms, flops / ms / 1e9);
+        }
+    std::vector<uint16_t> h2((size_t)M * N), h3((size_t)M * N);
+    CK(hipMemcpy(h2.data(), c2, h2.size() * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(h3.data(), c3, h3.size() * 2, hipMemcpyDeviceToHost));
+    size_t diff = 0;
+    for (size_t i = 0; i < h2.size(); ++i) diff += h2[i] != h3[i];
+    printf("dense mismatching elements: %zu of %zu\n", diff, h2.size());
+    CK(hipFree(da)); CK(hipFree(db)); CK(hipFree(c2)); CK(hipFree(c3));
+    return diff != 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc > 1 && !strcmp(argv[1], "dense")) {
+        int rc = 0;
+        for (int i = 2; i + 2 < argc + 0 && i + 2 <= argc - 1; i += 3) rc |= dense(atoi(argv[i]), atoi(argv[i + 1]), atoi(argv[i + 2]));
+        return rc;
+    }
     const int Nn = 32768, D = 768, NC = 26;
     std::mt19937 rng(1);
     std::uniform_real_distribution<float> U(-1.f, 1.f);
@@ -47,10 +96,10 @@ int main(int argc, char** argv) {
     };
     auto t128 = table(128), t256 = table(256);
     printf("rows %d  tiles128 %zu tiles256 %zu\n", rows, t128.size() / 2, t256.size() / 2);
-    uint16_t *dx, *dw, *c1, *c2;
+    uint16_t *dx, *dw, *c1, *c2, *c3;
     int *darows, *dgoff, *dt128, *dt256;
     CK(hipMalloc(&dx, hx.size() * 2)); CK(hipMalloc(&dw, hw.size() * 2));
-    CK(hipMalloc(&c1, (size_t)rows * D * 2)); CK(hipMalloc(&c2, (size_t)rows * D * 2));
+    CK(hipMalloc(&c1, (size_t)rows * D * 2)); CK(hipMalloc(&c2, (size_t)rows * D * 2)); CK(hipMalloc(&c3, (size_t)rows * D * 2));
     CK(hipMalloc(&darows, arows.size() * 4)); CK(hipMalloc(&dgoff, goff.size() * 4));
     CK(hipMalloc(&dt128, t128.size() * 4)); CK(hipMalloc(&dt256, t256.size() * 4));
     CK(hipMemcpy(dx, hx.data(), hx.size() * 2, hipMemcpyHostToDevice));
@@ -62,33 +111,36 @@ int main(int argc, char** argv) {
     GemmParams p = {};
     p.A = dx; p.lda = D; p.a_rows = darows; p.B = dw; p.ldb = D; p.sB_seg = (long)D * D;
     p.M = rows; p.N = D; p.K = D; p.nseg = 1; p.group_off = dgoff; p.epi = EPI_STORE; p.ldc = D;
-    GemmParams p1 = p, p2 = p;
+    GemmParams p1 = p, p2 = p, p3;
     p1.tile_info = dt128; p1.Ct = c1; p1.remap_mtiles = (int)t128.size() / 2;
     p2.tile_info = dt256; p2.Ct = c2; p2.remap_mtiles = (int)t256.size() / 2;
+    p3 = p2; p3.Ct = c3;
     dim3 g1(remap_grid(D, p1.remap_mtiles)), g2(remap_grid256(D, p2.remap_mtiles));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     const double flops = 2.0 * rows * (double)D * D;
     const int reps = 20;
     for (int round = 0; round < 3; ++round) {
-        for (int v = 0; v < 2; ++v) {
+        for (int v = 0; v < 3; ++v) {
             CK(hipEventRecord(e0));
             for (int r = 0; r < reps; ++r) {
                 if (v == 0) hipLaunchKernelGGL((gemm_kernel<bf16_t, false>), g1, dim3(GTHREADS), 0, 0, p1);
-                else hipLaunchKernelGGL((gemm_big_kernel<256, EPI_STORE, false>), g2, dim3(G2_THREADS), 0, 0, p2);
+                else if (v == 1) hipLaunchKernelGGL((gemm_big_kernel<256, EPI_STORE, false>), g2, dim3(G2_THREADS), 0, 0, p2);
+                else hipLaunchKernelGGL((gemm_phase_kernel<EPI_STORE, false>), g2, dim3(G2_THREADS), 0, 0, p3);
             }
             CK(hipEventRecord(e1));
             CK(hipEventSynchronize(e1));
             float ms; CK(hipEventElapsedTime(&ms, e0, e1));
             ms /= reps;
-            printf("round %d %-10s %.4f ms  %.1f TF/s\n", round, v ? "256x256" : "128x128", ms, flops / ms / 1e9);
+            printf("round %d %-10s %.4f ms  %.1f TF/s\n", round, v == 2 ? "phase256" : v ? "256x256" : "128x128", ms, flops / ms / 1e9);
         }
     }
-    std::vector<uint16_t> h1((size_t)rows * D), h2((size_t)rows * D);
+    std::vector<uint16_t> h1((size_t)rows * D), h2((size_t)rows * D), h3((size_t)rows * D);
     CK(hipMemcpy(h1.data(), c1, h1.size() * 2, hipMemcpyDeviceToHost));
     CK(hipMemcpy(h2.data(), c2, h2.size() * 2, hipMemcpyDeviceToHost));
-    size_t diff = 0;
-    for (size_t i = 0; i < h1.size(); ++i) diff += h1[i] != h2[i];
-    printf("mismatching elements: %zu of %zu\n", diff, h1.size());
-    return diff != 0;
+    CK(hipMemcpy(h3.data(), c3, h3.size() * 2, hipMemcpyDeviceToHost));
+    size_t diff = 0, diff3 = 0;
+    for (size_t i = 0; i < h1.size(); ++i) { diff += h1[i] != h2[i]; diff3 += h3[i] != h2[i]; }
+    printf("mismatching elements 128 vs 256: %zu, phase vs 256: %zu of %zu\n", diff, diff3, h1.size());
+    return diff != 0 || diff3 != 0;
 }
