@@ -3,6 +3,7 @@
 // affinity Kp (affinity_layer.py:15-18), AFA-U projections/FFN (afau.py:99-103,188-199).
 #include "gemm_phase.h"
 #include <cstdlib>
+#include <cstring>
 
 extern "C" int fpm_gemm(int dtype, const void* A, long lda, long sA, const int* a_rows, const void* B, long ldb,
                         long sB, int M, int N, int K, int batch, int epi, const float* bias, float* Cf, void* Ct,
@@ -70,9 +71,18 @@ int& gemm_phase_flag() {
 }
 }  // namespace fpm
 
-extern "C" int fpm_set_gemm_phase(int on) {
-    const int prev = fpm::gemm_phase_flag();
-    fpm::gemm_phase_flag() = on;
+int& gnn_packed_flag();
+
+extern "C" int fpm_set_tuning(const char* key, int value) {
+    int* f = nullptr;
+    if (key && !strcmp(key, "gemm_phase")) f = &fpm::gemm_phase_flag();
+    else if (key && !strcmp(key, "gnn_packed")) f = &gnn_packed_flag();
+    if (!f) {
+        fpm::set_error("fpm_set_tuning: unknown key '%s'", key ? key : "(null)");
+        return -1;
+    }
+    const int prev = *f;
+    *f = value;
     return prev;
 }
 

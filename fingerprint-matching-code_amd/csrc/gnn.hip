@@ -14,6 +14,7 @@
 // round-robin by linear id), so the pair's 17-channel slab (4.4 MB at n = 256) is re-read from
 // that XCD's L2 by the ~6 neighbour blocks instead of from the fabric.
 #include "fpm_common.h"
+#include <cstdlib>
 
 namespace {
 
@@ -27,15 +28,25 @@ __device__ __forceinline__ bool pair_block(int n2max, int B, int& b, int& d) {
 
 inline unsigned pair_grid(int n2max, int B) { return (unsigned)(((B + 7) / 8) * 8 * n2max); }
 
-// packed per-layer parameters (f32): Wl[16][C] bl[16] Wr[16][C] W1[16][C] b1[16] W2[16][16] b2[16] wc[16] bc
+// packed per-layer parameters (f32), weights TRANSPOSED so output channels o, o+1 are adjacent
+// (one 64-bit scalar operand of v_pk_fma_f32): WlT[C][16] bl[16] WrT[C][16] W1T[C][16] b1[16]
+// W2T[16 (m)][16 (o)] b2[16] wc[16] bc; every block offset is even (8-B aligned pairs)
 template <int C>
 struct GnnPack {
     static constexpr int Wl = 0, bl = Wl + 16 * C, Wr = bl + 16, W1 = Wr + 16 * C, b1 = W1 + 16 * C, W2 = b1 + 16,
                          b2 = W2 + 256, wc = b2 + 16, bc = wc + 16, total = bc + 1;
 };
 
-template <int C>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6, 8))) void gnn_layer_kernel(const float* __restrict__ X, int n1max, int n2max,
+typedef float f2_t __attribute__((ext_vector_type(2)));
+
+// acc += w * (v.lo, v.lo) (hi = false) or w * (v.hi, v.hi): one v_pk_fma_f32, w a scalar pair
+__device__ __forceinline__ void pk_fma_bcast(f2_t& acc, f2_t w, f2_t v, bool hi) {
+    if (hi) asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "s"(w), "v"(v));
+    else asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1]" : "+v"(acc) : "s"(w), "v"(v));
+}
+
+template <int C, bool PACKED>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(PACKED ? 5 : 6, 8))) void gnn_layer_kernel(const float* __restrict__ X, int n1max, int n2max,
                                                          const int* __restrict__ ptr1, const int* __restrict__ nbr1,
                                                          const int* __restrict__ ptr2, const int* __restrict__ nbr2,
                                                          const int* __restrict__ n1, const int* __restrict__ n2,
@@ -45,9 +56,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6, 8))) vo
     // one thread per graph-1 node i (blockDim >= n1max): no loop, so the uniform weight loads
     // stay scalar (s_load, SGPR operands of the FMAs) instead of being hoisted into VGPRs.
     using P = GnnPack<C>;
-    extern __shared__ float T[];          // [C][n1max]: sum of graph-2 neighbour rows
+    // T[a][TS]: sum of graph-2 neighbour rows, node-major with 80-B rows (C = 17) so phase 2
+    // reads a neighbour's 17 channels with 4 ds_read_b128 + 1 ds_read_b32
+    constexpr int TS = C == 1 ? 1 : 20;
+    extern __shared__ __attribute__((aligned(16))) float T[];
     __shared__ int nb2[64];
-    __shared__ int nnb2;
+    __shared__ int nnb2, beg2;
 
     int d, b;
     if (!pair_block(n2max, B, b, d)) return;
@@ -55,11 +69,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6, 8))) vo
     const long N = (long)n1max * n2max;
     const float* Xb = X + (long)b * C * N;
     if (i == 0) {
-        int beg = ptr2[(long)b * n2max + d], end = ptr2[(long)b * n2max + d + 1];
-        int n = end - beg;
-        if (n > 64) n = 64;   // Delaunay in-degree is far below 64; guarded
-        nnb2 = n;
-        for (int k = 0; k < n; ++k) nb2[k] = nbr2[beg + k];
+        const int beg = ptr2[(long)b * n2max + d], end = ptr2[(long)b * n2max + d + 1];
+        nnb2 = end - beg;
+        beg2 = beg;
+        for (int k = 0; k < end - beg && k < 64; ++k) nb2[k] = nbr2[beg + k];
     }
     __syncthreads();
     const int nn2 = nnb2;
@@ -68,16 +81,27 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6, 8))) vo
         float acc[C];
 #pragma unroll
         for (int c = 0; c < C; ++c) acc[c] = 0.f;
-        for (int k = 0; k < nn2; ++k) {
-            const float* row = Xb + (long)nb2[k] * n1max + i;
+        auto add_row = [&](int nb) {
+            const float* row = Xb + (long)nb * n1max + i;
             float v[C];
 #pragma unroll
             for (int c = 0; c < C; ++c) v[c] = row[(long)c * N];
 #pragma unroll
             for (int c = 0; c < C; ++c) acc[c] += v[c];
-        }
+        };
+        const int nl = nn2 < 64 ? nn2 : 64;
+        for (int k = 0; k < nl; ++k) add_row(nb2[k]);                  // LDS copy of the first 64
+        for (int k = 64; k < nn2; ++k) add_row(nbr2[beg2 + k]);
+
+        float* Ti = T + i * TS;
+        if constexpr (C == 17) {
 #pragma unroll
-        for (int c = 0; c < C; ++c) T[c * n1max + i] = acc[c];
+            for (int q = 0; q < 4; ++q)
+                *(float4*)(Ti + 4 * q) = make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
+            Ti[16] = acc[16];
+        } else {
+            Ti[0] = acc[0];
+        }
     }
     __syncthreads();
     if (i >= n1max) return;
@@ -92,9 +116,20 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6, 8))) vo
         agg[c] = 0.f;
     }
     for (int e = beg; e < end; ++e) {
-        const int a = nbr1[e];
+        const float* Ta = T + nbr1[e] * TS;
+        if constexpr (C == 17) {
 #pragma unroll
-        for (int c = 0; c < C; ++c) agg[c] += T[c * n1max + a];
+            for (int q = 0; q < 4; ++q) {
+                const float4 t4 = *(const float4*)(Ta + 4 * q);
+                agg[4 * q] += t4.x;
+                agg[4 * q + 1] += t4.y;
+                agg[4 * q + 2] += t4.z;
+                agg[4 * q + 3] += t4.w;
+            }
+            agg[16] += Ta[16];
+        } else {
+            agg[0] += Ta[0];
+        }
     }
     const float cnt = (float)((end - beg) * nn2 + (self ? 1 : 0));
 #pragma unroll
@@ -102,30 +137,79 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6, 8))) vo
         float v = self ? agg[c] + x[c] : agg[c];
         agg[c] = cnt > 0.f ? v / cnt : 0.f;
     }
-    float h[16];
+    if (!PACKED) {
+        float h[16];
 #pragma unroll
-    for (int m = 0; m < 16; ++m) {
-        float s = W[P::b1 + m];
+        for (int m = 0; m < 16; ++m) {
+            float s = W[P::b1 + m];
 #pragma unroll
-        for (int c = 0; c < C; ++c) s += W[P::W1 + m * C + c] * x[c];
-        h[m] = fmaxf(s, 0.f);
+            for (int c = 0; c < C; ++c) s += W[P::W1 + c * 16 + m] * x[c];
+            h[m] = fmaxf(s, 0.f);
+        }
+        float z = 0.f, vp = 0.f;
+        float* Xob = Xo + (long)b * 17 * N + p;
+#pragma unroll
+        for (int o = 0; o < 16; ++o) {
+            float l = 0.f, r = 0.f, t = 0.f;
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                l += W[P::Wl + c * 16 + o] * agg[c];
+                r += W[P::Wr + c * 16 + o] * x[c];
+            }
+#pragma unroll
+            for (int m = 0; m < 16; ++m) t += W[P::W2 + m * 16 + o] * h[m];
+            float x1 = ((l + W[P::bl + o]) + r) + fmaxf(t + W[P::b2 + o], 0.f);
+            if (vpart) vp = fmaf(cls_w[o], x1, vp);      // last layer: only w[0:16] . x1 is consumed
+            else Xob[(long)o * N] = x1;
+            z += W[P::wc + o] * x1;
+        }
+        if (vpart) vpart[(long)b * N + p] = vp;
+        zbuf[(long)b * N + p] = z + W[P::bc];
+        return;
+    }
+    // packed: output channels in pairs (o, o+1) on v_pk_fma_f32 -- the same fma chain per channel
+    // as the scalar path (bit-identical), half the VALU instructions.  The weight pair is one
+    // 64-bit scalar operand; the input value is broadcast from one half of a VGPR pair by op_sel.
+    constexpr int CP = (C + 1) / 2;
+    f2_t x2[CP], a2[CP];
+#pragma unroll
+    for (int k = 0; k < CP; ++k) {
+        x2[k] = (f2_t){x[2 * k], 2 * k + 1 < C ? x[2 * k + 1] : 0.f};
+        a2[k] = (f2_t){agg[2 * k], 2 * k + 1 < C ? agg[2 * k + 1] : 0.f};
+    }
+    const f2_t* W2p = (const f2_t*)W;                     // pair view (all block offsets even)
+    f2_t h[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        f2_t s = W2p[(P::b1 >> 1) + m];
+#pragma unroll
+        for (int c = 0; c < C; ++c) pk_fma_bcast(s, W2p[((P::W1 + c * 16) >> 1) + m], x2[c >> 1], c & 1);
+        h[m] = (f2_t){fmaxf(s.x, 0.f), fmaxf(s.y, 0.f)};
     }
     float z = 0.f, vp = 0.f;
     float* Xob = Xo + (long)b * 17 * N + p;
 #pragma unroll
-    for (int o = 0; o < 16; ++o) {
-        float l = 0.f, r = 0.f, t = 0.f;
+    for (int op = 0; op < 8; ++op) {
+        const int o = 2 * op;
+        f2_t l = {0.f, 0.f}, r = {0.f, 0.f}, t = {0.f, 0.f};
 #pragma unroll
         for (int c = 0; c < C; ++c) {
-            l += W[P::Wl + o * C + c] * agg[c];
-            r += W[P::Wr + o * C + c] * x[c];
+            pk_fma_bcast(l, W2p[((P::Wl + c * 16) >> 1) + op], a2[c >> 1], c & 1);
+            pk_fma_bcast(r, W2p[((P::Wr + c * 16) >> 1) + op], x2[c >> 1], c & 1);
         }
 #pragma unroll
-        for (int m = 0; m < 16; ++m) t += W[P::W2 + o * 16 + m] * h[m];
-        float x1 = ((l + W[P::bl + o]) + r) + fmaxf(t + W[P::b2 + o], 0.f);
-        if (vpart) vp = fmaf(cls_w[o], x1, vp);      // last layer: only w[0:16] . x1 is consumed
-        else Xob[(long)o * N] = x1;
-        z += W[P::wc + o] * x1;
+        for (int m = 0; m < 16; ++m) pk_fma_bcast(t, W2p[((P::W2 + m * 16) >> 1) + op], h[m >> 1], m & 1);
+        const f2_t tb = t + W2p[(P::b2 >> 1) + op];
+        const f2_t x1 = ((l + W2p[(P::bl >> 1) + op]) + r) + (f2_t){fmaxf(tb.x, 0.f), fmaxf(tb.y, 0.f)};
+        if (vpart) {
+            vp = fmaf(cls_w[o], x1.x, vp);
+            vp = fmaf(cls_w[o + 1], x1.y, vp);
+        } else {
+            Xob[(long)o * N] = x1.x;
+            Xob[(long)(o + 1) * N] = x1.y;
+        }
+        z = fmaf(W[P::wc + o], x1.x, z);
+        z = fmaf(W[P::wc + o + 1], x1.y, z);
     }
     if (vpart) vpart[(long)b * N + p] = vp;
     zbuf[(long)b * N + p] = z + W[P::bc];
@@ -156,6 +240,16 @@ __global__ __launch_bounds__(256) void node_classifier_kernel(const float* __res
 
 }  // namespace
 
+// MLP on packed fp32 FMAs (default) or scalar FMAs (bit-identical); env FPM_GNN_PACKED or
+// fpm_set_tuning("gnn_packed", v)
+int& gnn_packed_flag() {
+    static int on = [] {
+        const char* e = getenv("FPM_GNN_PACKED");
+        return e ? atoi(e) : 1;
+    }();
+    return on;
+}
+
 extern "C" int fpm_kron_gnn_layer_fwd(const float* X, int C, int B, int n1max, int n2max, const int* ptr1,
                                       const int* nbr1, const int* ptr2, const int* nbr2, const int* n1, const int* n2,
                                       const float* params, float* Xout, float* zbuf, float* vpart, const float* cls_w,
@@ -166,14 +260,20 @@ extern "C" int fpm_kron_gnn_layer_fwd(const float* X, int C, int B, int n1max, i
     FPM_CHECK_ARG(n1max <= 1024, "gnn_layer: n1max must be <= 1024");
     dim3 grid(pair_grid(n2max, B));
     hipStream_t st = (hipStream_t)stream;
-    const size_t sh = (size_t)C * n1max * 4;
+    const size_t sh = (size_t)(C == 1 ? 1 : 20) * n1max * 4;
     const int threads = (n1max + 63) / 64 * 64;
-    if (C == 1)
-        hipLaunchKernelGGL((gnn_layer_kernel<1>), grid, dim3(threads), sh, st, X, n1max, n2max, ptr1, nbr1, ptr2, nbr2,
-                           n1, n2, params, Xout, zbuf, vpart, cls_w, B);
-    else
-        hipLaunchKernelGGL((gnn_layer_kernel<17>), grid, dim3(threads), sh, st, X, n1max, n2max, ptr1, nbr1, ptr2, nbr2,
-                           n1, n2, params, Xout, zbuf, vpart, cls_w, B);
+    const bool packed = gnn_packed_flag() != 0;
+#define FPM_GNN(C_, P_)                                                                                          \
+    do {                                                                                                         \
+        if (sh > 65536)                                                                                          \
+            (void)hipFuncSetAttribute((const void*)gnn_layer_kernel<C_, P_>,                                     \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);                      \
+        hipLaunchKernelGGL((gnn_layer_kernel<C_, P_>), grid, dim3(threads), sh, st, X, n1max, n2max, ptr1, nbr1,  \
+                           ptr2, nbr2, n1, n2, params, Xout, zbuf, vpart, cls_w, B);                             \
+    } while (0)
+    if (C == 1) { if (packed) FPM_GNN(1, true); else FPM_GNN(1, false); }
+    else { if (packed) FPM_GNN(17, true); else FPM_GNN(17, false); }
+#undef FPM_GNN
     return fpm::check_launch("fpm_kron_gnn_layer_fwd");
 }
 

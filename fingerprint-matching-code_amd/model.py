@@ -108,9 +108,10 @@ class Net(nn.Module):
         d["eaff_b"] = g("edge_affinity.A.bias")
         for l in range(C.GNN_LAYER):
             pre = "gnn_layer_%d" % l
-            parts = [sd[pre + ".conv2.lin_l.weight"], sd[pre + ".conv2.lin_l.bias"], sd[pre + ".conv2.lin_r.weight"],
-                     sd[pre + ".n_self_func.0.weight"], sd[pre + ".n_self_func.0.bias"],
-                     sd[pre + ".n_self_func.2.weight"], sd[pre + ".n_self_func.2.bias"],
+            # kernel layout (gnn.hip GnnPack): weight matrices transposed to [in][out]
+            parts = [sd[pre + ".conv2.lin_l.weight"].t(), sd[pre + ".conv2.lin_l.bias"], sd[pre + ".conv2.lin_r.weight"].t(),
+                     sd[pre + ".n_self_func.0.weight"].t(), sd[pre + ".n_self_func.0.bias"],
+                     sd[pre + ".n_self_func.2.weight"].t(), sd[pre + ".n_self_func.2.bias"],
                      sd[pre + ".classifier.weight"], sd[pre + ".classifier.bias"]]
             d["gnn%d" % l] = torch.cat([t.reshape(-1).float() for t in parts]).to(device).contiguous()
         d["cls_w"] = g("classifier.weight").reshape(-1).contiguous()

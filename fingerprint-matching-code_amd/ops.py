@@ -79,10 +79,13 @@ def topk_select(ds, assign, k, lsa_out=None, out=None):
     return perm
 
 
-def set_gemm_phase(on):
-    """Select the 256x256 bf16 GEMM schedule (1: phase-pipelined, 0: two-stage; bit-identical).
-    Returns the previous setting."""
-    return int(_lib.load().fpm_set_gemm_phase(int(on)))
+def set_tuning(key, value):
+    """Kernel-variant switch (fpm_set_tuning: "gemm_phase", "gnn_packed"; all variants are
+    bit-identical).  Returns the previous value."""
+    prev = int(_lib.load().fpm_set_tuning(key.encode(), int(value)))
+    if prev < 0:
+        raise _lib.FpmError(_lib.load().fpm_last_error().decode(errors="replace"))
+    return prev
 
 
 def gemm(A, B, M, N, K, lda, ldb, batch=1, sA=0, sB=0, a_rows=None, epi=EPI_STORE, bias=None, out_f=None,

@@ -62,10 +62,12 @@ int fpm_gemm(int dtype, const void* A, long lda, long sA, const int* a_rows, con
              const int* n1, const int* n2, void* stream);
 int fpm_cast_bf16(const float* x, void* y, long n, void* stream);
 
-/* Selects the 256x256 bf16 GEMM tile schedule: 1 (default, or env FPM_GEMM_PHASE) = the
- * phase-pipelined kernel, 0 = the two-stage kernel.  Both give bit-identical results; returns the
- * previous setting.  Tuning / A-B switch only, no reference counterpart. */
-int fpm_set_gemm_phase(int on);
+/* Kernel-variant switches for A/B timing; every variant gives bit-identical results.  Returns the
+ * previous value, or -1 (error channel set) for an unknown key.  No reference counterpart.
+ *   "gemm_phase" (env FPM_GEMM_PHASE, default 1): 256x256 bf16 GEMM tiles on the phase-pipelined
+ *                kernel (1) or the two-stage kernel (0)
+ *   "gnn_packed" (env FPM_GNN_PACKED, default 1): GNN-layer MLPs on packed (1) or scalar (0) FMAs */
+int fpm_set_tuning(const char* key, int value);
 
 /* ---- SplineConv message passing ---------------------------------------------------------------
  * Replaces PyG 1.6.3 SplineConv(768, 768, dim=2, kernel_size=5, aggr='max') inside SConv /
@@ -104,7 +106,10 @@ int fpm_edge_diff_padded(const float* x, const int* src, const int* dst, const i
  * X: (B, C, n2max, n1max) with C in {1, 17}; Xout channels 0..15 and zbuf (B, n2max, n1max)
  * are written; the caller runs fpm_sinkhorn_log_fwd(zbuf -> Xout channel 16).  Last layer: pass
  * vpart (B, n2max, n1max) and the final classifier weights cls_w (17): vpart = cls_w[0:16] . x1
- * is written instead of Xout channels 0..15 (fpm_node_classifier then reads vpart + channel 16). */
+ * is written instead of Xout channels 0..15 (fpm_node_classifier then reads vpart + channel 16).
+ * params: fpm_gnn_param_count(C) floats = lin_l.weight^T [C][16], lin_l.bias [16],
+ * lin_r.weight^T [C][16], n_self_func.0.weight^T [C][16], n_self_func.0.bias [16],
+ * n_self_func.2.weight^T [16][16], n_self_func.2.bias [16], classifier.weight [16], classifier.bias. */
 int fpm_kron_gnn_layer_fwd(const float* X, int C, int B, int n1max, int n2max, const int* ptr1, const int* nbr1,
                            const int* ptr2, const int* nbr2, const int* n1, const int* n2, const float* params,
                            float* Xout, float* zbuf, float* vpart, const float* cls_w, void* stream);

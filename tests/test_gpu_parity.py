@@ -279,6 +279,51 @@ def test_gconv_golden():
     assert (y2 - ref).abs().max() < 1e-5
 
 
+@pytest.mark.parametrize("C,layer", [(1, 0), (17, 1)])
+def test_gnn_layer_vs_oracle(sd, C, layer):
+    """Kronecker GNN layer (gnn.hip) on a ragged batch: x1 (Xout channels 0..15) and the
+    classifier logit z against the oracle's factorised aggregation + MLPs; the packed-FMA and
+    scalar-FMA MLPs bit-identical."""
+    import torch.nn.functional as F
+    from fpm import synth
+    n1s, n2s = [40, 33, 25], [40, 38, 20]
+    B, nm = 3, 40
+    pairs = synth.make_batch(11, B, n1s, n2s)
+    bt = DeviceBatch.from_pairs(pairs, DEV)
+    plans = [ops.spline_plan(bt.src[s], bt.dst[s], bt.pseudo[s], B * nm, nm) for s in range(2)]
+    csr = [ops.plan_csr(plans[s], bt.E[s], B * nm) for s in range(2)]
+    net = fpm.Net(regression=True, dtype="f32", seed=7)
+    wp = net.packed(DEV)
+    g = torch.Generator().manual_seed(C)
+    X = torch.randn(B, C, nm, nm, generator=g)                 # [b][c][j (graph 2)][i (graph 1)]
+    outs = []
+    for packed in (1, 0):
+        prev = ops.set_tuning("gnn_packed", packed)
+        try:
+            Xn = torch.full((B, 17, nm, nm), 5.0, device=DEV)
+            z = torch.full((B, nm, nm), 5.0, device=DEV)
+            ops.gnn_layer(X.to(DEV), C, B, nm, nm, csr[0], csr[1], bt.n1, bt.n2, wp["gnn%d" % layer], Xn, z)
+            torch.cuda.synchronize()
+        finally:
+            ops.set_tuning("gnn_packed", prev)
+        outs.append((Xn.cpu(), z.cpu()))
+    assert torch.equal(outs[0][0][:, :16], outs[1][0][:, :16]) and torch.equal(outs[0][1], outs[1][1])
+    Xn, z = outs[0]
+    pre = "gnn_layer_%d" % layer
+    w = lambda k: sd[pre + k].float()
+    for b in range(B):
+        ei1 = torch.as_tensor(pairs[b][0]["edge_index"])
+        ei2 = torch.as_tensor(pairs[b][1]["edge_index"])
+        x = X[b].reshape(C, nm * nm).t()                       # p = j * nm + i
+        agg = O.pattern_mean_factorized(x, ei1, ei2, nm, nm, n1s[b], n2s[b])
+        x1 = F.linear(agg, w(".conv2.lin_l.weight"), w(".conv2.lin_l.bias")) + F.linear(x, w(".conv2.lin_r.weight"))
+        h = F.relu(F.linear(x, w(".n_self_func.0.weight"), w(".n_self_func.0.bias")))
+        x1 = x1 + F.relu(F.linear(h, w(".n_self_func.2.weight"), w(".n_self_func.2.bias")))
+        zr = F.linear(x1, w(".classifier.weight"), w(".classifier.bias"))[:, 0]
+        assert (Xn[b, :16].reshape(16, -1).t() - x1).abs().max() < 1e-4
+        assert (z[b].reshape(-1) - zr).abs().max() < 1e-4
+
+
 @pytest.mark.parametrize("M,N,K,batch,epi,f32out,gather", [
     (1000, 600, 256, 1, 1, True, False),      # AFA-U W2 / Wc shape: N tail, 256x128 tiles
     (1000, 256, 640, 1, 1, False, False),     # FFN W1 (zero-padded K), bf16 out
@@ -324,7 +369,7 @@ def test_gemm_phase_bit_identical(M, N, K, batch, epi, f32out, gather):
     n2 = torch.randint(1, 257, (batch,), generator=g).int().to(DEV) if epi == 3 else None
     outs = []
     for phase in (1, 0):
-        prev = ops.set_gemm_phase(phase)
+        prev = ops.set_tuning("gemm_phase", phase)
         try:
             out = torch.full((batch, M, N), 3.0, device=DEV, dtype=torch.float32 if f32out else torch.bfloat16)
             kw = dict(out_f=out) if f32out else dict(out_t=out)
@@ -332,7 +377,7 @@ def test_gemm_phase_bit_identical(M, N, K, batch, epi, f32out, gather):
                      epi=epi, bias=bias, n1=n1, n2=n2, **kw)
             torch.cuda.synchronize()
         finally:
-            ops.set_gemm_phase(prev)
+            ops.set_tuning("gemm_phase", prev)
         outs.append(out)
     assert torch.equal(outs[0], outs[1])
     Af = A.float()[:, rows.long()] if gather else A.float()[:, :M]
