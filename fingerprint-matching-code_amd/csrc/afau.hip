@@ -12,10 +12,34 @@
 
 namespace {
 
-// one workgroup per (pair, 16-row tile); 4 waves x 4 rows; heads looped.  The tile's costs stay
-// in registers across the 16 heads (lane j-slots: j = lane + 64 jj, jj < NJ); scores stay in
-// registers through max / exp / sum, and only the normalised probabilities go to LDS for AV.
-template <typename T, int NJ>
+// Row-block cross-set attention: one workgroup per (pair, 16-row tile), 4 waves; wave wv owns the
+// column quarter j in [wv*4*TJ, (wv+1)*4*TJ) of all 16 rows, lane l row l&15 and the columns
+// j = base + 4t + (l>>4), t < TJ -- exactly the operand layout of the fp32 MFMA 16x16x4, so the
+// softmax numerators feed P . V straight from registers.  The tile's costs stay in registers
+// across the 16 heads; V comes from global (L2-resident Wv), prefetched one head ahead.
+//
+// Scores: with q = 0 the mixed score is a scalar function of the cost,
+//   f_h(c) = sum_m w2[m] relu(w1[m] c + b1[m]) + b2,
+// piecewise linear with <= 16 breakpoints t_m = -b1[m] / w1[m].  At start the block builds in LDS,
+// for all 16 heads, the sorted breakpoints, the 17 segments' (A, B) with f = A + B c, and a
+// 64-bucket table over c in [0, 1] (the Sinkhorn output's range): the segment at the bucket's left
+// edge and the <= 4 breakpoints inside it.  A score is one bucket lookup, four compares and one
+// fma instead of 48 VALU operations; costs outside [0, 1] and buckets with 5+ breakpoints take the
+// 16-term sum.  (Rounding differs from the 16-term sum by O(ulp) of the terms.)
+// Softmax per wave quarter with its own running max (flash-style); the four quarters' (max, sum,
+// partial P.V) are merged through LDS, one barrier per head (double-buffered partials).
+constexpr int AF_NB = 64;      // score-LUT buckets over [0, 1]
+
+struct AfSmem {
+    int lseg[16][AF_NB];
+    float4 lbp[16][AF_NB];
+    float segA[16][17], segB[16][17];
+    float part[2][4][256];     // [buffer][wave][row * 16 + d]
+    float2 rowms[2][4][16];    // [buffer][wave][row] (running max, sum)
+    float traw[256], tsort[256];
+};
+
+template <typename T, int TJ>
 __global__ __launch_bounds__(256) void afau_row_attn_kernel(const float* __restrict__ cost, long c_sb, long c_ld,
                                                             int n1max, int n2max, const int* __restrict__ n2,
                                                             const float* __restrict__ Wv, int emb,
@@ -23,96 +47,144 @@ __global__ __launch_bounds__(256) void afau_row_attn_kernel(const float* __restr
                                                             const float* __restrict__ mix1b,
                                                             const float* __restrict__ mix2w,
                                                             const float* __restrict__ mix2b, T* __restrict__ out) {
-    constexpr int VS = 20;                // V row stride (floats): float4-aligned, spreads the LDS banks
-    extern __shared__ float sh[];
-    float* V = sh;                        // [n2max][VS]
-    float* Pm = sh + n2max * VS;          // [16 rows][n2max]
+    typedef float f32x4_t __attribute__((ext_vector_type(4)));
+    __shared__ AfSmem S;
     const int b = blockIdx.x, i0 = blockIdx.y * 16, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int n2b = n2[b];
-    const float* Cb = cost + (long)b * c_sb;
-    float creg[4][NJ];
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-        const int i = i0 + wv * 4 + rr;
-#pragma unroll
-        for (int jj = 0; jj < NJ; ++jj) {
-            const int j = lane + 64 * jj;
-            creg[rr][jj] = (i < n1max && j < n2max) ? Cb[(long)i * c_ld + j] : 0.f;
+
+    // ---- score LUTs of the 16 heads
+    {
+        const int hh = tid >> 4, m = tid & 15;
+        const float w = mix1w[(hh * 2 + 1) * 16 + m];
+        S.traw[tid] = w != 0.f ? -mix1b[hh * 16 + m] / w : INFINITY;
+    }
+    __syncthreads();
+    {
+        const int hh = tid >> 4, m = tid & 15;
+        const float t = S.traw[tid];
+        int r = 0;
+        for (int k = 0; k < 16; ++k) {
+            const float u = S.traw[hh * 16 + k];
+            r += (u < t) || (u == t && k < m);
         }
+        S.tsort[hh * 16 + r] = t;
+    }
+    __syncthreads();
+    for (int k = tid; k < 16 * 17; k += 256) {            // segment sg of head hh: (tsort[sg-1], tsort[sg])
+        const int hh = k / 17, sg = k - 17 * hh;
+        const float lo = sg == 0 ? -INFINITY : S.tsort[hh * 16 + sg - 1];
+        const float hi = sg == 16 ? INFINITY : S.tsort[hh * 16 + sg];
+        const bool flo = lo > -INFINITY && lo < INFINITY, fhi = hi > -INFINITY && hi < INFINITY;
+        const float rep = (flo && fhi) ? 0.5f * (lo + hi) : flo ? lo + 1.f : fhi ? hi - 1.f : 0.f;
+        float A = mix2b[hh], Bc = 0.f;
+        for (int m = 0; m < 16; ++m) {
+            const float w = mix1w[(hh * 2 + 1) * 16 + m], bb = mix1b[hh * 16 + m], w2 = mix2w[hh * 16 + m];
+            const bool act = w != 0.f ? (w * rep + bb > 0.f) : (bb > 0.f);
+            if (act) {
+                A = fmaf(w2, bb, A);
+                Bc = fmaf(w2, w, Bc);
+            }
+        }
+        S.segA[hh][sg] = A;
+        S.segB[hh][sg] = Bc;
+    }
+#pragma unroll
+    for (int q = 0; q < 16 * AF_NB / 256; ++q) {          // bucket bk of head hh
+        const int k = tid + 256 * q, hh = k / AF_NB, bk = k % AF_NB;
+        const float lo = (float)bk / AF_NB, hi = (float)(bk + 1) / AF_NB;
+        int s0 = 0, nin = 0;
+        float bp[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
+        for (int m = 0; m < 16; ++m) {
+            const float t = S.tsort[hh * 16 + m];
+            s0 += t < lo;
+            if (t >= lo && t < hi) {
+                if (nin < 4) bp[nin] = t;
+                ++nin;
+            }
+        }
+        S.lseg[hh][bk] = nin > 4 ? -1 : s0;
+        S.lbp[hh][bk] = make_float4(bp[0], bp[1], bp[2], bp[3]);
+    }
+    __syncthreads();
+
+    // ---- costs and the first head's V (B operand: V[j][d], d = lane & 15)
+    const int r = lane & 15, i = i0 + r, jbase = wv * 4 * TJ + (lane >> 4);
+    const float* Cb = cost + (long)b * c_sb + (long)i * c_ld;
+    float creg[TJ], vreg[TJ];
+#pragma unroll
+    for (int t = 0; t < TJ; ++t) {
+        const int j = jbase + 4 * t;
+        creg[t] = (i < n1max && j < n2max) ? Cb[j] : 0.f;
+        vreg[t] = j < n2b ? Wv[(long)r * emb + j] : 0.f;
     }
     for (int h = 0; h < 16; ++h) {
+        float p[TJ];
+        float mloc = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < TJ; ++t) {
+            const float c = creg[t];
+            float sc;
+            int s0 = -1;
+            float4 bp;
+            if (c >= 0.f && c <= 1.f) {
+                const int bk = min((int)(c * AF_NB), AF_NB - 1);
+                s0 = S.lseg[h][bk];
+                bp = S.lbp[h][bk];
+            }
+            if (s0 >= 0) {
+                const int sg = s0 + (bp.x < c) + (bp.y < c) + (bp.z < c) + (bp.w < c);
+                sc = fmaf(S.segB[h][sg], c, S.segA[h][sg]);
+            } else {
+                sc = 0.f;
+#pragma unroll 1
+                for (int m = 0; m < 16; ++m)
+                    sc += fmaxf(c * mix1w[(h * 2 + 1) * 16 + m] + mix1b[h * 16 + m], 0.f) * mix2w[h * 16 + m];
+                sc += mix2b[h];
+            }
+            p[t] = sc;
+            if (jbase + 4 * t < n2max) mloc = fmaxf(mloc, sc);
+        }
+        mloc = fmaxf(mloc, __shfl_xor(mloc, 16));
+        mloc = fmaxf(mloc, __shfl_xor(mloc, 32));
+        float sloc = 0.f;
+#pragma unroll
+        for (int t = 0; t < TJ; ++t) {
+            const float e = jbase + 4 * t < n2max ? fpm::fast_exp2((p[t] - mloc) * fpm::LOG2E_F) : 0.f;
+            p[t] = e;
+            sloc += e;
+        }
+        sloc += __shfl_xor(sloc, 16);
+        sloc += __shfl_xor(sloc, 32);
+        // unnormalised P . V over this wave's columns
+        f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < TJ; ++t) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(p[t], vreg[t], acc, 0, 0, 0);
+        if (h + 1 < 16) {                                 // next head's V
+#pragma unroll
+            for (int t = 0; t < TJ; ++t) {
+                const int j = jbase + 4 * t;
+                vreg[t] = j < n2b ? Wv[(long)((h + 1) * 16 + r) * emb + j] : 0.f;
+            }
+        }
+        const int buf = h & 1;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) S.part[buf][wv][(4 * (lane >> 4) + k) * 16 + r] = acc[k];
+        if (lane < 16) S.rowms[buf][wv][lane] = make_float2(mloc, sloc);
         __syncthreads();
-        for (int k = tid; k < n2max * 16; k += 256) {      // coalesced along j
-            const int dd = k / n2max, j = k - dd * n2max;
-            V[j * VS + dd] = j < n2b ? Wv[(long)(h * 16 + dd) * emb + j] : 0.f;
-        }
-        float w1[16], b1[16], w2[16];
-#pragma unroll
-        for (int m = 0; m < 16; ++m) {
-            w1[m] = mix1w[(h * 2 + 1) * 16 + m];
-            b1[m] = mix1b[h * 16 + m];
-            w2[m] = mix2w[h * 16 + m];
-        }
-        const float b2 = mix2b[h];
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-            const int lr = wv * 4 + rr, i = i0 + lr;
-            if (i >= n1max) break;
-            float sv[NJ];
-            float mx = -INFINITY;
-#pragma unroll
-            for (int jj = 0; jj < NJ; ++jj) {
-                const float c = creg[rr][jj];
-                float sc = 0.f;
-#pragma unroll
-                for (int m = 0; m < 16; ++m) sc += fmaxf(c * w1[m] + b1[m], 0.f) * w2[m];
-                sc += b2;
-                sv[jj] = sc;
-                if (lane + 64 * jj < n2max) mx = fmaxf(mx, sc);
-            }
-            mx = fpm::warp_max(mx);
-            float sum = 0.f;
-#pragma unroll
-            for (int jj = 0; jj < NJ; ++jj) {
-                const float e = fpm::fast_exp2((sv[jj] - mx) * fpm::LOG2E_F);
-                sv[jj] = e;
-                if (lane + 64 * jj < n2max) sum += e;
-            }
-            sum = fpm::warp_sum(sum);
-            const float inv = 1.f / sum;
-#pragma unroll
-            for (int jj = 0; jj < NJ; ++jj) {
-                const int j = lane + 64 * jj;
-                if (j < n2max) Pm[lr * n2max + j] = sv[jj] * inv;
-            }
-        }
-        __syncthreads();
-        // out[i][h*16 + d] for the 16 rows: thread = (row, 4 d's, j residue mod 4), float4 V reads
         {
-            const int lr = tid >> 4, dq = (tid >> 2) & 3, jp = tid & 3, i = i0 + lr;
-            float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-            for (int j = jp; j < n2max; j += 4) {
-                const float pj = Pm[lr * n2max + j];
-                const float4 v = *(const float4*)(V + j * VS + dq * 4);
-                acc.x = fmaf(pj, v.x, acc.x);
-                acc.y = fmaf(pj, v.y, acc.y);
-                acc.z = fmaf(pj, v.z, acc.z);
-                acc.w = fmaf(pj, v.w, acc.w);
-            }
+            const int rr = tid >> 4, d = tid & 15, ii = i0 + rr;
+            float M = -INFINITY;
 #pragma unroll
-            for (int o = 1; o <= 2; o <<= 1) {
-                acc.x += __shfl_xor(acc.x, o);
-                acc.y += __shfl_xor(acc.y, o);
-                acc.z += __shfl_xor(acc.z, o);
-                acc.w += __shfl_xor(acc.w, o);
+            for (int w = 0; w < 4; ++w) M = fmaxf(M, S.rowms[buf][w][rr].x);
+            float o = 0.f, sum = 0.f;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const float2 ms = S.rowms[buf][w][rr];
+                const float sc = fpm::fast_exp2((ms.x - M) * fpm::LOG2E_F);
+                sum = fmaf(ms.y, sc, sum);
+                o = fmaf(S.part[buf][w][tid], sc, o);
             }
-            if (i < n1max && jp == 0) {
-                T* o = out + ((long)b * n1max + i) * 256 + h * 16 + dq * 4;
-                o[0] = fpm::from_f<T>(acc.x);
-                o[1] = fpm::from_f<T>(acc.y);
-                o[2] = fpm::from_f<T>(acc.z);
-                o[3] = fpm::from_f<T>(acc.w);
-            }
+            if (ii < n1max) out[((long)b * n1max + ii) * 256 + h * 16 + d] = fpm::from_f<T>(o / sum);
         }
     }
 }
@@ -234,20 +306,13 @@ extern "C" int fpm_crossset_attn_fwd(int dtype, const float* cost, long c_sb, lo
     FPM_CHECK_ARG(n2max <= emb, "crossset_attn: n2max > embedding dim");
     if (B == 0) return 0;
     dim3 grid(B, (n1max + 15) / 16);
-    size_t sh = (size_t)(n2max * 20 + 16 * n2max) * 4;
-    FPM_CHECK_ARG(sh <= 160 * 1024, "crossset_attn: n2max %d needs %zu B of LDS", n2max, sh);
     hipStream_t st = (hipStream_t)stream;
     FPM_CHECK_ARG(n2max <= 640, "crossset_attn: n2max %d > 640", n2max);
-#define FPM_ATT(TT, NJ)                                                                                      \
-    do {                                                                                                     \
-        if (sh > 64 * 1024)                                                                                  \
-            (void)hipFuncSetAttribute((const void*)afau_row_attn_kernel<TT, NJ>,                             \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);                   \
-        hipLaunchKernelGGL((afau_row_attn_kernel<TT, NJ>), grid, dim3(256), sh, st, cost, c_sb, c_ld, n1max, n2max, \
-                           n2, Wv, emb, mix1w, mix1b, mix2w, mix2b, (TT*)out);                               \
-    } while (0)
-    if (dtype == 0) { if (n2max <= 256) FPM_ATT(float, 4); else FPM_ATT(float, 10); }
-    else { if (n2max <= 256) FPM_ATT(bf16_t, 4); else FPM_ATT(bf16_t, 10); }
+#define FPM_ATT(TT, TJ_)                                                                                         \
+    hipLaunchKernelGGL((afau_row_attn_kernel<TT, TJ_>), grid, dim3(256), 0, st, cost, c_sb, c_ld, n1max, n2max, n2, \
+                       Wv, emb, mix1w, mix1b, mix2w, mix2b, (TT*)out)
+    if (dtype == 0) { if (n2max <= 256) FPM_ATT(float, 16); else FPM_ATT(float, 40); }
+    else { if (n2max <= 256) FPM_ATT(bf16_t, 16); else FPM_ATT(bf16_t, 40); }
 #undef FPM_ATT
     return fpm::check_launch("fpm_crossset_attn_fwd");
 }
