@@ -1,0 +1,39 @@
+"""Build profiles/<round>_pmc_product_gemm.json from the tools/pmc_gemm.sh counter CSVs:
+   python tools/pmc_summary.py gpurun_out/pmc_gemm profiles/r01_pmc_product_gemm.json"""
+import csv
+import json
+import os
+import sys
+
+src, dst = sys.argv[1], sys.argv[2]
+
+
+def mean_kb(pass_name, counter):
+    path = os.path.join(src, pass_name, "run_counter_collection.csv")
+    vals = {}
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter:
+            vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+    names = {r["Kernel_Name"] for r in csv.DictReader(open(path))}
+    return sum(vals.values()) / len(vals), len(vals), sorted(names)
+
+
+f_kb, f_n, names = mean_kb("fetch", "FETCH_SIZE")
+w_kb, w_n, _ = mean_kb("write", "WRITE_SIZE")
+fetch = f_kb * 1024 * 2          # gfx950: FETCH_SIZE reports half the bytes of 16-B/lane reads
+write = w_kb * 1024
+out = {
+    "kernel": "; ".join(n.split("(")[0] for n in names) + " (SplineConv (node, cell) product GEMM)",
+    "command": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE --kernel-include-regex 'gemm_(big_kernel<256|phase_kernel)' "
+               "-- python bench.py --steps 1 --warmup 1 --no-cpu-baseline (separate passes, tools/pmc_gemm.sh)",
+    "gfx950_correction": "FETCH_SIZE x2 (reports half the bytes of 16-B/lane streaming reads, MI355X_MICROARCH.md "
+                         "HBM section); WRITE_SIZE as reported",
+    "units": "bytes per launch (mean over dispatches)",
+    "FETCH_SIZE_raw_KB_mean": f_kb, "FETCH_SIZE_dispatches": f_n,
+    "WRITE_SIZE_raw_KB_mean": w_kb, "WRITE_SIZE_dispatches": w_n,
+    "fetch_bytes": fetch, "write_bytes": write, "traffic_bytes_per_launch": fetch + write,
+    "algorithmic_bytes_per_launch_note": "gathered A rows ~rows*1536 B (MALL-resident node rows re-read once per "
+                                         "cell), weights 26*1.18 MB, Y write rows*1536 B",
+}
+json.dump(out, open(dst, "w"), indent=1)
+print(json.dumps(out, indent=1))
