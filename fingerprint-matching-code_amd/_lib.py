@@ -51,6 +51,10 @@ SIGNATURES = {
     "fpm_bilinear_diag_host": (I, [I, P, P, P, P, L, P, P, P, L, L, P]),
     "fpm_gconv_ws_floats": (L, [I, I, I]),
     "fpm_gconv_fwd": (I, [P, P, I, I, I, I, P, P, I, P, P, P]),
+    "fpm_graph_words": (I, [I]),
+    "fpm_graph_build": (I, [P, P, I, I, I, ctypes.c_double, P, P, P, P, P]),
+    "fpm_graph_edges": (I, [P, P, P, P, I, I, ctypes.c_double, P, P, P, P, P, P, I, P]),
+    "fpm_kron_pattern": (I, [P, P, L, P, P, L, I, I, I, I, P, P, P]),
     "fpm_profile_enable": (I, [I]),
     "fpm_profile_read": (I, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(I)]),

@@ -115,6 +115,28 @@ class DeviceBatch:
         return DeviceBatch(B, ns[0], ns[1], xs, ws, srcs, dsts, pss, device, edge_off=eoffs)
 
     @staticmethod
+    def from_keypoints(P, n, x, w, device, stg="tri"):
+        """Keypoints straight to a device batch: both sides' graphs are built on the GPU
+        (``fpm.graphs``: Delaunay adjacency, np.nonzero edge order, pseudo-coordinates), as the
+        reference's DataLoader does on the host (gmdataset.py:233-244, build_graphs.py:77-100).
+
+        P: 2 x (B, nmax_g, 2) fp32 keypoints; n: 2 x (B,) node counts; x: 2 x (B*nmax_g, 768) fp32
+        node features (zero padding rows); w: 2 x (B, 512) global features."""
+        from . import graphs
+        B = int(P[0].shape[0])
+        srcs, dsts, pss, eoffs, ns = [], [], [], [], []
+        for side in range(2):
+            gb = graphs.build_graph_batch(P[side].to(device), n[side], stg=stg)
+            srcs.append(gb.src)
+            dsts.append(gb.dst)
+            pss.append(gb.pseudo)
+            eoffs.append(gb.edge_off_host)
+            ns.append(torch.as_tensor(n[side], dtype=torch.int32).cpu())
+        bt = DeviceBatch(B, ns[0], ns[1], [x[0], x[1]], [w[0], w[1]], srcs, dsts, pss, device,
+                         nmax=[int(P[0].shape[1]), int(P[1].shape[1])], edge_off=eoffs)
+        return bt
+
+    @staticmethod
     def from_probe_gallery(probe, gallery, device):
         """One probe graph against a gallery (C4): pairs (probe, g) with the probe's
         per-graph stage shared.  Inputs are staged per pair (simple layout); compute is not."""

@@ -174,6 +174,29 @@ long fpm_gconv_ws_floats(int B, int n, int dout);
 int fpm_gconv_fwd(const float* A, const float* x, int B, int n, int din, int dout, const float* W, const float* bias,
                   int norm, float* ws, float* out, void* stream);
 
+/* ---- on-device graph construction ------------------------------------------
+ * Replaces the DataLoader-side utils/build_graphs.py:12-120 (build_graphs / delaunay_triangulate /
+ * fully_connect, sym=True), GMDataset.to_pyg_graph (src/gmdataset.py:170-189) and the collate's
+ * Kronecker index lists (src/gmdataset.py:614-642).  G graphs of padded size nmax <= 1024.
+ * fpm_graph_build: P (G, nmax, 2) fp32 keypoints, n (G) int32; strategy 0 = 'tri' (Delaunay),
+ *   1 = 'fc', 2 = 'near' (edges longer than thre removed).  Writes adj (G, nmax, W) uint32 bit rows
+ *   (W = fpm_graph_words(nmax)), deg (G, nmax) int32 out-degrees, ecount (G) int32 and, if Adense
+ *   is not NULL, the dense adjacency (G, nmax, nmax) fp32 of build_graphs.
+ * fpm_graph_edges: edge list in np.nonzero(A) order with node ids g*nmax + i: src/dst (sum E)
+ *   int32, pseudo (sum E, 2) = clip(0.5*(P_src-P_dst)/rescale + 0.5, 0, 1); edge_off (G+1) int64
+ *   (may be NULL); Ginc/Hinc (G, nmax, epad) fp32 incidence matrices, caller-zeroed (may be NULL).
+ * fpm_kron_pattern: one pair's (rowG, colH) = (CSCMatrix3d(kron(G2,G1)).indices,
+ *   CSCMatrix3d(kron(H2,H1)).transpose().indices) over E1*E2 edge pairs; node ids minus base1/base2;
+ *   out_dtype 0 = float32, 1 = int64. */
+int fpm_graph_words(int nmax);
+int fpm_graph_build(const float* P, const int* n, int G, int nmax, int strategy, double thre, uint32_t* adj, int* deg,
+                    int* ecount, float* Adense, void* stream);
+int fpm_graph_edges(const float* P, const uint32_t* adj, const int* deg, const int* ecount, int G, int nmax,
+                    double rescale, int* src, int* dst, float* pseudo, long* edge_off, float* Ginc, float* Hinc,
+                    int epad, void* stream);
+int fpm_kron_pattern(const int* src1, const int* dst1, long E1, const int* src2, const int* dst2, long E2, int base1,
+                     int base2, int n1pad, int out_dtype, void* rowG, void* colH, void* stream);
+
 /* ---- profiling hooks: HIP-event timing of the dominant kernel (edge-message GEMM) ------------ */
 int fpm_profile_enable(int on);
 int fpm_profile_read(double* ms_total, double* flops_total, int* count);

@@ -17,3 +17,4 @@ cross-checks documented in ``DESIGN.md`` (log-domain step shared with the pinned
 factorised SAGE-mean vs the reference's explicit Kronecker pattern).
 """
 from .ngm_oracle import *  # noqa: F401,F403
+from . import graphs_oracle  # noqa: F401,E402
