@@ -55,6 +55,8 @@ SIGNATURES = {
     "fpm_graph_build": (I, [P, P, I, I, I, ctypes.c_double, P, P, P, P, P]),
     "fpm_graph_edges": (I, [P, P, P, P, I, I, ctypes.c_double, P, P, P, P, P, P, I, P]),
     "fpm_kron_pattern": (I, [P, P, L, P, P, L, I, I, I, I, P, P, P]),
+    "fpm_feature_align_ws_floats": (L, [P, P]),
+    "fpm_feature_align_fwd": (I, [P, P, P, P, P, P, P, P, I, F, F, P, P, L, P, P]),
     "fpm_profile_enable": (I, [I]),
     "fpm_profile_read": (I, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(I)]),

@@ -186,8 +186,8 @@ class DeviceBatch:
             if nf.dim() == 3:
                 X = torch.zeros(B, nmax, nf.shape[-1], dtype=torch.float32, device=nf.device)
                 X[:, :nf.shape[1]] = nf[:, :nmax]
-                for b in range(B):
-                    X[b, int(n[b]):] = 0
+                keep = torch.arange(nmax, device=nf.device)[None, :] < n.to(nf.device).view(-1, 1)
+                X = torch.where(keep[..., None], X, torch.zeros((), device=nf.device))
             else:
                 X = torch.zeros(B, nmax, nf.shape[-1], dtype=torch.float32, device=nf.device)
                 for b in range(B):

@@ -23,6 +23,7 @@ GNN_SK_ITER = 20                    # PYGNNLayer default sk_iter (gnn.py:173/182
 
 SPLINE_KERNEL = 5                   # spline_conv.py:17  (kernel_size=5, dim=2, degree 1 open)
 SPLINE_CELLS = SPLINE_KERNEL * SPLINE_KERNEL
+RESCALE = (320.0, 240.0)            # Net.rescale, ngm.py:160 (feature_align's ori_size)
 PSEUDO_RESCALE = 320.0              # gmdataset.py:36,171 (max(RESCALE))
 
 AFAU_EMB = 600                      # afau.py:27

@@ -5,8 +5,11 @@ Drop-in for the reference's ``Net`` (``src/model/ngm.py:117-491``): same constru
 ``ds_mat``, ``perm_mat``, ``ks_loss``, ``ks_error``, ``cls_loss``, ``cls_prob``, ``k_prob``
 (ngm.py:479-487), and the same state_dict names/shapes (so ``utils/models_sl.load_model`` works).
 The forward starts from per-graph node features (``data_dict['node_features']`` /
-``['global_features']``, or a prebuilt ``data_dict['fpm_batch']``); the ResNet-18 backbone and
-``feature_align`` are out of scope.  Every compute stage runs in ``libfpm_hip.so``; the
+``['global_features']``, or a prebuilt ``data_dict['fpm_batch']``), or -- with
+``Net(backbone=True)`` -- from the reference's ``images`` / ``Ps`` / ``ns`` keys: ResNet-18 on
+MIOpen (``fpm.backbone``), then the fused normalise + feature_align + concat kernel
+(``fpm_feature_align_fwd``); missing ``pyg_graphs`` are built on the device from ``Ps``
+(Delaunay, ``fpm.graphs``).  Every compute stage runs in ``libfpm_hip.so``; the
 Hungarian step runs on host threads (``fpm_lsa_batch_host``) as the reference's does.
 
 ``dtype``: ``"f32"`` (parity mode: fp32 MFMA, matches the CPU oracle) or ``"bf16"`` (bf16 MFMA
@@ -47,9 +50,15 @@ def _build_tree(root, sd):
 
 
 class Net(nn.Module):
-    def __init__(self, regression=False, dtype="f32", seed=0, lsa_threads=None, chunks=None, compute_ke=False):
+    def __init__(self, regression=False, dtype="f32", seed=0, lsa_threads=None, chunks=None, compute_ke=False,
+                 backbone=False):
         super().__init__()
         _build_tree(self, P.init_params(seed))
+        if backbone:
+            # ResNet18_final split (feature_extractor.py:7-75), reference parameter names
+            from .backbone import build_resnet18_split
+            self.node_layers, self.edge_layers, self.final_layers = build_resnet18_split(seed)
+        self._backbone_dev = None
         self.regression = regression
         self.mean_k = True
         self.tau = C.SK_TAU
@@ -460,12 +469,64 @@ class Net(nn.Module):
                                 enqueue_s=t_enq - t0, total_s=time.perf_counter() - t0)
         return res
 
+    def image_features(self, images, Ps, ns, dev=None):
+        """ngm.py:226-248 on the device: per side, node_layers/edge_layers (ResNet-18 convolutions
+        on MIOpen, channels_last; bf16 autocast in the bf16 mode), then one HIP kernel set for
+        global max-pool + channel L2-norm + bilinear feature_align + [U || F] concat.
+        Returns (node feature rows 2 x (B*nmax, 768) with zero padding rows, globals 2 x (B, 512))."""
+        if not hasattr(self, "node_layers"):
+            raise NotImplementedError("image input needs the backbone: construct Net(backbone=True) "
+                                      "(or pass data_dict['node_features'] / ['global_features'])")
+        dev = dev or torch.device("cuda", torch.cuda.current_device())
+        if self._backbone_dev != dev:
+            for m in (self.node_layers, self.edge_layers):
+                m.to(device=dev, memory_format=torch.channels_last)
+            self._backbone_dev = dev
+        xs, gs = [], []
+        for img, pts, n in zip(images, Ps, ns):
+            img = torch.as_tensor(img)
+            if img.dim() == 3:
+                img = img.unsqueeze(0)
+            img = img.to(device=dev, dtype=torch.float32).contiguous(memory_format=torch.channels_last)
+            with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.dtype_mode == "bf16"):
+                nodes = self.node_layers(img)
+                edges = self.edge_layers(nodes)
+            pts = torch.as_tensor(pts).to(device=dev, dtype=torch.float32)
+            n32 = torch.as_tensor(n).view(-1).to(device=dev, dtype=torch.int32)
+            x, g = ops.feature_align(nodes.float(), edges.float(), pts, n32, ori_size=C.RESCALE)
+            xs.append(x)
+            gs.append(g)
+        return xs, gs
+
+    def _batch_from_dict(self, data_dict, dev):
+        dd = data_dict
+        if "node_features" not in dd and "images" in dd:
+            xs, gs = self.image_features(dd["images"], dd["Ps"], dd["ns"], dev)
+            dd = dict(dd)
+            dd["node_features"] = [x.view(int(torch.as_tensor(p).shape[0]), int(torch.as_tensor(p).shape[1]), -1)
+                                   for x, p in zip(xs, dd["Ps"])]
+            dd["global_features"] = gs
+        if "pyg_graphs" not in dd and "Ps" in dd and "node_features" in dd:
+            # graphs as GMDataset builds them ('tri', gmdataset.py:233-244), on the device
+            nf = [torch.as_tensor(t) for t in dd["node_features"]]
+            Ps = [torch.as_tensor(p).to(device=dev, dtype=torch.float32) for p in dd["Ps"]]
+            if any(t.dim() != 3 for t in nf):
+                raise ValueError("device graph build needs padded (B, nmax, 768) node_features")
+            x = []
+            for t, n in zip(nf, dd["ns"]):
+                t = t.to(device=dev, dtype=torch.float32)
+                keep = torch.arange(t.shape[1], device=dev)[None, :] < torch.as_tensor(n).to(dev).view(-1, 1)
+                x.append(torch.where(keep[..., None], t, torch.zeros((), device=dev)).reshape(-1, t.shape[-1]).contiguous())
+            w = [torch.as_tensor(t).to(device=dev, dtype=torch.float32).contiguous() for t in dd["global_features"]]
+            return DeviceBatch.from_keypoints(Ps, [torch.as_tensor(n).view(-1) for n in dd["ns"]], x, w, dev)
+        return DeviceBatch.from_data_dict(dd, dev)
+
     def forward(self, data_dict, regression=True):
         """Reference signature (ngm.py:205).  ``regression`` is accepted and ignored there too."""
         dev = torch.device("cuda", torch.cuda.current_device())
         bt = data_dict.get("fpm_batch")
         if bt is None:
-            bt = DeviceBatch.from_data_dict(data_dict, dev)
+            bt = self._batch_from_dict(data_dict, dev)
         gt = data_dict.get("gt_perm_mat")
         res = self.run(bt, gt_perm=gt, label=data_dict.get("label"))
         data_dict.update({

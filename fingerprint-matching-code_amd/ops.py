@@ -215,6 +215,35 @@ def match_cls(s, perm, w1, b1, bn1_sc, bn1_sh, w2, b2, bn2_sc, bn2_sh, fcw, fcb,
     return logits, prob
 
 
+def feature_align(nodes, edges, P, n, nmax=None, ori_size=(320.0, 240.0), out=None, wglob=None):
+    """Normalise both CNN maps over channels, bilinear-gather them at the keypoints
+    (utils/feature_align.py) and concatenate -> X (B*nmax, C_n + C_e) fp32 with zero padding rows;
+    also the global max-pooled edge feature (B, C_e).  Maps may be NCHW or channels_last."""
+    _dev(nodes, edges, P, n)
+    for t in (nodes, edges, P):
+        if t.dtype != torch.float32:
+            raise _lib.FpmError("feature_align: float32 maps and keypoints expected")
+    if nodes.dim() != 4 or edges.dim() != 4 or P.dim() != 3 or P.shape[-1] != 2:
+        raise _lib.FpmError("feature_align: maps (B, C, H, W) and keypoints (B, nmax, 2) expected")
+    B = int(nodes.shape[0])
+    nmax = int(P.shape[1]) if nmax is None else int(nmax)
+    if int(P.shape[0]) != B or int(P.shape[1]) != nmax or n.numel() != B or n.dtype != torch.int32:
+        raise _lib.FpmError("feature_align: P must be (B, nmax, 2) and n (B,) int32")
+    P = P.contiguous()
+    C = int(nodes.shape[1]) + int(edges.shape[1])
+    if out is None:
+        out = torch.empty(B * nmax, C, dtype=torch.float32, device=nodes.device)
+    if wglob is None:
+        wglob = torch.empty(B, int(edges.shape[1]), dtype=torch.float32, device=nodes.device)
+    arr = lambda v: ctypes.cast((ctypes.c_long * 4)(*[int(x) for x in v]), ctypes.c_void_p)
+    ns_, nst, es_, est = arr(nodes.shape), arr(nodes.stride()), arr(edges.shape), arr(edges.stride())
+    lib = _lib.load()
+    ws = torch.empty(int(lib.fpm_feature_align_ws_floats(ns_, es_)), dtype=torch.float32, device=nodes.device)
+    _lib.call("fpm_feature_align_fwd", _p(nodes), ns_, nst, _p(edges), es_, est, _p(P), _p(n), nmax,
+              float(ori_size[0]), float(ori_size[1]), _p(ws), _p(out), int(out.stride(0)), _p(wglob), _stream(nodes))
+    return out, wglob
+
+
 def lsa_batch_host(s_host, n1_host, n2_host, nthreads=1):
     """Host LSA (maximise s) over a pinned/CPU float32 (B, n1max, n2max) tensor -> (B, n1max) int32."""
     if s_host.is_cuda:

@@ -197,6 +197,19 @@ int fpm_graph_edges(const float* P, const uint32_t* adj, const int* deg, const i
 int fpm_kron_pattern(const int* src1, const int* dst1, long E1, const int* src2, const int* dst2, long E2, int base1,
                      int base2, int n1pad, int out_dtype, void* rowG, void* colH, void* stream);
 
+/* ---- image front end after the CNN (ngm.py:235-248) -----------------------
+ * Replaces normalize_over_channels (ngm.py:65-67) + utils/feature_align.py:5-126 (bilinear gather at
+ * the keypoints, with its (H, W) vs (320, 240) scale mix and border nearest-neighbour branch) +
+ * concat_features (ngm.py:70-72) + the AdaptiveMaxPool2d(1) global feature (feature_extractor.py:62).
+ * nodes/edges: (B, C, H, W) fp32 maps given by shape[4] and element strides[4] (NCHW or
+ * channels_last); P (B, nmax, 2) fp32 keypoints in the ori_w x ori_h frame; n (B) int32.
+ * X (B*nmax, ldx) fp32 rows = [U (C_nodes) || F (C_edges)], zero rows past n[b];
+ * wglob (B, C_edges) fp32 (may be NULL); ws: fpm_feature_align_ws_floats(...) floats. */
+long fpm_feature_align_ws_floats(const long* node_shape, const long* edge_shape);
+int fpm_feature_align_fwd(const float* nodes, const long* node_shape, const long* node_stride, const float* edges,
+                          const long* edge_shape, const long* edge_stride, const float* P, const int* n, int nmax,
+                          float ori_w, float ori_h, float* ws, float* X, long ldx, float* wglob, void* stream);
+
 /* ---- profiling hooks: HIP-event timing of the dominant kernel (edge-message GEMM) ------------ */
 int fpm_profile_enable(int on);
 int fpm_profile_read(double* ms_total, double* flops_total, int* count);

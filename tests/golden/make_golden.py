@@ -10,7 +10,8 @@ Run ONLY in the build container (the reference tree does not exist on the GPU bo
 written (``tests/golden/*.npz``); no reference source is copied.  Modules used:
 ``src.model.soft_topk`` (soft_topk -> Sinkhorn_m, greedy_perm), ``src.model.afau.Encoder``,
 ``src.model.affinity_layer``, ``src.model.gcn.Gconv``, ``utils.hungarian``,
-``utils.build_graphs``, ``utils.factorize_graph_matching`` + ``src.sparse_torch``.
+``utils.build_graphs``, ``utils.factorize_graph_matching`` + ``src.sparse_torch``,
+``utils.feature_align``.  ``python make_golden.py NAME ...`` regenerates only the named fixtures.
 """
 import os
 import sys
@@ -33,6 +34,7 @@ from utils.hungarian import hungarian  # noqa: E402
 from utils.build_graphs import build_graphs  # noqa: E402
 from utils.factorize_graph_matching import kronecker_sparse, construct_sparse_aff_mat  # noqa: E402
 from src.sparse_torch import CSCMatrix3d  # noqa: E402
+from utils.feature_align import feature_align  # noqa: E402
 
 
 def save(name, **arrs):
@@ -162,11 +164,33 @@ def gen_gconv():
          u_b=gc.u_fc.bias.detach().numpy(), y=y.numpy())
 
 
+def gen_feature_align():
+    """utils/feature_align.py on maps of the backbone's spatial sizes (240x320 image: stride-16
+    15x20, stride-32 8x10) with keypoints on the borders and outside the frame (clamped /
+    nearest-neighbour branches).  Maps are normalised over channels first (ngm.py:65-67)."""
+    g = torch.Generator().manual_seed(23)
+    nodes = torch.randn(2, 70, 15, 20, generator=g)
+    edges = torch.randn(2, 130, 8, 10, generator=g)
+    P = torch.rand(2, 9, 2, generator=g) * torch.tensor([320.0, 240.0])
+    P[0, 0] = torch.tensor([0.0, 0.0])
+    P[0, 1] = torch.tensor([319.9, 239.9])
+    P[0, 2] = torch.tensor([-5.0, 250.0])
+    P[0, 3] = torch.tensor([10.6, 6.0])
+    P[0, 4] = torch.tensor([330.0, -3.0])
+    P[1, 0] = torch.tensor([160.0, 120.0])
+    ns = torch.tensor([9, 6])
+    nn_ = nodes / torch.norm(nodes, dim=1, keepdim=True)
+    ne_ = edges / torch.norm(edges, dim=1, keepdim=True)
+    U = feature_align(nn_, P, ns, (320, 240))
+    F = feature_align(ne_, P, ns, (320, 240))
+    save("feature_align", nodes=nodes.numpy(), edges=edges.numpy(), P=P.numpy(), ns=ns.numpy(),
+         U=U.numpy(), F=F.numpy())
+
+
+GENERATORS = dict(soft_topk=gen_soft_topk, hungarian_greedy=gen_hungarian_greedy, encoder=gen_encoder,
+                  affinity=gen_affinity, graphs_pattern=gen_graphs_and_pattern, delaunay=gen_pyg_edges,
+                  gconv=gen_gconv, feature_align=gen_feature_align)
+
 if __name__ == "__main__":
-    gen_soft_topk()
-    gen_hungarian_greedy()
-    gen_encoder()
-    gen_affinity()
-    gen_graphs_and_pattern()
-    gen_pyg_edges()
-    gen_gconv()
+    for name in (sys.argv[1:] or list(GENERATORS)):
+        GENERATORS[name]()

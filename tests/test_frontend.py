@@ -1,0 +1,157 @@
+"""Image front end: ResNet-18 backbone (fpm.backbone, MIOpen convolutions) +
+the fused normalise / feature_align / concat / global-max-pool kernel (fpm_feature_align_fwd), and
+the full images -> match forward through Net(backbone=True).
+
+Oracle: oracle/frontend_oracle.py, pinned bit-exactly by tests/golden/feature_align.npz (the
+reference's own utils/feature_align.py).  GPU tolerance: 2e-6 abs on the aligned features (the
+channel norm's summation order differs from torch's; the interpolation itself is evaluated in the
+reference's fp32 operation order without FMA contraction).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import frontend_oracle as FO
+
+
+def _golden():
+    z = np.load(os.path.join(GOLDEN, "feature_align.npz"))
+    return {k: torch.from_numpy(z[k]) for k in z.files}
+
+
+def test_oracle_feature_align_golden():
+    z = _golden()
+    U = FO.feature_align(FO.normalize_over_channels(z["nodes"]), z["P"], z["ns"])
+    F = FO.feature_align(FO.normalize_over_channels(z["edges"]), z["P"], z["ns"])
+    assert torch.equal(U, z["U"]) and torch.equal(F, z["F"])
+
+
+def test_backbone_layout_and_shapes():
+    """torchvision resnet18 names inside the reference's Sequential split; stride-16 / stride-32
+    maps of a 240x320 image are 15x20x256 and 8x10x512 (feature_extractor.py:46-58)."""
+    from fpm.backbone import build_resnet18_split, backbone_state_dict
+    sd = backbone_state_dict(0)
+    for k, shape in (("node_layers.0.weight", (64, 3, 7, 7)), ("node_layers.1.running_var", (64,)),
+                     ("node_layers.4.0.conv1.weight", (64, 64, 3, 3)),
+                     ("node_layers.5.0.downsample.0.weight", (128, 64, 1, 1)),
+                     ("node_layers.6.1.bn2.bias", (256,)), ("edge_layers.0.0.downsample.1.weight", (512,)),
+                     ("edge_layers.0.1.conv2.weight", (512, 512, 3, 3))):
+        assert tuple(sd[k].shape) == shape, k
+    assert sum(v.numel() for k, v in sd.items() if not k.endswith("num_batches_tracked")) == 11176512 + 9600
+    nl, el, fl = build_resnet18_split(0)
+    nl.eval()
+    el.eval()
+    with torch.no_grad():
+        nodes = nl(torch.randn(1, 3, 240, 320))
+        edges = el(nodes)
+    assert nodes.shape == (1, 256, 15, 20) and edges.shape == (1, 512, 8, 10)
+    assert fl(edges).shape == (1, 512, 1, 1)
+
+
+# ------------------------------------------------------------------------------- GPU
+DEV = torch.device("cuda", 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("channels_last", [False, True])
+def test_feature_align_kernel_golden(channels_last):
+    from fpm import ops
+    z = _golden()
+    mf = torch.channels_last if channels_last else torch.contiguous_format
+    nodes = z["nodes"].to(DEV).contiguous(memory_format=mf)
+    edges = z["edges"].to(DEV).contiguous(memory_format=mf)
+    B, nmax = z["P"].shape[:2]
+    n = z["ns"].to(torch.int32).to(DEV)
+    X, g = ops.feature_align(nodes, edges, z["P"].to(DEV), n)
+    X = X.cpu().view(B, nmax, -1)
+    U, F = z["U"].transpose(1, 2), z["F"].transpose(1, 2)
+    cn = U.shape[-1]
+    assert (X[..., :cn] - U).abs().max() < 2e-6
+    assert (X[..., cn:] - F).abs().max() < 2e-6
+    for b in range(B):
+        assert not X[b, int(z["ns"][b]):].any()
+    assert torch.equal(g.cpu(), torch.amax(z["edges"], dim=(2, 3)))
+
+
+def _image_batch(B, n, seed):
+    g = torch.Generator().manual_seed(seed)
+    imgs = [torch.rand(B, 3, 240, 320, generator=g) for _ in range(2)]
+    Ps, ns = [], []
+    rng = np.random.default_rng(seed)
+    for side in range(2):
+        P = np.zeros((B, n, 2), np.float32)
+        nn_ = []
+        for b in range(B):
+            m = n - (b % 3) * 5
+            P[b, :m] = np.stack([rng.uniform(0, 320, m), rng.uniform(0, 240, m)], 1)
+            nn_.append(m)
+        Ps.append(torch.from_numpy(P))
+        ns.append(torch.tensor(nn_))
+    return imgs, Ps, ns
+
+
+@pytest.mark.gpu
+def test_image_features_vs_oracle():
+    """Backbone on MIOpen + HIP align vs the same backbone on CPU + the oracle front end."""
+    import fpm
+    net = fpm.Net(regression=True, backbone=True)
+    imgs, Ps, ns = _image_batch(2, 40, 3)
+    xs, gs = net.image_features(imgs, Ps, ns, DEV)
+    from fpm.backbone import build_resnet18_split
+    nl, el, _ = build_resnet18_split(0)
+    nl.eval()
+    el.eval()
+    for side in range(2):
+        with torch.no_grad():
+            nodes = nl(imgs[side])
+            edges = el(nodes)
+        xr, gr = FO.image_features(nodes, edges, Ps[side], ns[side])
+        assert (xs[side].cpu().view_as(xr) - xr).abs().max() < 1e-4
+        assert (gs[side].cpu() - gr).abs().max() < 1e-3 * max(1.0, float(gr.abs().max()))
+
+
+@pytest.mark.gpu
+def test_images_to_match_forward():
+    """data_dict with only images / Ps / ns (+ gt, label): backbone, feature_align, device Delaunay
+    graphs and the matcher, through Net.forward.  Device-built graphs give the same result bit for
+    bit as host-built (scipy) ones; both paths agree with the CPU oracle within the 1e-4 gate."""
+    import fpm
+    from fpm import params
+    from fpm.batch import DeviceBatch
+    import oracle as O
+    from oracle import graphs_oracle as GO
+    net = fpm.Net(regression=True, backbone=True)
+    sd = params.init_params(5)
+    net.load_state_dict({**net.state_dict(), **sd})
+    B, n = 3, 32
+    imgs, Ps, ns = _image_batch(B, n, 8)
+    dd = {"images": imgs, "Ps": Ps, "ns": ns, "gt_perm_mat": torch.zeros(B, n, n)}
+    out = net.forward(dict(dd))
+    xs, gs = net.image_features(imgs, Ps, ns, DEV)
+    pairs = []
+    for b in range(B):
+        pr = []
+        for side in range(2):
+            m = int(ns[side][b])
+            p = Ps[side][b, :m].numpy()
+            A = GO.delaunay_triangulate(p.astype(np.float64))
+            ei, attr = GO.pyg_edges(A, p)
+            x = xs[side].view(B, n, -1)[b, :m].cpu().numpy()
+            pr.append(dict(n=m, x=x, w=gs[side][b].cpu().numpy(), edge_index=ei, pseudo=attr, P=p, A=A))
+        pairs.append(tuple(pr))
+    ref = net.run(DeviceBatch.from_pairs(pairs, DEV), gt_perm=dd["gt_perm_mat"])
+    # same features, graphs built on the device from Ps (no pyg_graphs): bit-identical
+    dd2 = {"node_features": [x.view(B, n, -1) for x in xs], "global_features": gs, "Ps": Ps, "ns": ns,
+           "gt_perm_mat": dd["gt_perm_mat"]}
+    out2 = net.forward(dd2)
+    for k in ("ds_mat", "perm_mat", "k_prob", "cls_prob"):
+        assert torch.equal(out2[k], ref[k]), k
+    # MIOpen may pick a different convolution algorithm per call: the images path is compared
+    # within the fp32 gate, not bitwise
+    orc = O.forward(pairs, {k: v for k, v in net.state_dict().items()})
+    for r in (ref, out):
+        assert (r["ds_mat"].cpu() - orc["ds_mat"]).abs().max() < 1e-4
+        assert (r["k_prob"].cpu() - orc["k_prob"]).abs().max() < 1e-4
