@@ -15,6 +15,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
@@ -92,6 +94,43 @@ def cpu_baseline(n, npairs, seed, sd):
             "sample": "%d pairs, n=%d, fp32 oracle forward incl. scipy Hungarian (1 process)" % (npairs, n)}
 
 
+def bench_graph_build(kp, bt, dev, args):
+    """On-device Delaunay graph build of both sides of the batch (fpm.graphs; untimed w.r.t. the
+    metric: the reference builds graphs in DataLoader workers) vs scipy on a host sample; the
+    device edge lists are checked against the host-built ones the bench ran on (full size)."""
+    import torch
+    from scipy.spatial import Delaunay
+    from fpm import graphs
+    P = [torch.from_numpy(k).to(dev) for k in kp]
+    ns = [bt.n_host[0], bt.n_host[1]]
+    for side in range(2):          # warm-up (module load)
+        graphs.build_graph_batch(P[side][:4], ns[side][:4])
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    gbs = [graphs.build_graph_batch(P[side], ns[side]) for side in range(2)]
+    e1.record()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    mism = 0
+    for side in range(2):
+        g = gbs[side]
+        if not (torch.equal(g.src, bt.src[side]) and torch.equal(g.dst, bt.dst[side])
+                and torch.equal(g.pseudo, bt.pseudo[side])):
+            mism += 1
+    sample = min(64, kp[0].shape[0])
+    t0 = time.perf_counter()
+    for b in range(sample):
+        Delaunay(kp[0][b].astype(np.float64))
+    host = (time.perf_counter() - t0) / sample
+    ngraph = 2 * kp[0].shape[0]
+    return {"graphs": ngraph, "n": int(kp[0].shape[1]), "gpu_ms": e0.elapsed_time(e1), "wall_ms": wall * 1e3,
+            "gpu_graphs_per_s": ngraph / (e0.elapsed_time(e1) / 1e3),
+            "host_scipy_delaunay_ms_per_graph": host * 1e3,
+            "edge_lists_identical_to_host": mism == 0}
+
+
 def log(*a):
     print("[bench %.1fs]" % (time.perf_counter() - T0), *a, file=sys.stderr, flush=True)
 
@@ -164,6 +203,7 @@ def main():
         del gallery
     else:
         bt = DeviceBatch.from_pairs(pairs, dev)
+        kp = [np.stack([p[side]["P"] for p in pairs]).astype(np.float32) for side in range(2)]
         del pairs
     E_tot = bt.E[0] + bt.E[1]
 
@@ -227,6 +267,11 @@ def main():
         with open(pmc_file) as f:
             traffic = json.load(f).get("traffic_bytes_per_launch")
 
+    graph_build = None
+    if rank == 0 and args.config != "c4":
+        graph_build = bench_graph_build(kp, bt, dev, args)
+        log("graph build: %s" % json.dumps(graph_build))
+
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -269,6 +314,7 @@ def main():
                          "isolated_avg_launch_ms": iso_ms.value / max(iso_cnt.value, 1)},
             "cpu_baseline": cpu,
             "input_gen_s": t_gen,
+            "graph_build": graph_build,
         }
         print(json.dumps(res))
     if world > 1:

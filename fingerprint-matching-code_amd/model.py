@@ -51,7 +51,7 @@ def _build_tree(root, sd):
 
 class Net(nn.Module):
     def __init__(self, regression=False, dtype="f32", seed=0, lsa_threads=None, chunks=None, compute_ke=False,
-                 backbone=False):
+                 backbone=False, lsa=None):
         super().__init__()
         _build_tree(self, P.init_params(seed))
         if backbone:
@@ -59,6 +59,11 @@ class Net(nn.Module):
             from .backbone import build_resnet18_split
             self.node_layers, self.edge_layers, self.final_layers = build_resnet18_split(seed)
         self._backbone_dev = None
+        # Hungarian step (utils/hungarian.py): "host" = C++ thread pool over a pinned ds_mat copy,
+        # "device" = the same solver restated per wavefront (fpm_lsa_batch_device, bit-identical)
+        self.lsa_mode = lsa or os.environ.get("FPM_LSA", "host")
+        if self.lsa_mode not in ("host", "device"):
+            raise ValueError("lsa must be 'host' or 'device'")
         self.regression = regression
         self.mean_k = True
         self.tau = C.SK_TAU
@@ -345,6 +350,12 @@ class Net(nn.Module):
             self._stream_cache[key] = [torch.cuda.Stream(dev) for _ in range(self.n_streams)]
         return self._stream_cache[key]
 
+    def _lsa_streams(self, dev):
+        key = "lsa:" + str(dev)
+        if key not in self._stream_cache:
+            self._stream_cache[key] = [torch.cuda.Stream(dev) for _ in range(2)]
+        return self._stream_cache[key]
+
     def pipeline_chunks(self, B):
         """Sub-batches per forward so the host Hungarian of chunk c overlaps the GPU work of c+1."""
         if self.chunks is not None:
@@ -370,11 +381,34 @@ class Net(nn.Module):
                       out_host=self._pinned[b0:b1] if self.zero_copy else None)
         o["_kk"][b0:b1].copy_(ks * min_pt[b0:b1])
         self._mark("soft_topk")
+        if self.lsa_mode == "device":
+            # the Hungarian kernel is latency-bound (one wave per pair): run it and the selection /
+            # classifier on a side stream so the next chunks' GPU stages are not queued behind it
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(st)
+            self._lsa_rr = getattr(self, "_lsa_rr", 0) + 1
+            side = self._lsa_streams(dev)[self._lsa_rr % 2]
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                self._stage_c_device(part, b0, b1, o)
+            return r, ev
         if not self.zero_copy:
             self._pinned[b0:b1].copy_(o["ds_mat"][b0:b1], non_blocking=True)
         ev = torch.cuda.Event(enable_timing=True)
         ev.record(st)
         return r, ev
+
+    def _stage_c_device(self, part, b0, b1, o):
+        """Device Hungarian + greedy selection + MatchClassifier of one chunk, queued on the
+        chunk's stream right behind its soft top-k (no host round trip)."""
+        wp = self._pack
+        assign, status = ops.lsa_batch_device(o["ds_mat"][b0:b1], part.n1, part.n2,
+                                              status=o["_lsa_status"][b0:b1])
+        ops.topk_select(o["ds_mat"][b0:b1], assign, o["_kk"][b0:b1], lsa_out=o["lsa"][b0:b1],
+                        out=o["perm_mat"][b0:b1])
+        ops.match_cls(o["s"][b0:b1], o["perm_mat"][b0:b1], wp["mc_w1"], wp["mc_b1"], wp["mc_sc1"], wp["mc_sh1"],
+                      wp["mc_w2"], wp["mc_b2"], wp["mc_sc2"], wp["mc_sh2"], wp["mc_fcw"], wp["mc_fcb"],
+                      logits=o["cls_logits"][b0:b1], prob=o["cls_prob"][b0:b1])
 
     def _stage_c(self, part, b0, b1, o):
         """Host Hungarian (utils/hungarian.py: LSA of -ds_mat per pair) + greedy selection +
@@ -416,7 +450,9 @@ class Net(nn.Module):
         o = {k: torch.empty(B, n1max, n2max, **f32) for k in ("s", "ss", "ds_mat", "perm_mat", "lsa")}
         o.update({k: torch.empty(B, **f32) for k in ("k_prob", "cls_logits", "cls_prob", "_kk")})
         o["sk_steps"] = torch.empty(B, device=dev, dtype=torch.int32)
-        if self._pinned is None or self._pinned.shape != o["ds_mat"].shape:
+        o["_lsa_status"] = torch.zeros(B, device=dev, dtype=torch.int32)
+        device_lsa = self.lsa_mode == "device"
+        if not device_lsa and (self._pinned is None or self._pinned.shape != o["ds_mat"].shape):
             self._pinned = torch.empty(o["ds_mat"].shape, dtype=torch.float32, pin_memory=True)
         main = torch.cuda.current_stream(dev)
         ev_start = torch.cuda.Event(enable_timing=True)
@@ -439,6 +475,8 @@ class Net(nn.Module):
         t_enq = time.perf_counter()
         t_lsa, t_first = 0.0, None
         for c, (part, ev) in enumerate(zip(parts, events)):
+            if device_lsa:
+                break
             b0, b1 = getattr(part, "pair_range", (0, B))
             ev.synchronize()
             t_first = t_first or time.perf_counter()
@@ -447,6 +485,12 @@ class Net(nn.Module):
         for st in streams:
             if st is not main:
                 main.wait_stream(st)
+        if device_lsa:
+            for st in self._lsa_streams(dev):
+                main.wait_stream(st)
+            bad = torch.nonzero(o["_lsa_status"]).view(-1)
+            if bad.numel():
+                raise RuntimeError("hungarian: pair %d is infeasible or has NaN/-inf costs" % int(bad[0]))
         res = {k: v for k, v in o.items() if not k.startswith("_")}
         if len(outs) == 1 or keep_feats:
             for k in outs[0]:

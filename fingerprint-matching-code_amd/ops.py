@@ -244,6 +244,23 @@ def feature_align(nodes, edges, P, n, nmax=None, ori_size=(320.0, 240.0), out=No
     return out, wglob
 
 
+def lsa_batch_device(s, n1, n2, assign=None, status=None):
+    """Device LSA (maximise s) over a (B, n1max, n2max) float32 view with unit column stride ->
+    (assign (B, n1max) int32, status (B,) int32); bit-identical to ``lsa_batch_host``.  Asynchronous:
+    check ``status`` (0 ok, 1 infeasible, 2 NaN/-inf) after synchronising."""
+    _dev(s, n1, n2)
+    if s.dtype != torch.float32 or s.dim() != 3 or s.stride(2) != 1:
+        raise _lib.FpmError("lsa_batch_device: (B, n1max, n2max) float32 with unit column stride expected")
+    B, n1max, n2max = s.shape
+    if assign is None:
+        assign = torch.empty(B, n1max, dtype=torch.int32, device=s.device)
+    if status is None:
+        status = torch.empty(B, dtype=torch.int32, device=s.device)
+    _lib.call("fpm_lsa_batch_device", _p(s), int(s.stride(0)), int(s.stride(1)), _p(n1), _p(n2), B, n1max, n2max,
+              _p(assign), _p(status), _stream(s))
+    return assign, status
+
+
 def lsa_batch_host(s_host, n1_host, n2_host, nthreads=1):
     """Host LSA (maximise s) over a pinned/CPU float32 (B, n1max, n2max) tensor -> (B, n1max) int32."""
     if s_host.is_cuda:

@@ -47,7 +47,8 @@ def edges_from_adjacency(A, P):
 def make_graph(base_seed, p, g, n):
     rng = _rng(base_seed, p, g)
     while True:
-        P = np.stack([rng.uniform(0, 320, n), rng.uniform(0, 240, n)], axis=1)
+        # keypoints are float32 (the reference's Ps tensors); graphs are built from those values
+        P = np.stack([rng.uniform(0, 320, n), rng.uniform(0, 240, n)], axis=1).astype(np.float32).astype(np.float64)
         if len(np.unique(P, axis=0)) == n:
             break
     A = delaunay_adjacency(P)

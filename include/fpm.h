@@ -214,6 +214,15 @@ int fpm_feature_align_fwd(const float* nodes, const long* node_shape, const long
 int fpm_profile_enable(int on);
 int fpm_profile_read(double* ms_total, double* flops_total, int* count);
 
+/* ---- device: batched linear sum assignment -------------------------------
+ * The host solver's algorithm (utils/hungarian.py:8-66 -> scipy LSAP, csrc/lsa.cpp) restated for
+ * one wavefront per pair with identical arithmetic, scan order and tie rule: assignments are
+ * bit-identical to fpm_lsa_batch_host.  s: device float32, batch stride sb, row stride ld; maximise
+ * s over each n1[b] x n2[b] block.  assign (B, n1max) int32 (column or -1); status (B) int32:
+ * 0 ok, 1 infeasible, 2 NaN / -inf cost.  n1max, n2max <= 1024.  Asynchronous on stream. */
+int fpm_lsa_batch_device(const float* s, long sb, long ld, const int* n1, const int* n2, int B, int n1max, int n2max,
+                         int* assign, int* status, void* stream);
+
 /* ---- host: batched linear sum assignment ------------------------------------------------------
  * Replaces utils/hungarian.py:8-66 (scipy linear_sum_assignment on -s, per pair).  Synchronous,
  * HOST memory, nthreads worker threads.  assign[b][r] = column or -1.  Returns 0 or (pair + 1). */
