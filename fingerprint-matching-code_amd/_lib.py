@@ -58,6 +58,13 @@ SIGNATURES = {
     "fpm_kron_pattern": (I, [P, P, L, P, P, L, I, I, I, I, P, P, P]),
     "fpm_feature_align_ws_floats": (L, [P, P]),
     "fpm_feature_align_fwd": (I, [P, P, P, P, P, P, P, P, I, F, F, P, P, L, P, P]),
+    "fpm_sinkhorn_bwd_ws_floats": (L, [I, I, I, I]),
+    "fpm_sinkhorn_log_bwd": (I, [P, L, L, L, P, L, L, L, P, P, P, I, I, I, I, F, I, P, L, P]),
+    "fpm_soft_topk_bwd_ws_floats": (L, [I, I, I]),
+    "fpm_soft_topk_bwd": (I, [P, L, L, P, P, P, P, I, I, I, F, P, L, L, P, P, L, P, P]),
+    "fpm_spline_plan_rows": (I, [P, L, L, ctypes.POINTER(P), ctypes.POINTER(P)]),
+    "fpm_spline_conv_bwd_data": (I, [I, P, L, L, I, P, P, P, I, P, P, P, P, P, P, I, P]),
+    "fpm_kron_agg": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, I, P, P]),
     "fpm_profile_enable": (I, [I]),
     "fpm_profile_read": (I, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(I)]),

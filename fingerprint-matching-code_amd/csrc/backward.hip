@@ -1,0 +1,406 @@
+// Training backward of the normalisation stages:
+//   * pygmtools log-domain Sinkhorn (reference src/model/sinkhorn.py:58-87 -> pygm.sinkhorn,
+//     also inside PYGNNLayer, src/model/gnn.py:221), and
+//   * the soft top-k's 2-column Sinkhorn_m incl. the data-dependent continuation
+//     (src/model/soft_topk.py:23-45, 166-255), with the anchor min/max and |.| of the distance
+//     construction (soft_topk.py:28-29).
+//
+// Both forwards are alternating log-normalisations  L' = L - lse_dim(L) (+ log marginal).  Their
+// vector-Jacobian product is  dL = dL' - exp(L' - log marginal) * sum_dim(dL'), so the backward
+// needs every intermediate L'.  Storing them would cost n1*n2 floats per step; instead the kernel
+// replays the forward in dual form (L = S/tau - u_row - v_col) keeping only the potential history
+// (rows + cols floats per step), then walks the steps in reverse.  One 1024-thread workgroup per
+// pair; reductions are fixed-order (wave trees, per-thread serial column sums), so the gradients
+// are deterministic.  Values are in log2 units as in the forward kernels.
+#include "fpm_common.h"
+
+namespace {
+
+constexpr float DUMMY_L2 = -100.f * fpm::LOG2E_F;   // dummy rows' log value (pygm), log2 units
+
+__device__ __forceinline__ float wave_max(float v) { return fpm::warp_max(v); }
+__device__ __forceinline__ float wave_sum(float v) { return fpm::warp_sum(v); }
+
+struct SinkBwdArgs {
+    const float* s;
+    long s_sb, s_si, s_sj;
+    const float* dp;
+    long d_sb, d_si, d_sj;
+    float* ds;        // (B, n1max, n2max) contiguous
+    const int* n1;
+    const int* n2;
+    int n1max, n2max, iters;
+    float tau;
+    int dummy_row;
+    float* dL;        // B x n1max*n2max scratch (algorithmic R x C, row-major)
+    float* hist;      // B x iters x H potentials after each step
+    int H;            // max(n1max, n2max) + 1 (slot H-1: the dummy rows' potential)
+};
+
+__global__ __launch_bounds__(1024) void sinkhorn_bwd_kernel(SinkBwdArgs a) {
+    extern __shared__ float sh[];
+    const int H = a.H;
+    float* u = sh;           // row potentials (+ dummy at H-1)
+    float* v = sh + H;       // column potentials
+    float* dLd = sh + 2 * H; // gradient of one dummy row (all nd dummy rows are identical)
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int n1b = a.n1[b], n2b = a.n2[b];
+    const bool tr = n1b > n2b;
+    const int R = tr ? n2b : n1b, C = tr ? n1b : n2b;
+    const int nd = (a.dummy_row && C > R) ? C - R : 0;
+    const float sc = fpm::LOG2E_F / a.tau;
+    const float* S = a.s + (long)b * a.s_sb;
+    const float* DP = a.dp + (long)b * a.d_sb;
+    float* dL = a.dL + (long)b * a.n1max * a.n2max;
+    float* hist = a.hist + (long)b * a.iters * H;
+    float* out = a.ds + (long)b * a.n1max * a.n2max;
+    const long boxN = (long)a.n1max * a.n2max;
+    // algorithmic (r, c) -> physical element (transposed when n1 > n2)
+    auto Sv = [&](int r, int c) -> float {
+        const long o = tr ? (long)c * a.s_si + (long)r * a.s_sj : (long)r * a.s_si + (long)c * a.s_sj;
+        return S[o] * sc;
+    };
+    auto DPv = [&](int r, int c) -> float {
+        const long o = tr ? (long)c * a.d_si + (long)r * a.d_sj : (long)r * a.d_si + (long)c * a.d_sj;
+        return DP[o];
+    };
+    for (long k = tid; k < boxN; k += 1024) out[k] = 0.f;
+    if (R == 0 || C == 0) return;
+    for (int k = tid; k < H; k += 1024) { u[k] = 0.f; v[k] = 0.f; dLd[k] = 0.f; }
+    __syncthreads();
+
+    auto row_step = [&](int t) {
+        for (int r = wv; r < R; r += 16) {
+            float m = -INFINITY;
+            for (int c = lane; c < C; c += 64) m = fmaxf(m, Sv(r, c) - v[c]);
+            m = wave_max(m);
+            float s = 0.f;
+            if (m != -INFINITY)
+                for (int c = lane; c < C; c += 64) s += fpm::fast_exp2(Sv(r, c) - v[c] - m);
+            s = wave_sum(s);
+            const float pr = m == -INFINITY ? 0.f : m + fpm::fast_log2(s);
+            if (lane == 0) { u[r] = pr; hist[(long)t * H + r] = pr; }
+        }
+        if (nd > 0 && wv == 15) {
+            float m = -INFINITY;
+            for (int c = lane; c < C; c += 64) m = fmaxf(m, DUMMY_L2 - v[c]);
+            m = wave_max(m);
+            float s = 0.f;
+            for (int c = lane; c < C; c += 64) s += fpm::fast_exp2(DUMMY_L2 - v[c] - m);
+            s = wave_sum(s);
+            const float pr = m + fpm::fast_log2(s);
+            if (lane == 0) { u[H - 1] = pr; hist[(long)t * H + H - 1] = pr; }
+        }
+        __syncthreads();
+    };
+    auto col_step = [&](int t) {
+        const float ud = u[H - 1];
+        for (int c = tid; c < C; c += 1024) {
+            float m = nd > 0 ? DUMMY_L2 - ud : -INFINITY, s = nd > 0 ? (float)nd : 0.f;
+            for (int r = 0; r < R; ++r) {
+                const float x = Sv(r, c) - u[r];
+                if (x > m) { s = s * fpm::fast_exp2(m - x) + 1.f; m = x; }
+                else s += fpm::fast_exp2(x - m);
+            }
+            const float pc = m == -INFINITY ? 0.f : m + fpm::fast_log2(s);
+            v[c] = pc;
+            hist[(long)t * H + c] = pc;
+        }
+        __syncthreads();
+    };
+    for (int t = 0; t < a.iters; ++t) {
+        if (t & 1) col_step(t);
+        else row_step(t);
+    }
+
+    // dL_T = dP o P on the real rows (the output is exp(L) there); dummy rows get no direct gradient
+    for (int r = wv; r < R; r += 16)
+        for (int c = lane; c < C; c += 64)
+            dL[(long)r * C + c] = DPv(r, c) * fpm::fast_exp2(Sv(r, c) - u[r] - v[c]);
+    __syncthreads();
+
+    for (int t = a.iters - 1; t >= 0; --t) {
+        if ((t & 1) == 0) {
+            // row step: dL -= exp(L') * rowsum(dL)
+            for (int r = wv; r < R; r += 16) {
+                float s = 0.f;
+                for (int c = lane; c < C; c += 64) s += dL[(long)r * C + c];
+                s = wave_sum(s);
+                for (int c = lane; c < C; c += 64)
+                    dL[(long)r * C + c] -= fpm::fast_exp2(Sv(r, c) - u[r] - v[c]) * s;
+            }
+            if (nd > 0 && wv == 15) {
+                float s = 0.f;
+                for (int c = lane; c < C; c += 64) s += dLd[c];
+                s = wave_sum(s);
+                for (int c = lane; c < C; c += 64) dLd[c] -= fpm::fast_exp2(DUMMY_L2 - u[H - 1] - v[c]) * s;
+            }
+            __syncthreads();
+            // restore the row potentials in effect before this step
+            for (int r = tid; r < H; r += 1024) {
+                if (r < R || r == H - 1) u[r] = t >= 2 ? hist[(long)(t - 2) * H + r] : 0.f;
+            }
+            __syncthreads();
+        } else {
+            // column step (nd identical dummy rows included): dL -= exp(L') * colsum(dL)
+            const float ud = u[H - 1];
+            for (int c = tid; c < C; c += 1024) {
+                float s = nd > 0 ? (float)nd * dLd[c] : 0.f;
+                for (int r = 0; r < R; ++r) s += dL[(long)r * C + c];
+                for (int r = 0; r < R; ++r) dL[(long)r * C + c] -= fpm::fast_exp2(Sv(r, c) - u[r] - v[c]) * s;
+                if (nd > 0) dLd[c] -= fpm::fast_exp2(DUMMY_L2 - ud - v[c]) * s;
+            }
+            __syncthreads();
+            for (int c = tid; c < C; c += 1024) v[c] = t >= 2 ? hist[(long)(t - 2) * H + c] : 0.f;
+            __syncthreads();
+        }
+    }
+    // dS = dL0 / tau on the valid block (zeros elsewhere, written above)
+    const float it = 1.f / a.tau;
+    for (int r = wv; r < R; r += 16)
+        for (int c = lane; c < C; c += 64) {
+            const long o = tr ? (long)c * a.n2max + r : (long)r * a.n2max + c;
+            out[o] = dL[(long)r * C + c] * it;
+        }
+}
+
+// ---------------------------------------------------------------------------------------------
+// soft top-k backward.  Forward state (topk.hip): L[q,c] = D[q,c] - V[c] - u(q; Vu) with
+// D[q,c] = -|ss_q - anchor_c| / tau, u(q; V) = lse_c(D[q,c] - V[c]) and V accumulating
+// lse_c - lcp_c at each column step.  Steps alternate row (t even) / column (t odd); the forward's
+// step count (incl. the while-loop continuation) is read from its ``steps`` output.
+// ---------------------------------------------------------------------------------------------
+constexpr int TOPK_MAX_STEPS = 4096;
+
+__device__ __forceinline__ float urow2(float a0, float a1) {
+    float m = fmaxf(a0, a1);
+    if (m == -INFINITY) return INFINITY;
+    return m + fpm::fast_log2(fpm::fast_exp2(a0 - m) + fpm::fast_exp2(a1 - m));
+}
+
+// fixed-order block reduction of two sums (16 waves)
+__device__ __forceinline__ void block_sum2(float& x0, float& x1, float (*red)[16]) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    x0 = wave_sum(x0);
+    x1 = wave_sum(x1);
+    if (lane == 0) { red[0][wv] = x0; red[1][wv] = x1; }
+    __syncthreads();
+    x0 = 0.f; x1 = 0.f;
+    for (int w = 0; w < 16; ++w) { x0 += red[0][w]; x1 += red[1][w]; }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(1024) void soft_topk_bwd_kernel(const float* __restrict__ ss, long sb, long ld,
+                                                             const int* __restrict__ n1, const int* __restrict__ n2,
+                                                             const float* __restrict__ kvec,
+                                                             const int* __restrict__ steps, float tau,
+                                                             const float* __restrict__ dds, long db, long dld,
+                                                             float* __restrict__ dss, int n1max, int n2max,
+                                                             float2* __restrict__ dLws, int* __restrict__ status) {
+    __shared__ float red[2][16];
+    __shared__ float Vh[TOPK_MAX_STEPS / 2 + 2][2];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const int n1b = n1[b], n2b = n2[b];
+    const int N = n1b * n2b;
+    const float* S = ss + (long)b * sb;
+    const float* G = dds + (long)b * db;
+    float* O = dss + (long)b * n1max * n2max;
+    float2* dL = dLws + (long)b * n1max * n2max;
+    const long boxN = (long)n1max * n2max;
+    for (long k = tid; k < boxN; k += 1024) O[k] = 0.f;
+    const int T = steps[b];
+    if (N == 0 || T <= 0) return;
+    if (T > TOPK_MAX_STEPS) {
+        if (tid == 0) status[b] = 1;
+        return;
+    }
+    auto sval = [&](int q) { const int i = q / n2b, j = q - i * n2b; return S[i * ld + j]; };
+    // anchors
+    float mn = INFINITY, mx = -INFINITY;
+    for (int q = tid; q < N; q += 1024) { const float x = sval(q); mn = fminf(mn, x); mx = fmaxf(mx, x); }
+    {
+        float a0 = -mn, a1 = mx;
+        a0 = wave_max(a0);
+        a1 = wave_max(a1);
+        const int lane = tid & 63, wv = tid >> 6;
+        if (lane == 0) { red[0][wv] = a0; red[1][wv] = a1; }
+        __syncthreads();
+        a0 = -INFINITY; a1 = -INFINITY;
+        for (int w = 0; w < 16; ++w) { a0 = fmaxf(a0, red[0][w]); a1 = fmaxf(a1, red[1][w]); }
+        __syncthreads();
+        mn = -a0; mx = a1;
+    }
+    const float dsc = fpm::LOG2E_F / tau;
+    const float kk = kvec[b];
+    const float lcp0 = fpm::fast_log2((float)N - kk), lcp1 = fpm::fast_log2(kk);
+    auto Dq = [&](float x, float& d0, float& d1) {
+        d0 = (-fabsf(x - mn)) * dsc;
+        d1 = (-fabsf(x - mx)) * dsc;
+    };
+    // replay: V history after each column step (Vh[0] = 0)
+    if (tid == 0) { Vh[0][0] = 0.f; Vh[0][1] = 0.f; }
+    __syncthreads();
+    int kc = 0;
+    for (int t = 1; t < T; t += 2) {
+        const float V0 = Vh[kc][0], V1 = Vh[kc][1];
+        float m0 = -INFINITY, m1 = -INFINITY;
+        for (int q = tid; q < N; q += 1024) {
+            float d0, d1;
+            Dq(sval(q), d0, d1);
+            const float uu = urow2(d0 - V0, d1 - V1);
+            m0 = fmaxf(m0, d0 - V0 - uu);
+            m1 = fmaxf(m1, d1 - V1 - uu);
+        }
+        {
+            float a0 = wave_max(m0), a1 = wave_max(m1);
+            const int lane = tid & 63, wv = tid >> 6;
+            if (lane == 0) { red[0][wv] = a0; red[1][wv] = a1; }
+            __syncthreads();
+            m0 = -INFINITY; m1 = -INFINITY;
+            for (int w = 0; w < 16; ++w) { m0 = fmaxf(m0, red[0][w]); m1 = fmaxf(m1, red[1][w]); }
+            __syncthreads();
+        }
+        float s0 = 0.f, s1 = 0.f;
+        for (int q = tid; q < N; q += 1024) {
+            float d0, d1;
+            Dq(sval(q), d0, d1);
+            const float uu = urow2(d0 - V0, d1 - V1);
+            if (m0 != -INFINITY) s0 += fpm::fast_exp2(d0 - V0 - uu - m0);
+            if (m1 != -INFINITY) s1 += fpm::fast_exp2(d1 - V1 - uu - m1);
+        }
+        block_sum2(s0, s1, red);
+        const float lse0 = m0 == -INFINITY ? -INFINITY : m0 + fpm::fast_log2(s0);
+        const float lse1 = m1 == -INFINITY ? -INFINITY : m1 + fpm::fast_log2(s1);
+        if (tid == 0) {
+            Vh[kc + 1][0] = V0 + (lse0 - lcp0);
+            Vh[kc + 1][1] = V1 + (lse1 - lcp1);
+        }
+        __syncthreads();
+        ++kc;
+    }
+    // kc = number of column steps.  Final state: V = Vh[kc]; u from Vh[kc] (last step a row step,
+    // T odd) or Vh[kc - 1] (last step a column step, T even).
+    const bool last_row = (T & 1) == 1;
+    float c0 = 0.f, c1 = 0.f;   // column sums of dL for the next (reverse) column step
+    {
+        const float Vc0 = Vh[kc][0], Vc1 = Vh[kc][1];
+        const int ku = last_row ? kc : kc - 1;
+        const float Vu0 = Vh[ku][0], Vu1 = Vh[ku][1];
+        for (int q = tid; q < N; q += 1024) {
+            const int i = q / n2b, j = q - i * n2b;
+            float d0, d1;
+            Dq(S[i * ld + j], d0, d1);
+            const float uu = urow2(d0 - Vu0, d1 - Vu1);
+            float g0 = 0.f, g1 = G[i * dld + j] * fpm::fast_exp2(d1 - Vc1 - uu);
+            if (last_row) {   // the trailing row step (V = Vh[kc])
+                const float rs = g0 + g1;
+                g0 -= fpm::fast_exp2(d0 - Vc0 - uu) * rs;
+                g1 -= fpm::fast_exp2(d1 - Vc1 - uu) * rs;
+            }
+            dL[q] = make_float2(g0, g1);
+            c0 += g0;
+            c1 += g1;
+        }
+    }
+    // (column step k, then row step with V = Vh[k - 1]) pairs in reverse
+    for (int k = kc; k >= 1; --k) {
+        block_sum2(c0, c1, red);
+        const float cs0 = c0, cs1 = c1;
+        c0 = 0.f; c1 = 0.f;
+        const float Va0 = Vh[k][0], Va1 = Vh[k][1], Vb0 = Vh[k - 1][0], Vb1 = Vh[k - 1][1];
+        for (int q = tid; q < N; q += 1024) {
+            float d0, d1;
+            Dq(sval(q), d0, d1);
+            const float uu = urow2(d0 - Vb0, d1 - Vb1);
+            float2 g = dL[q];
+            // column step: softmax over q of column c = exp(L' - lcp_c)
+            g.x -= fpm::fast_exp2(d0 - Va0 - uu - lcp0) * cs0;
+            g.y -= fpm::fast_exp2(d1 - Va1 - uu - lcp1) * cs1;
+            // row step before it (V = Vh[k-1], same u)
+            const float rs = g.x + g.y;
+            g.x -= fpm::fast_exp2(d0 - Vb0 - uu) * rs;
+            g.y -= fpm::fast_exp2(d1 - Vb1 - uu) * rs;
+            dL[q] = g;
+            c0 += g.x;
+            c1 += g.y;
+        }
+    }
+    // D = -|ss - anchor| / tau: direct term and the anchors' (min / max) share, split evenly among
+    // tied extrema as torch's min()/max() backward does; sgn(0) = 0 as in torch.abs
+    const float itau = 1.f / tau;
+    float da0 = 0.f, da1 = 0.f, cn0 = 0.f, cn1 = 0.f;
+    for (int q = tid; q < N; q += 1024) {
+        const float x = sval(q);
+        const float2 g = dL[q];
+        const float s0 = (x > mn) ? 1.f : ((x < mn) ? -1.f : 0.f);
+        const float s1 = (x > mx) ? 1.f : ((x < mx) ? -1.f : 0.f);
+        da0 += g.x * itau * s0;
+        da1 += g.y * itau * s1;
+        cn0 += x == mn ? 1.f : 0.f;
+        cn1 += x == mx ? 1.f : 0.f;
+    }
+    block_sum2(da0, da1, red);
+    block_sum2(cn0, cn1, red);
+    for (int q = tid; q < N; q += 1024) {
+        const int i = q / n2b, j = q - i * n2b;
+        const float x = S[i * ld + j];
+        const float2 g = dL[q];
+        const float s0 = (x > mn) ? 1.f : ((x < mn) ? -1.f : 0.f);
+        const float s1 = (x > mx) ? 1.f : ((x < mx) ? -1.f : 0.f);
+        float r = -(g.x * s0 + g.y * s1) * itau;
+        if (x == mn) r += da0 / cn0;
+        if (x == mx) r += da1 / cn1;
+        O[(long)i * n2max + j] = r;
+    }
+}
+
+}  // namespace
+
+extern "C" long fpm_sinkhorn_bwd_ws_floats(int B, int n1max, int n2max, int iters) {
+    const long H = (long)(n1max > n2max ? n1max : n2max) + 1;
+    return (long)B * n1max * n2max + (long)B * iters * H;
+}
+
+// s / dP: strided (B, n1max, n2max) views (input of the forward Sinkhorn and gradient of its
+// output); dS: contiguous (B, n1max, n2max), zero outside each pair's valid block.
+extern "C" int fpm_sinkhorn_log_bwd(const float* s, long s_sb, long s_si, long s_sj, const float* dp, long d_sb,
+                                    long d_si, long d_sj, float* ds, const int* n1, const int* n2, int B, int n1max,
+                                    int n2max, int iters, float tau, int dummy_row, float* ws, long ws_floats,
+                                    void* stream) {
+    FPM_CHECK_ARG(iters >= 0 && tau > 0.f, "sinkhorn_bwd: bad iters/tau");
+    FPM_CHECK_ARG(ws_floats >= fpm_sinkhorn_bwd_ws_floats(B, n1max, n2max, iters), "sinkhorn_bwd: workspace too small");
+    FPM_CHECK_ARG(n1max <= 4096 && n2max <= 4096, "sinkhorn_bwd: n1max/n2max must be <= 4096");
+    if (B == 0) return 0;
+    SinkBwdArgs a;
+    a.s = s; a.s_sb = s_sb; a.s_si = s_si; a.s_sj = s_sj;
+    a.dp = dp; a.d_sb = d_sb; a.d_si = d_si; a.d_sj = d_sj;
+    a.ds = ds; a.n1 = n1; a.n2 = n2; a.n1max = n1max; a.n2max = n2max; a.iters = iters; a.tau = tau;
+    a.dummy_row = dummy_row;
+    a.H = (n1max > n2max ? n1max : n2max) + 1;
+    a.dL = ws;
+    a.hist = ws + (long)B * n1max * n2max;
+    const size_t sh = (size_t)3 * a.H * sizeof(float);
+    if (sh > 65536)
+        (void)hipFuncSetAttribute((const void*)sinkhorn_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
+    hipLaunchKernelGGL(sinkhorn_bwd_kernel, dim3(B), dim3(1024), sh, (hipStream_t)stream, a);
+    return fpm::check_launch("fpm_sinkhorn_log_bwd");
+}
+
+extern "C" long fpm_soft_topk_bwd_ws_floats(int B, int n1max, int n2max) {
+    return 2L * B * n1max * n2max;
+}
+
+// ss: (B, n1max, n2max) view with unit column stride (the forward's input), k: the forward's k,
+// steps: the forward's step counts; dds: gradient of ds_mat (unit column stride); dss contiguous.
+// status[b] = 1 if the forward ran more steps than the backward's history holds.
+extern "C" int fpm_soft_topk_bwd(const float* ss, long sb, long ld, const int* n1, const int* n2, const float* k,
+                                 const int* steps, int B, int n1max, int n2max, float tau, const float* dds, long db,
+                                 long dld, float* dss, float* ws, long ws_floats, int* status, void* stream) {
+    FPM_CHECK_ARG(tau > 0.f, "soft_topk_bwd: bad tau");
+    FPM_CHECK_ARG(ws_floats >= fpm_soft_topk_bwd_ws_floats(B, n1max, n2max), "soft_topk_bwd: workspace too small");
+    FPM_CHECK_ARG(steps && status, "soft_topk_bwd: steps and status are required");
+    if (B == 0) return 0;
+    hipLaunchKernelGGL(soft_topk_bwd_kernel, dim3(B), dim3(1024), 0, (hipStream_t)stream, ss, sb, ld, n1, n2, k, steps,
+                       tau, dds, db, dld, dss, n1max, n2max, (float2*)ws, status);
+    return fpm::check_launch("fpm_soft_topk_bwd");
+}

@@ -286,3 +286,75 @@ extern "C" int fpm_node_classifier(const float* X, int B, int n1max, int n2max, 
                        n2max, w, bias, vpart, s, B);
     return fpm::check_launch("fpm_node_classifier");
 }
+
+// ---- training backward -------------------------------------------------
+// The factorised SAGE-mean aggregation alone (no MLPs), in two directions:
+//   adj = 0:  out[c][d][i] = ( sum_{a in T1(i)} sum_{e in T2(d)} X[c][e][a] + D[d][i] X[c][d][i] ) / den[d][i]
+//   adj = 1:  the same traversal of Xs = X / den (0 where den = 0) without the final division,
+// where den[d][i] = deg1(i) deg2(d) + D[d][i] with in-degrees from (q1, q2).  With (T1, T2) the
+// in-edge CSRs, adj = 0 recomputes the forward's agg (gnn_layer_kernel); with the OUT-edge CSRs
+// (the plans of the reversed edge lists), adj = 1 is its transpose, the gradient path
+// dX = A1^T G A2 + D o G, G = dagg / den.  One workgroup per (pair, graph-2 node), one thread per
+// graph-1 node, the graph-2 neighbour sums staged in LDS [c][n1max].
+namespace {
+__global__ __launch_bounds__(1024) void kron_agg_kernel(const float* __restrict__ X, int C, int n1max, int n2max,
+                                                        const int* __restrict__ tptr1, const int* __restrict__ tnbr1,
+                                                        const int* __restrict__ tptr2, const int* __restrict__ tnbr2,
+                                                        const int* __restrict__ q1, const int* __restrict__ q2,
+                                                        const int* __restrict__ n1, const int* __restrict__ n2,
+                                                        int adj, float* __restrict__ out, int B) {
+    extern __shared__ float T[];
+    int d, b;
+    if (!pair_block(n2max, B, b, d)) return;
+    const int i = threadIdx.x;
+    const long N = (long)n1max * n2max;
+    const float* Xb = X + (long)b * C * N;
+    const long nb1 = (long)b * n1max, nb2 = (long)b * n2max;
+    const long nn = (long)n1[b] * n2[b];
+    auto den = [&](int dd, int ii) -> float {
+        const int g1 = q1[nb1 + ii + 1] - q1[nb1 + ii];
+        const int g2 = q2[nb2 + dd + 1] - q2[nb2 + dd];
+        return (float)(g1 * g2 + (((long)dd * n1max + ii) < nn ? 1 : 0));
+    };
+    auto xval = [&](int c, int dd, int ii) -> float {
+        const float x = Xb[(long)c * N + (long)dd * n1max + ii];
+        if (!adj) return x;
+        const float dn = den(dd, ii);
+        return dn > 0.f ? x / dn : 0.f;
+    };
+    if (i < n1max) {
+        const int beg = tptr2[nb2 + d], end = tptr2[nb2 + d + 1];
+        for (int c = 0; c < C; ++c) {
+            float acc = 0.f;
+            for (int e = beg; e < end; ++e) acc += xval(c, tnbr2[e], i);
+            T[c * n1max + i] = acc;
+        }
+    }
+    __syncthreads();
+    if (i >= n1max) return;
+    const int beg = tptr1[nb1 + i], end = tptr1[nb1 + i + 1];
+    const bool self = ((long)d * n1max + i) < nn;
+    const float dn = adj ? 1.f : den(d, i);
+    for (int c = 0; c < C; ++c) {
+        float acc = 0.f;
+        for (int e = beg; e < end; ++e) acc += T[c * n1max + tnbr1[e]];
+        if (self) acc += xval(c, d, i);
+        out[(long)b * C * N + (long)c * N + (long)d * n1max + i] = adj ? acc : (dn > 0.f ? acc / dn : 0.f);
+    }
+}
+}  // namespace
+
+extern "C" int fpm_kron_agg(const float* X, int C, int B, int n1max, int n2max, const int* tptr1, const int* tnbr1,
+                            const int* tptr2, const int* tnbr2, const int* q1, const int* q2, const int* n1,
+                            const int* n2, int adjoint, float* out, void* stream) {
+    FPM_CHECK_ARG(C >= 1 && C <= 32, "kron_agg: C must be in [1, 32]");
+    FPM_CHECK_ARG(n1max <= 1024, "kron_agg: n1max must be <= 1024");
+    if (B == 0) return 0;
+    const size_t sh = (size_t)C * n1max * sizeof(float);
+    if (sh > 65536)
+        (void)hipFuncSetAttribute((const void*)kron_agg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
+    const int threads = (n1max + 63) / 64 * 64;
+    hipLaunchKernelGGL(kron_agg_kernel, dim3(pair_grid(n2max, B)), dim3(threads), sh, (hipStream_t)stream, X, C, n1max,
+                       n2max, tptr1, tnbr1, tptr2, tnbr2, q1, q2, n1, n2, adjoint, out, B);
+    return fpm::check_launch("fpm_kron_agg");
+}

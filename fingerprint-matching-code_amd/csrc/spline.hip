@@ -391,6 +391,113 @@ __global__ __launch_bounds__(256) void combine_kernel(const T* __restrict__ Y, c
     }
 }
 
+
+// ---- training backward -------------------------------------------------
+// Gradient of one SplineConv layer w.r.t. its product rows:  with g the gradient of the layer's
+// pre-activation (mode 0: gout * [out > 0], the F.relu; mode 1: 0.1 * gout, the Siamese residual
+// scale), the max over in-edges routes g[v, c] to the in-edge e* attaining the max (the first one
+// in the deterministic CSR order; messages are recomputed exactly as the forward did), i.e.
+// dY[row(src e*, cell_s)] += basis_s * g, and the root product row of v receives g itself.
+// Several destinations share a (source, cell) row, so those adds are fp32 atomics.
+template <typename T>
+__global__ __launch_bounds__(256) void combine_bwd_kernel(const T* __restrict__ Y, const int* __restrict__ cell_off,
+                                                          const int* __restrict__ dst_ptr,
+                                                          const int4* __restrict__ rows4,
+                                                          const float4* __restrict__ basis4, long num_nodes, int nmax,
+                                                          const int* __restrict__ nvalid, int mode,
+                                                          const float* __restrict__ gout,
+                                                          const float* __restrict__ hout, float* __restrict__ dY) {
+    const int lane = threadIdx.x & 63;
+    const long v = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (v >= num_nodes) return;
+    const int b = (int)(v / nmax), loc = (int)(v - (long)b * nmax);
+    const bool valid = loc < nvalid[b];
+    const int beg = dst_ptr[v], end = dst_ptr[v + 1];
+    const long root_row = (long)cell_off[25] + v;
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+        const int c0 = 4 * lane + 256 * t;
+        float g[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float gv = valid ? gout[v * 768 + c0 + j] : 0.f;
+            if (mode == 0) gv = (valid && hout[v * 768 + c0 + j] > 0.f) ? gv : 0.f;
+            else gv *= 0.1f;
+            g[j] = gv;
+        }
+        *(float4*)(dY + root_row * 768 + c0) = make_float4(g[0], g[1], g[2], g[3]);
+        if (beg >= end) continue;
+        float m[4];
+        int am[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { m[j] = -INFINITY; am[j] = beg; }
+        for (int e = beg; e < end; ++e) {
+            const int4 r = rows4[e];
+            const float4 bs = basis4[e];
+            float a0[4], a1[4], a2[4], a3[4];
+            fpm::load4(Y + (long)r.x * 768 + c0, a0);
+            fpm::load4(Y + (long)r.y * 768 + c0, a1);
+            fpm::load4(Y + (long)r.z * 768 + c0, a2);
+            fpm::load4(Y + (long)r.w * 768 + c0, a3);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float msg = bs.x * a0[j];
+                msg = fmaf(bs.y, a1[j], msg);
+                msg = fmaf(bs.z, a2[j], msg);
+                msg = fmaf(bs.w, a3[j], msg);
+                if (msg > m[j]) { m[j] = msg; am[j] = e; }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (g[j] == 0.f) continue;
+            const int4 r = rows4[am[j]];
+            const float4 bs = basis4[am[j]];
+            unsafeAtomicAdd(dY + (long)r.x * 768 + c0 + j, bs.x * g[j]);
+            unsafeAtomicAdd(dY + (long)r.y * 768 + c0 + j, bs.y * g[j]);
+            unsafeAtomicAdd(dY + (long)r.z * 768 + c0 + j, bs.z * g[j]);
+            unsafeAtomicAdd(dY + (long)r.w * 768 + c0 + j, bs.w * g[j]);
+        }
+    }
+}
+
+// dX[u] (+)= sum over u's product rows (cells in ascending order, then the root) of dXrows[row]:
+// the transpose of the forward's row gather, in a fixed order (no atomics).
+__global__ __launch_bounds__(256) void node_rows_sum_kernel(const float* __restrict__ dXrows,
+                                                            const int* __restrict__ rowid, long num_nodes,
+                                                            int accumulate, float* __restrict__ dX) {
+    const long u = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (u >= num_nodes) return;
+    float acc[3][4];
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[t][j] = 0.f;
+    for (int k = 0; k < NCELL; ++k) {
+        const int r = rowid[u * NCELL + k];
+        if (r < 0) continue;
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            float a[4];
+            fpm::load4(dXrows + (long)r * 768 + 4 * lane + 256 * t, a);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[t][j] += a[j];
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+        float* o = dX + u * 768 + 4 * lane + 256 * t;
+        if (accumulate) {
+            float p[4];
+            fpm::load4(o, p);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[t][j] += p[j];
+        }
+        fpm::store4(o, acc[t]);
+    }
+}
+
 }  // namespace
 
 extern "C" long fpm_spline_plan_bytes(long E, long num_nodes) {
@@ -616,4 +723,70 @@ extern "C" int fpm_profile_read(double* ms_total, double* flops_total, int* coun
     if (ms_total) *ms_total = ms;
     if (flops_total) *flops_total = fl;
     return 0;
+}
+
+extern "C" int fpm_cast_bf16(const float* x, void* out, long n, void* stream);
+
+// Product-row bookkeeping of a plan for the weight gradient: arows[r] = source node of product row
+// r; cell_off[0..26] = row ranges per cell (cell 25 = the root weight).  Device pointers.
+extern "C" int fpm_spline_plan_rows(void* ws, long E, long num_nodes, int** arows, int** cell_off) {
+    PlanLayout L = plan_layout(E, num_nodes);
+    *arows = (int*)((char*)ws + L.arows);
+    *cell_off = (int*)((char*)ws + L.cell_off);
+    return 0;
+}
+
+// Backward of one SplineConv layer w.r.t. its input rows (the weight gradient is the caller's
+// grouped X^T dY product over the same row ranges):
+//   dY   = combine backward (max routing, root rows)                     fp32, max_rows x 768
+//   dXr  = dY_cell W_cell^T per product row: the forward's grouped GEMM with the weights in the
+//          reference's [cell][in][out] layout as the B operand (Wb, 26 x 768 x 768, operand dtype)
+//   dX   = per-node sum of its rows' dXr (accumulate: dX += ...)
+// y_ws: the forward's product rows of this layer; dY_op: bf16 copy of dY (dtype 1 only).
+extern "C" int fpm_spline_conv_bwd_data(int dtype, const void* plan_ws, long E, long num_nodes, int nmax,
+                                        const int* nvalid, const void* Wb, const void* y_ws, int mode,
+                                        const float* gout, const float* hout, float* dY, void* dY_op,
+                                        float* dXrows, float* dX, int accumulate, void* stream) {
+    using namespace fpm;
+    FPM_CHECK_ARG(dtype == 0 || dtype == 1, "spline_conv_bwd: bad dtype");
+    FPM_CHECK_ARG(mode == 1 || (mode == 0 && hout), "spline_conv_bwd: mode 0 needs the layer output");
+    FPM_CHECK_ARG(dtype == 0 || dY_op, "spline_conv_bwd: bf16 needs the dY operand buffer");
+    PlanLayout L = plan_layout(E, num_nodes);
+    const char* w = (const char*)plan_ws;
+    hipStream_t st = (hipStream_t)stream;
+    const int D = 768;
+    (void)hipMemsetAsync(dY, 0, (size_t)L.max_rows * D * sizeof(float), st);
+    const unsigned nb = (unsigned)((num_nodes + 3) / 4);
+    if (dtype == 0)
+        hipLaunchKernelGGL((combine_bwd_kernel<float>), dim3(nb), dim3(256), 0, st, (const float*)y_ws,
+                           (const int*)(w + L.cell_off), (const int*)(w + L.dst_ptr), (const int4*)(w + L.rows4),
+                           (const float4*)(w + L.basis4), num_nodes, nmax, nvalid, mode, gout, hout, dY);
+    else
+        hipLaunchKernelGGL((combine_bwd_kernel<bf16_t>), dim3(nb), dim3(256), 0, st, (const bf16_t*)y_ws,
+                           (const int*)(w + L.cell_off), (const int*)(w + L.dst_ptr), (const int4*)(w + L.rows4),
+                           (const float4*)(w + L.basis4), num_nodes, nmax, nvalid, mode, gout, hout, dY);
+    if (dtype == 1) {
+        int rc = fpm_cast_bf16(dY, dY_op, L.max_rows * D, stream);
+        if (rc) return rc;
+    }
+    GemmParams p = {};
+    p.A = dtype == 0 ? (const void*)dY : (const void*)dY_op; p.lda = D; p.a_rows = nullptr;
+    p.B = Wb; p.ldb = D; p.sB_seg = (long)D * D;
+    p.M = (int)L.max_rows; p.N = D; p.K = D; p.nseg = 1;
+    p.group_off = (const int*)(w + L.cell_off);
+    p.epi = EPI_STORE; p.ldc = D; p.Cf = dXrows;
+    if (dtype == 0) {
+        p.tile_info = (const int*)(w + L.tile_info);
+        p.remap_mtiles = (int)L.max_tiles;
+        hipLaunchKernelGGL((gemm_kernel<float, false>), dim3(remap_grid(D, p.remap_mtiles)), dim3(GTHREADS), 0, st, p);
+    } else {
+        p.tile_info = (const int*)(w + L.tile_info2);
+        p.remap_mtiles = (int)L.max_tiles2;
+        dim3 grid(remap_grid256(D, p.remap_mtiles));
+        if (use_gemm_phase(D)) hipLaunchKernelGGL((gemm_phase_kernel<EPI_STORE, true>), grid, dim3(G2_THREADS), 0, st, p);
+        else hipLaunchKernelGGL((gemm_big_kernel<256, EPI_STORE, true>), grid, dim3(G2_THREADS), 0, st, p);
+    }
+    hipLaunchKernelGGL(node_rows_sum_kernel, dim3(nb), dim3(256), 0, st, dXrows, (const int*)(w + L.rowid), num_nodes,
+                       accumulate, dX);
+    return check_launch("fpm_spline_conv_bwd_data");
 }

@@ -46,7 +46,7 @@ def _build_tree(root, sd):
         if is_buf:
             m.register_buffer(leaf, t.clone())
         else:
-            m.register_parameter(leaf, nn.Parameter(t.clone(), requires_grad=False))
+            m.register_parameter(leaf, nn.Parameter(t.clone()))
 
 
 class Net(nn.Module):
@@ -572,7 +572,13 @@ class Net(nn.Module):
         if bt is None:
             bt = self._batch_from_dict(data_dict, dev)
         gt = data_dict.get("gt_perm_mat")
-        res = self.run(bt, gt_perm=gt, label=data_dict.get("label"))
+        if self.training and torch.is_grad_enabled():
+            # train.py / training_loop.py: differentiable forward, hand-written HIP backward (fpm.train)
+            from .train import run_train
+            res = run_train(self, bt, gt_perm=gt, label=data_dict.get("label"))
+        else:
+            res = self.run(bt, gt_perm=gt, label=data_dict.get("label"))
+        self.last_outputs = res          # all outputs incl. intermediates (s, ss, ...) for inspection
         data_dict.update({
             "ds_mat": res["ds_mat"],
             "perm_mat": res["perm_mat"],

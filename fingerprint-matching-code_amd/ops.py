@@ -275,3 +275,69 @@ def lsa_batch_host(s_host, n1_host, n2_host, nthreads=1):
     if rc != 0:
         raise _lib.FpmError("fpm_lsa_batch_host: pair %d is infeasible or has NaN/-inf costs" % (rc - 1))
     return out
+
+
+# ---- training backward -----------------------------------------------------
+def sinkhorn_bwd(s, dp, ds, n1, n2, iters, tau, dummy_row, ws):
+    """d/ds of ``sinkhorn`` given dp = d/d(out); s, dp: strided (B, n1max, n2max) views; ds contiguous."""
+    _dev(s, dp, ds, n1, n2, ws)
+    B, n1max, n2max = s.shape
+    if tuple(dp.shape) != (B, n1max, n2max) or not ds.is_contiguous() or tuple(ds.shape) != (B, n1max, n2max):
+        raise _lib.FpmError("sinkhorn_bwd: shape mismatch")
+    _lib.call("fpm_sinkhorn_log_bwd", _p(s), s.stride(0), s.stride(1), s.stride(2), _p(dp), dp.stride(0),
+              dp.stride(1), dp.stride(2), _p(ds), _p(n1), _p(n2), B, n1max, n2max, int(iters), float(tau),
+              int(bool(dummy_row)), _p(ws), ws.numel(), _stream(s))
+    return ds
+
+
+def soft_topk_bwd(ss, n1, n2, k, steps, tau, dds):
+    """d/dss of ``soft_topk`` (k and steps as used / returned by the forward) -> (B, n1max, n2max)."""
+    _dev(ss, n1, n2, k, steps, dds)
+    B, n1max, n2max = ss.shape
+    if ss.stride(2) != 1 or dds.stride(2) != 1 or tuple(dds.shape) != (B, n1max, n2max):
+        raise _lib.FpmError("soft_topk_bwd: (B, n1max, n2max) views with unit column stride expected")
+    lib = _lib.load()
+    ws = torch.empty(max(int(lib.fpm_soft_topk_bwd_ws_floats(B, n1max, n2max)), 1), device=ss.device,
+                     dtype=torch.float32)
+    status = torch.zeros(B, device=ss.device, dtype=torch.int32)
+    dss = torch.empty(B, n1max, n2max, device=ss.device, dtype=torch.float32)
+    _lib.call("fpm_soft_topk_bwd", _p(ss), ss.stride(0), ss.stride(1), _p(n1), _p(n2), _p(k), _p(steps), B, n1max,
+              n2max, float(tau), _p(dds), dds.stride(0), dds.stride(1), _p(dss), _p(ws), ws.numel(), _p(status),
+              _stream(ss))
+    if int(status.sum()):
+        raise _lib.FpmError("soft_topk_bwd: forward ran more steps than the backward replay holds")
+    return dss
+
+
+def spline_plan_rows(plan, E, num_nodes):
+    """(arows, cell_off) int32 views into a plan: product row -> source node, per-cell row ranges."""
+    a, c = ctypes.c_void_p(), ctypes.c_void_p()
+    _lib.call("fpm_spline_plan_rows", _p(plan), E, num_nodes, ctypes.byref(a), ctypes.byref(c))
+    base = plan.data_ptr()
+    oa, oc = a.value - base, c.value - base
+    arows = plan[oa:].view(torch.int32)
+    cell_off = plan[oc:oc + 4 * 27].view(torch.int32)
+    return arows, cell_off
+
+
+def spline_conv_bwd_data(x_op, plan, E, num_nodes, nmax, nvalid, Wb, y_ws, mode, gout, hout, dY, dY_op, dXrows, dX,
+                         accumulate=False):
+    """Input gradient of one SplineConv layer (see include/fpm.h); fills dY (product-row grads)."""
+    _dev(plan, nvalid, Wb, y_ws, gout, dY, dXrows, dX)
+    code = _code(x_op)
+    if _code(Wb) != code or tuple(Wb.shape) != (26, 768, 768):
+        raise _lib.FpmError("spline_conv_bwd: Wb must be (26, 768, 768) in the operand dtype")
+    if mode == 0 and hout is None:
+        raise _lib.FpmError("spline_conv_bwd: mode 0 needs the layer output")
+    _lib.call("fpm_spline_conv_bwd_data", code, _p(plan), E, num_nodes, nmax, _p(nvalid), _p(Wb), _p(y_ws), int(mode),
+              _p(gout), _p(hout), _p(dY), _p(dY_op), _p(dXrows), _p(dX), int(bool(accumulate)), _stream(gout))
+
+
+def kron_agg(X, C, B, n1max, n2max, tcsr1, tcsr2, q1, q2, n1, n2, adjoint, out):
+    """Factorised Kronecker SAGE-mean aggregation (adjoint=False: forward agg over the in-edge CSRs
+    tcsr*; adjoint=True: its transpose over the out-edge CSRs).  q1/q2: in-edge CSR pointers."""
+    _dev(X, n1, n2, out)
+    _lib.call("fpm_kron_agg", _p(X), int(C), int(B), int(n1max), int(n2max), ctypes.c_void_p(tcsr1[0]),
+              ctypes.c_void_p(tcsr1[1]), ctypes.c_void_p(tcsr2[0]), ctypes.c_void_p(tcsr2[1]), ctypes.c_void_p(q1),
+              ctypes.c_void_p(q2), _p(n1), _p(n2), int(bool(adjoint)), _p(out), _stream(X))
+    return out

@@ -1,0 +1,421 @@
+"""Training forward + backward of ``Net``.
+
+``Net.forward`` in train mode with autograd enabled (``train.py:449`` / ``training_loop.py:32``:
+``outputs = model(batch)``, then ``PermutationLoss(ds_mat) + ks_loss + cls_loss`` and
+``total_loss.backward()``) builds its graph from the autograd Functions below.  Each one runs the
+same HIP forward kernels as inference and has a hand-written backward:
+
+  * ``SplineLayerFn``  SplineConv (aggr='max') + ReLU / Siamese residual: combine backward (max
+    routing, fp32 atomics into the product rows), the grouped product GEMM with the reference
+    weight layout as B (dX), a per-node row sum, and the weight gradient X_rows^T dY per spline cell
+    (``fpm_spline_conv_bwd_data`` + hipBLASLt for the per-cell weight GEMMs);
+  * ``AffinityFn``     Kp = softplus((X1 o c) X2^T) - 0.5 (batched GEMMs);
+  * ``GnnLayerFn``     PYGNNLayer: Sinkhorn backward (``fpm_sinkhorn_log_bwd``), node MLP algebra,
+    and the Kronecker aggregation's transpose (``fpm_kron_agg`` over the out-edge CSRs);
+  * ``NodeClsFn`` / ``SinkhornFn`` / ``SoftTopkFn`` (``fpm_soft_topk_bwd``, incl. the anchors);
+  * ``AfauFn``         AFA-U: HIP forward, backward by replaying ``afau_torch`` under autograd
+    (``ks`` reads ``ss.detach()``, ngm.py:398, so only the regressor's parameters get gradients).
+
+The MatchClassifier runs as torch conv / batch-norm (MIOpen) in train mode (batch statistics,
+running buffers updated), like the reference module.  The Hungarian + greedy selection carry no
+gradient (``perm_mat`` is a constant mask of ``s``, ngm.py:444-453).  Gradients reach every
+parameter of the matcher and the node / global feature rows; the backbone is not trained here.
+"""
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+from . import afau_torch
+from . import config as C
+from . import ops
+from . import params as P
+
+
+def _op_dtype(mode):
+    return torch.bfloat16 if mode == "bf16" else torch.float32
+
+
+class _Side:
+    """Per-side graph context: spline plan (in-edge CSR), reversed plan (out-edge CSR)."""
+
+    def __init__(self, bt, side):
+        self.bt, self.side = bt, side
+        self.nmax = bt.nmax[side]
+        self.num_nodes = bt.B * self.nmax
+        self.E = bt.E[side]
+        self.nvalid = bt.n[side]
+        self.plan = ops.spline_plan(bt.src[side], bt.dst[side], bt.pseudo[side], self.num_nodes, self.nmax)
+        self.csr = ops.plan_csr(self.plan, self.E, self.num_nodes)
+        self._rplan = None
+
+    def out_csr(self):
+        if self._rplan is None:
+            bt = self.bt
+            self._rplan = ops.spline_plan(bt.dst[self.side], bt.src[self.side], bt.pseudo[self.side],
+                                          self.num_nodes, self.nmax)
+        return ops.plan_csr(self._rplan, self.E, self.num_nodes)
+
+
+class SplineLayerFn(torch.autograd.Function):
+    """mode 0: relu(SplineConv(x)); mode 1: xres + 0.1 * SplineConv(x)   (spline_conv.py:33-38, 56)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, root, bias, xres, sd, mode, dmode):
+        op = _op_dtype(dmode)
+        Wf = torch.cat([weight.detach().transpose(1, 2), root.detach().t()[None]]).contiguous().to(op)
+        x_op = x.detach().to(op).contiguous()
+        code = ops.BF16 if op == torch.bfloat16 else ops.F32
+        yws = ops.spline_y_ws(code, sd.E, sd.num_nodes, x.device)
+        out = torch.empty(sd.num_nodes, C.NODE_FEATURE_DIM, device=x.device, dtype=torch.float32)
+        ops.spline_conv(x_op, sd.plan, sd.E, sd.num_nodes, sd.nmax, sd.nvalid, Wf, bias.detach().contiguous(), yws,
+                        mode, xres=None if xres is None else xres.detach().contiguous(), out_f=out)
+        ctx.sd, ctx.mode, ctx.dmode, ctx.has_res = sd, mode, dmode, xres is not None
+        ctx.save_for_backward(x_op, weight, root, out if mode == 0 else None)
+        ctx.yws = yws
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        sd, mode = ctx.sd, ctx.mode
+        x_op, weight, root, out = ctx.saved_tensors
+        op = _op_dtype(ctx.dmode)
+        dev = gout.device
+        gout = gout.contiguous().float()
+        Wb = torch.cat([weight.detach(), root.detach()[None]]).contiguous().to(op)
+        nbytes = _lib.load().fpm_spline_y_bytes(ops.F32, sd.E, sd.num_nodes)
+        rows_max = nbytes // (4 * C.NODE_FEATURE_DIM)
+        dY = torch.empty(rows_max, C.NODE_FEATURE_DIM, device=dev, dtype=torch.float32)
+        dXr = torch.empty_like(dY)
+        dY_op = dY.to(op) if op == torch.bfloat16 else None
+        dX = torch.empty(sd.num_nodes, C.NODE_FEATURE_DIM, device=dev, dtype=torch.float32)
+        ops.spline_conv_bwd_data(x_op, sd.plan, sd.E, sd.num_nodes, sd.nmax, sd.nvalid, Wb, ctx.yws, mode, gout,
+                                 out, dY, dY_op, dXr, dX)
+        arows, cell_off = ops.spline_plan_rows(sd.plan, sd.E, sd.num_nodes)
+        off = cell_off.cpu().tolist()
+        total = off[-1]
+        rows = arows[:total].long()
+        dW = torch.zeros(C.SPLINE_CELLS + 1, C.NODE_FEATURE_DIM, C.NODE_FEATURE_DIM, device=dev, dtype=torch.float32)
+        if total > 0:
+            xg = x_op.index_select(0, rows)
+            dyg = dY_op[:total] if dY_op is not None else dY[:total]
+            for k in range(C.SPLINE_CELLS + 1):
+                r0, r1 = off[k], off[k + 1]
+                if r1 > r0:
+                    dW[k] = torch.mm(xg[r0:r1].t(), dyg[r0:r1]).float()   # [in][out], reference layout
+        dbias = dY[off[25]:off[26]].sum(0)
+        gx = dX
+        gres = gout if ctx.has_res else None
+        return gx, dW[:C.SPLINE_CELLS], dW[C.SPLINE_CELLS], dbias, gres, None, None, None
+
+
+class AffinityFn(torch.autograd.Function):
+    """emb0[b][j][i] = softplus((x1_i o c_b) . x2_j) - 0.5 on the valid block, 0 elsewhere
+    (affinity_layer.py:11-19, pad_tensor + transpose at ngm.py:317-321)."""
+
+    @staticmethod
+    def forward(ctx, x1, x2, coef, bt, dmode):
+        B, n1max, n2max = bt.B, bt.n1max, bt.n2max
+        D = C.NODE_FEATURE_DIM
+        op = _op_dtype(dmode)
+        x1c = (x1.detach().view(B, n1max, D) * coef.detach()[:, None, :]).reshape(B * n1max, D)
+        X = torch.empty(B, 1, n2max, n1max, device=x1.device, dtype=torch.float32)
+        ops.gemm(x2.detach().to(op).contiguous(), x1c.to(op).contiguous(), n2max, n1max, D, D, D, batch=B,
+                 sA=n2max * D, sB=n1max * D, epi=ops.EPI_AFFINITY, out_f=X, ldc=n1max, sC=n1max * n2max,
+                 n1=bt.n1, n2=bt.n2)
+        ctx.bt = bt
+        ctx.save_for_backward(x1, x2, coef, X)
+        return X
+
+    @staticmethod
+    def backward(ctx, gX):
+        x1, x2, coef, X = ctx.saved_tensors
+        bt = ctx.bt
+        B, n1max, n2max = bt.B, bt.n1max, bt.n2max
+        D = C.NODE_FEATURE_DIM
+        j = torch.arange(n2max, device=X.device)[None, :, None]
+        i = torch.arange(n1max, device=X.device)[None, None, :]
+        valid = (j < bt.n2.view(-1, 1, 1)) & (i < bt.n1.view(-1, 1, 1))
+        E = X[:, 0]
+        dZ = torch.where(valid, gX[:, 0] * -torch.expm1(-(E + 0.5)), torch.zeros((), device=X.device))  # softplus'
+        x1v = x1.view(B, n1max, D)
+        x2v = x2.view(B, n2max, D)
+        x1c = x1v * coef[:, None, :]
+        dx2 = torch.bmm(dZ, x1c)                     # (B, n2max, D)
+        dx1c = torch.bmm(dZ.transpose(1, 2), x2v)    # (B, n1max, D)
+        dx1 = dx1c * coef[:, None, :]
+        dcoef = (dx1c * x1v).sum(1)
+        return dx1.reshape(B * n1max, D), dx2.reshape(B * n2max, D), dcoef, None, None
+
+
+def _gnn_pack(Wl, bl, Wr, W1, b1, W2, b2, wc, bc):
+    parts = [Wl.t(), bl, Wr.t(), W1.t(), b1, W2.t(), b2, wc, bc]
+    return torch.cat([t.detach().reshape(-1).float() for t in parts]).contiguous()
+
+
+class GnnLayerFn(torch.autograd.Function):
+    """PYGNNLayer.forward (gnn.py:207-226) on the factorised Kronecker pattern:
+    X (B, Cin, n2max, n1max) -> (B, 17, n2max, n1max) = [x1 || Sinkhorn(classifier(x1))]."""
+
+    @staticmethod
+    def forward(ctx, X, Wl, bl, Wr, W1, b1, W2, b2, wc, bc, g):
+        B, n1max, n2max = g.bt.B, g.bt.n1max, g.bt.n2max
+        Cin = X.shape[1]
+        dev = X.device
+        Xc = X.detach().contiguous()
+        Xn = torch.empty(B, 17, n2max, n1max, device=dev, dtype=torch.float32)
+        zbuf = torch.empty(B, n2max, n1max, device=dev, dtype=torch.float32)
+        ops.gnn_layer(Xc, Cin, B, n1max, n2max, g.s0.csr, g.s1.csr, g.bt.n1, g.bt.n2,
+                      _gnn_pack(Wl, bl, Wr, W1, b1, W2, b2, wc, bc), Xn, zbuf)
+        ops.sinkhorn(zbuf.transpose(1, 2), g.bt.n1, g.bt.n2, C.GNN_SK_ITER, C.SK_TAU, True,
+                     out=Xn[:, 16].transpose(1, 2))
+        ctx.g = g
+        ctx.save_for_backward(Xc, Xn, zbuf, Wl, Wr, W1, b1, W2, b2, wc)
+        return Xn
+
+    @staticmethod
+    def backward(ctx, gXn):
+        g = ctx.g
+        bt = g.bt
+        Xc, Xn, zbuf, Wl, Wr, W1, b1, W2, b2, wc = ctx.saved_tensors
+        B, n1max, n2max = bt.B, bt.n1max, bt.n2max
+        N = n1max * n2max
+        Cin = Xc.shape[1]
+        gXn = gXn.contiguous()
+        # Sinkhorn(20) on Z[i][j] = z[j*n1max + i]
+        dz = sinkhorn_bwd(zbuf.transpose(1, 2), gXn[:, 16].transpose(1, 2), bt.n1, bt.n2, C.GNN_SK_ITER,
+                          C.SK_TAU, True).transpose(1, 2).reshape(B, N)
+        x1 = Xn[:, :16].reshape(B, 16, N)
+        dx1 = gXn[:, :16].reshape(B, 16, N) + wc.reshape(16)[None, :, None] * dz[:, None, :]
+        dwc = torch.einsum("bp,bop->o", dz, x1)[None]
+        dbc = dz.sum().reshape(1)
+        Xf = Xc.view(B, Cin, N)
+        agg = torch.empty_like(Xc)
+        ops.kron_agg(Xc, Cin, B, n1max, n2max, g.s0.csr, g.s1.csr, g.s0.csr[0], g.s1.csr[0], bt.n1, bt.n2, False, agg)
+        agg = agg.view(B, Cin, N)
+        h1p = torch.einsum("mc,bcp->bmp", W1, Xf) + b1[None, :, None]
+        h1 = F.relu(h1p)
+        h2p = torch.einsum("om,bmp->bop", W2, h1) + b2[None, :, None]
+        dm = dx1 * (h2p > 0)
+        dW2 = torch.einsum("bop,bmp->om", dm, h1)
+        db2 = dm.sum((0, 2))
+        dh1 = torch.einsum("om,bop->bmp", W2, dm) * (h1p > 0)
+        dW1 = torch.einsum("bmp,bcp->mc", dh1, Xf)
+        db1 = dh1.sum((0, 2))
+        dWl = torch.einsum("bop,bcp->oc", dx1, agg)
+        dbl = dx1.sum((0, 2))
+        dWr = torch.einsum("bop,bcp->oc", dx1, Xf)
+        dX = torch.einsum("mc,bmp->bcp", W1, dh1) + torch.einsum("oc,bop->bcp", Wr, dx1)
+        dagg = torch.einsum("oc,bop->bcp", Wl, dx1).contiguous()
+        dXa = torch.empty(B, Cin, n2max, n1max, device=Xc.device, dtype=torch.float32)
+        ops.kron_agg(dagg.view(B, Cin, n2max, n1max), Cin, B, n1max, n2max, g.s0.out_csr(), g.s1.out_csr(),
+                     g.s0.csr[0], g.s1.csr[0], bt.n1, bt.n2, True, dXa)
+        dX = (dX.view(B, Cin, n2max, n1max) + dXa)
+        return dX, dWl, dbl, dWr, dW1, db1, dW2, db2, dwc, dbc, None
+
+
+class NodeClsFn(torch.autograd.Function):
+    """v = classifier(emb) (ngm.py:368) read as s[b][i][j] = v[b][j*n1max + i] (ngm.py:369)."""
+
+    @staticmethod
+    def forward(ctx, X, w, b, bt):
+        B, n1max, n2max = bt.B, bt.n1max, bt.n2max
+        s = torch.empty(B, n1max, n2max, device=X.device, dtype=torch.float32)
+        ops.node_classifier(X.detach().contiguous(), B, n1max, n2max, w.detach().reshape(-1).contiguous(),
+                            b.detach().contiguous(), s)
+        ctx.save_for_backward(X, w)
+        return s
+
+    @staticmethod
+    def backward(ctx, gs):
+        X, w = ctx.saved_tensors
+        gT = gs.transpose(1, 2)                                    # (B, n2max, n1max)
+        dX = w.reshape(-1)[None, :, None, None] * gT[:, None]
+        dw = torch.einsum("bji,bcji->c", gT, X)[None]
+        db = gs.sum().reshape(1)
+        return dX, dw, db, None
+
+
+def sinkhorn_bwd(s, dp, n1, n2, iters, tau, dummy_row):
+    """Gradient of ops.sinkhorn w.r.t. its input view ``s`` -> contiguous (B, n1max, n2max)."""
+    B, n1max, n2max = s.shape
+    lib = _lib.load()
+    nws = int(lib.fpm_sinkhorn_bwd_ws_floats(B, n1max, n2max, int(iters)))
+    ws = torch.empty(max(nws, 1), device=s.device, dtype=torch.float32)
+    ds = torch.empty(B, n1max, n2max, device=s.device, dtype=torch.float32)
+    ops.sinkhorn_bwd(s, dp, ds, n1, n2, iters, tau, dummy_row, ws)
+    return ds
+
+
+class SinkhornFn(torch.autograd.Function):
+    """Sinkhorn(max_iter, tau)(s, n1, n2, dummy_row=True) (sinkhorn.py:85-87, ngm.py:371)."""
+
+    @staticmethod
+    def forward(ctx, s, n1, n2, iters, tau):
+        sc = s.detach().contiguous()
+        out = ops.sinkhorn(sc, n1, n2, iters, tau, True)
+        ctx.save_for_backward(sc, n1, n2)
+        ctx.iters, ctx.tau = iters, tau
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        sc, n1, n2 = ctx.saved_tensors
+        return sinkhorn_bwd(sc, g.contiguous(), n1, n2, ctx.iters, ctx.tau, True), None, None, None, None
+
+
+class SoftTopkFn(torch.autograd.Function):
+    """soft_topk(ss, k, SK_ITER_NUM, tau, n1, n2, True)[1] (ngm.py:418-439)."""
+
+    @staticmethod
+    def forward(ctx, ss, k, n1, n2, iters, tau):
+        B = ss.shape[0]
+        ssc = ss.detach().contiguous()
+        kc = k.detach().float().contiguous()
+        steps = torch.empty(B, device=ss.device, dtype=torch.int32)
+        out = ops.soft_topk(ssc, n1, n2, kc, iters, tau, steps=steps)
+        ctx.save_for_backward(ssc, kc, steps, n1, n2)
+        ctx.tau = tau
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        ssc, kc, steps, n1, n2 = ctx.saved_tensors
+        dss = ops.soft_topk_bwd(ssc, n1, n2, kc, steps, ctx.tau, g.contiguous())
+        return dss, None, None, None, None, None
+
+
+class AfauFn(torch.autograd.Function):
+    """ks from the HIP AFA-U forward; gradients by replaying ``afau_torch`` under autograd."""
+
+    @staticmethod
+    def forward(ctx, ss, net, bt, *params):
+        ks = net._afau(net.packed(ss.device), ss.detach().contiguous(), bt)
+        ctx.net, ctx.bt = net, bt
+        ctx.save_for_backward(ss, *params)
+        return ks
+
+    @staticmethod
+    def backward(ctx, gks):
+        ss, *params = ctx.saved_tensors
+        net, bt = ctx.net, ctx.bt
+        names = net._afau_names
+        with torch.enable_grad():
+            leaves = [p.detach().requires_grad_(True) for p in params]
+            pm = dict(zip(names, leaves))
+            ks = afau_torch.afau_ks(ss.detach(), bt.n1, bt.n2, lambda k: pm[k])
+            grads = torch.autograd.grad(ks, leaves, gks, allow_unused=True)
+        grads = [torch.zeros_like(p) if gr is None else gr for p, gr in zip(params, grads)]
+        return (None, None, None) + tuple(grads)
+
+
+def match_cls_train(m, P_, B_):
+    """MatchClassifier.forward (ngm.py:75-106) with BatchNorm2d in train mode (batch statistics,
+    running buffers updated with momentum 0.1)."""
+    x = m.unsqueeze(1)
+    for ci, bi in ((0, 2), (4, 6)):
+        x = F.conv2d(x, P_("match_cls.conv.%d.weight" % ci), P_("match_cls.conv.%d.bias" % ci), padding=1)
+        x = F.relu(x)
+        x = F.batch_norm(x, B_("match_cls.conv.%d.running_mean" % bi), B_("match_cls.conv.%d.running_var" % bi),
+                         P_("match_cls.conv.%d.weight" % bi), P_("match_cls.conv.%d.bias" % bi), True, 0.1, C.BN_EPS)
+        nbt = B_("match_cls.conv.%d.num_batches_tracked" % bi)
+        nbt.add_(1)
+        x = F.max_pool2d(x, 2)
+    x = F.adaptive_avg_pool2d(x, 1).view(x.shape[0], -1)
+    return F.linear(x, P_("match_cls.fc.weight"), P_("match_cls.fc.bias")).squeeze(-1)
+
+
+class _GnnCtx:
+    def __init__(self, bt, s0, s1):
+        self.bt, self.s0, self.s1 = bt, s0, s1
+
+
+def run_train(net, bt, gt_perm=None, label=None):
+    """Differentiable forward of ``Net`` (train mode) over one DeviceBatch; returns the
+    data_dict outputs (ngm.py:479-487) plus ``s`` / ``ss``."""
+    if bt.shared0 and bt.B > 1:
+        raise NotImplementedError("training on shared-probe batches: pass per-pair graphs")
+    dev = bt.device
+    B, n1max, n2max = bt.B, bt.n1max, bt.n2max
+    pd = dict(net.named_parameters())
+    bd = dict(net.named_buffers())
+    off = [k for k, v in pd.items() if v.device != dev and not k.startswith(("node_layers", "edge_layers", "final_layers"))]
+    if off:
+        raise _lib.FpmError("training needs the matcher's parameters on %s (model.to(device), as train.py does); "
+                            "%s is on %s" % (dev, off[0], pd[off[0]].device))
+    Pm = lambda k: pd[k]
+    Bm = lambda k: bd[k]
+    dmode = net.dtype_mode
+    # global weights + vertex-affinity coefficients (ngm.py:262-268, affinity_layer.py:13)
+    gw = torch.cat([bt.w[0], bt.w[1]], dim=1)
+    gw = gw / torch.norm(gw, dim=1, keepdim=True)
+    coef = torch.tanh(F.linear(gw, Pm("vertex_affinity.A.weight"), Pm("vertex_affinity.A.bias")))
+    sides = [_Side(bt, 0), _Side(bt, 1)]
+    feats = []
+    for side in range(2):
+        sd = sides[side]
+        x0 = bt.x[side]
+        pre = P.SPLINE_PREFIX
+        h = SplineLayerFn.apply(x0, Pm(pre + ".0.weight"), Pm(pre + ".0.root"), Pm(pre + ".0.bias"), None, sd, 0,
+                                dmode)
+        o = SplineLayerFn.apply(h, Pm(pre + ".1.weight"), Pm(pre + ".1.root"), Pm(pre + ".1.bias"), x0, sd, 1,
+                                dmode)
+        feats.append(o)
+    X = AffinityFn.apply(feats[0], feats[1], coef, bt, dmode)
+    g = _GnnCtx(bt, sides[0], sides[1])
+    for l in range(C.GNN_LAYER):
+        p = "gnn_layer_%d." % l
+        X = GnnLayerFn.apply(X, Pm(p + "conv2.lin_l.weight"), Pm(p + "conv2.lin_l.bias"), Pm(p + "conv2.lin_r.weight"),
+                             Pm(p + "n_self_func.0.weight"), Pm(p + "n_self_func.0.bias"),
+                             Pm(p + "n_self_func.2.weight"), Pm(p + "n_self_func.2.bias"),
+                             Pm(p + "classifier.weight"), Pm(p + "classifier.bias"), g)
+    s = NodeClsFn.apply(X, Pm("classifier.weight"), Pm("classifier.bias"), bt)
+    ss = SinkhornFn.apply(s, bt.n1, bt.n2, C.SK_ITER_NUM, net.tau)
+    min_pt = torch.minimum(bt.n1, bt.n2).to(torch.float32)
+    if gt_perm is None:
+        gt_ks = min_pt.clone()
+    else:
+        gt_ks = torch.as_tensor(gt_perm).to(dev).reshape(B, -1).sum(-1).to(torch.float32)
+    if net.regression:
+        names = [k for k in pd if k.startswith(afau_torch.AFAU_PARAM_PREFIXES)]
+        net._afau_names = names
+        ks = AfauFn.apply(ss.detach(), net, bt, *[pd[k] for k in names])
+    else:
+        ks = gt_ks / min_pt
+    ds = SoftTopkFn.apply(ss, gt_ks, bt.n1, bt.n2, C.SK_ITER_NUM, net.tau)
+    with torch.no_grad():
+        kk = (ks.detach() * min_pt).contiguous()
+        dsd = ds.detach()
+        if net.lsa_mode == "device":
+            assign, status = ops.lsa_batch_device(dsd, bt.n1, bt.n2)
+            torch.cuda.current_stream(dev).synchronize()
+            if int(status.abs().sum()):
+                raise RuntimeError("hungarian: infeasible or NaN/-inf costs")
+        else:
+            assign = ops.lsa_batch_host(dsd.cpu(), bt.n_host[0], bt.n_host[1], net.lsa_threads).to(dev)
+        lsa = torch.empty_like(dsd)
+        perm = ops.topk_select(dsd, assign, kk, lsa_out=lsa)
+    logits = match_cls_train(s * perm, Pm, Bm)
+    res = dict(ds_mat=ds, perm_mat=perm, k_prob=ks, cls_logits=logits, cls_prob=torch.sigmoid(logits), s=s, ss=ss,
+               lsa=lsa)
+    if label is not None:
+        res["cls_loss"] = F.binary_cross_entropy_with_logits(logits, torch.as_tensor(label).to(dev).view(-1).float())
+    else:
+        res["cls_loss"] = torch.tensor(0.0, device=dev)
+    if net.regression:
+        res["ks_loss"] = F.mse_loss(ks, gt_ks / min_pt) * net.k_factor
+        res["ks_error"] = F.l1_loss(ks * min_pt, gt_ks)
+    else:
+        res["ks_loss"] = 0.0
+        res["ks_error"] = 0.0
+    return res
+
+
+def permutation_loss(ds, gt, n1, n2):
+    """PermutationLoss (src/loss_func.py:26-57): per-pair BCE over the valid blocks, summed, / sum(n1)."""
+    n1h = [int(v) for v in torch.as_tensor(n1).view(-1).tolist()]
+    n2h = [int(v) for v in torch.as_tensor(n2).view(-1).tolist()]
+    gt = torch.as_tensor(gt).to(ds.device, ds.dtype)
+    loss = ds.new_zeros(())
+    for b, (r, c) in enumerate(zip(n1h, n2h)):
+        loss = loss + F.binary_cross_entropy(ds[b, :r, :c], gt[b, :r, :c], reduction="sum")
+    return loss / float(sum(n1h))

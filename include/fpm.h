@@ -223,6 +223,45 @@ int fpm_profile_read(double* ms_total, double* flops_total, int* count);
 int fpm_lsa_batch_device(const float* s, long sb, long ld, const int* n1, const int* n2, int B, int n1max, int n2max,
                          int* assign, int* status, void* stream);
 
+/* ---- training backward ----------------------------------------------------
+ * Vector-Jacobian products of the forward ops above for train.py's stages
+ * (src/train/training_loop.py:32-60: PermutationLoss(ds_mat) + ks_loss + cls_loss, .backward()).
+ * The reference gets these from autograd through PyG / torch_sparse / pygmtools / torch ops.
+ *
+ * Sinkhorn (sinkhorn.py:85-87 -> pygm.sinkhorn): s and dp are strided (B, n1max, n2max) views of
+ * the forward's input and of the gradient of its output; ds (contiguous box) receives d/ds, zero
+ * outside each valid block.  ws: fpm_sinkhorn_bwd_ws_floats(...) floats.  Deterministic. */
+long fpm_sinkhorn_bwd_ws_floats(int B, int n1max, int n2max, int iters);
+int fpm_sinkhorn_log_bwd(const float* s, long s_sb, long s_si, long s_sj, const float* dp, long d_sb, long d_si,
+                         long d_sj, float* ds, const int* n1, const int* n2, int B, int n1max, int n2max, int iters,
+                         float tau, int dummy_row, float* ws, long ws_floats, void* stream);
+/* soft top-k (soft_topk.py:23-45 + Sinkhorn_m.forward_log :166-255, incl. the continuation):
+ * ss / k / steps as given to / returned by fpm_soft_topk_fwd; dds: gradient of ds_mat; dss
+ * (contiguous box) receives d/dss (anchor min/max share split over ties like torch's min()/max()).
+ * status[b] = 1 if the forward ran more steps than the replay holds (4096).  No gradient for k. */
+long fpm_soft_topk_bwd_ws_floats(int B, int n1max, int n2max);
+int fpm_soft_topk_bwd(const float* ss, long sb, long ld, const int* n1, const int* n2, const float* k,
+                      const int* steps, int B, int n1max, int n2max, float tau, const float* dds, long db, long dld,
+                      float* dss, float* ws, long ws_floats, int* status, void* stream);
+/* SplineConv layer w.r.t. its input (PyG SplineConv aggr='max' under SConv, spline_conv.py:17,
+ * 33-38): mode 0 = conv 0 + F.relu (hout = the layer's output), mode 1 = conv 1 under the Siamese
+ * residual (x + 0.1 * conv).  y_ws: the forward's product rows of this layer; Wb: (26, 768 in,
+ * 768 out) = the reference's weight layout then root, operand dtype.  dY (fp32, fpm_spline_y_bytes
+ * of dtype 0) receives the product-row gradients (the weight gradient is X_rows^T dY per cell, row
+ * ranges from fpm_spline_plan_rows); dY_op: bf16 copy (dtype 1); dXrows: fp32 like dY; dX (num_nodes,
+ * 768) fp32, overwritten or accumulated. */
+int fpm_spline_plan_rows(void* plan_ws, long E, long num_nodes, int** arows, int** cell_off);
+int fpm_spline_conv_bwd_data(int dtype, const void* plan_ws, long E, long num_nodes, int nmax, const int* nvalid,
+                             const void* Wb, const void* y_ws, int mode, const float* gout, const float* hout,
+                             float* dY, void* dY_op, float* dXrows, float* dX, int accumulate, void* stream);
+/* Factorised Kronecker SAGE-mean aggregation alone (SAGEConv mean over the association pattern,
+ * gnn.py:208 / ngm.py:339-344): adjoint = 0 recomputes the forward's agg (T = in-edge CSRs);
+ * adjoint = 1 with T = out-edge CSRs is its transpose (dX = A1^T (dagg / den) A2 + D o dagg / den).
+ * q1, q2: in-edge CSR pointers (degrees for den).  X / out: (B, C, n2max, n1max) fp32. */
+int fpm_kron_agg(const float* X, int C, int B, int n1max, int n2max, const int* tptr1, const int* tnbr1,
+                 const int* tptr2, const int* tnbr2, const int* q1, const int* q2, const int* n1, const int* n2,
+                 int adjoint, float* out, void* stream);
+
 /* ---- host: batched linear sum assignment ------------------------------------------------------
  * Replaces utils/hungarian.py:8-66 (scipy linear_sum_assignment on -s, per pair).  Synchronous,
  * HOST memory, nthreads worker threads.  assign[b][r] = column or -1.  Returns 0 or (pair + 1). */

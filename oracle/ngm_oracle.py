@@ -22,7 +22,7 @@ __all__ = [
     "spline_basis", "spline_conv", "siamese_sconv", "edge_diff", "global_weights", "affinity",
     "kron_pattern", "pattern_mean_explicit", "pattern_mean_factorized", "pygm_sinkhorn",
     "gnn_layer", "afau_encoder", "afau_ks", "sinkhorn_m", "soft_topk", "hungarian",
-    "greedy_perm", "match_classifier", "gconv", "forward",
+    "greedy_perm", "match_classifier", "gconv", "forward", "permutation_loss",
 ]
 
 
@@ -355,15 +355,18 @@ def greedy_perm(x, top_indices, ks):
 # ----------------------------------------------------------------------------------------------
 # MatchClassifier (ngm.py:75-106), eval-mode BatchNorm (running stats)
 # ----------------------------------------------------------------------------------------------
-def match_classifier(m, sd, eps=1e-5):
+def match_classifier(m, sd, eps=1e-5, training=False):
+    """``training``: BatchNorm2d in train mode (batch statistics; the running buffers in ``sd``
+    are updated in place with momentum 0.1, as nn.BatchNorm2d does)."""
     dt = m.dtype
     g = lambda k: sd[k].to(dt)
     x = m.unsqueeze(1)
     for ci, bi in ((0, 2), (4, 6)):
         x = F.conv2d(x, g("match_cls.conv.%d.weight" % ci), g("match_cls.conv.%d.bias" % ci), padding=1)
         x = F.relu(x)
-        x = F.batch_norm(x, g("match_cls.conv.%d.running_mean" % bi), g("match_cls.conv.%d.running_var" % bi),
-                         g("match_cls.conv.%d.weight" % bi), g("match_cls.conv.%d.bias" % bi), False, 0.0, eps)
+        rs = (lambda k: sd[k]) if training else g
+        x = F.batch_norm(x, rs("match_cls.conv.%d.running_mean" % bi), rs("match_cls.conv.%d.running_var" % bi),
+                         g("match_cls.conv.%d.weight" % bi), g("match_cls.conv.%d.bias" % bi), training, 0.1, eps)
         x = F.max_pool2d(x, 2)
     x = F.adaptive_avg_pool2d(x, 1).view(x.shape[0], -1)
     return F.linear(x, g("match_cls.fc.weight"), g("match_cls.fc.bias")).squeeze(-1)
@@ -441,7 +444,7 @@ def forward(pairs, sd, regression=True, training=False, gt_perm=None, labels=Non
             gt_perm[b, torch.arange(m), torch.arange(m)] = 1
     gt_ks = gt_perm.reshape(B, -1).sum(-1).to(dtype)
     if regression:
-        ks = afau_ks(ss, n1, n2, sd)
+        ks = afau_ks(ss.detach(), n1, n2, sd)          # encoder_k(..., ss.detach()), ngm.py:398
     else:
         ks = gt_ks / min_pt
     k_used = gt_ks.view(-1) if training else ks.view(-1) * min_pt
@@ -449,7 +452,7 @@ def forward(pairs, sd, regression=True, training=False, gt_perm=None, labels=Non
     x = hungarian(ds, n1, n2).to(dtype)
     top = torch.argsort(x.mul(ds).reshape(B, -1), descending=True, dim=-1)
     perm = greedy_perm(torch.zeros_like(ds), top, ks.view(-1) * min_pt)
-    logits = match_classifier(s * perm, sd)
+    logits = match_classifier(s * perm, sd, training=training)
     cls_prob = torch.sigmoid(logits)
     out = dict(ds_mat=ds, perm_mat=perm, k_prob=ks, cls_prob=cls_prob, cls_logits=logits,
                s=s, ss=ss, Kp=Kp, lsa=x)
@@ -466,3 +469,16 @@ def forward(pairs, sd, regression=True, training=False, gt_perm=None, labels=Non
         out["ks_loss"] = 0.0
         out["ks_error"] = 0.0
     return out
+
+
+# ----------------------------------------------------------------------------------------------
+# PermutationLoss (src/loss_func.py:26-57): sum of per-pair BCE over the valid blocks / sum(n1)
+# ----------------------------------------------------------------------------------------------
+def permutation_loss(ds, gt, n1, n2):
+    loss = ds.new_zeros(())
+    n_sum = ds.new_zeros(())
+    for b in range(ds.shape[0]):
+        r, c = int(n1[b]), int(n2[b])
+        loss = loss + F.binary_cross_entropy(ds[b, :r, :c], gt[b, :r, :c].to(ds.dtype), reduction="sum")
+        n_sum = n_sum + r
+    return loss / n_sum
