@@ -65,6 +65,7 @@ SIGNATURES = {
     "fpm_spline_plan_rows": (I, [P, L, L, ctypes.POINTER(P), ctypes.POINTER(P)]),
     "fpm_spline_conv_bwd_data": (I, [I, P, L, L, I, P, P, P, I, P, P, P, P, P, P, I, P]),
     "fpm_kron_agg": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, I, P, P]),
+    "fpm_kron_gnn_layer_bwd_point": (I, [P, I, I, I, I, P, P, P, P, P, P, P]),
     "fpm_profile_enable": (I, [I]),
     "fpm_profile_read": (I, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(I)]),

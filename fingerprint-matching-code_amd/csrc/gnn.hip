@@ -358,3 +358,94 @@ extern "C" int fpm_kron_agg(const float* X, int C, int B, int n1max, int n2max, 
                        n2max, tptr1, tnbr1, tptr2, tnbr2, q1, q2, n1, n2, adjoint, out, B);
     return fpm::check_launch("fpm_kron_agg");
 }
+
+// Per-position part of the PYGNNLayer backward (the node MLPs of gnn_layer_kernel, transposed):
+// with dx1 = dXn[0:16] + wc * dz (classifier), recompute h1 = relu(W1 x + b1), h2 = W2 h1 + b2,
+//   dm = dx1 o [h2 > 0],  dh1 = (W2^T dm) o [h1 > 0],
+//   dX = W1^T dh1 + Wr^T dx1 (the direct part; the aggregation part is fpm_kron_agg's adjoint
+//   of dagg),  dagg = Wl^T dx1,
+// and store the per-position vectors the weight gradients reduce over: V[b] = [dx1 | dh1 | dm | h1]
+// (4 x 16 channels, channel-major).  One thread per (pair, position); uniform weights in SGPRs.
+namespace {
+template <int C>
+__global__ __launch_bounds__(256) void gnn_bwd_point_kernel(const float* __restrict__ X, const float* __restrict__ dXn,
+                                                            const float* __restrict__ dz, const float* __restrict__ W,
+                                                            int B, long N, float* __restrict__ dX,
+                                                            float* __restrict__ dagg, float* __restrict__ V) {
+    using P = GnnPack<C>;
+    const long t = (long)blockIdx.x * 256 + threadIdx.x;
+    if (t >= (long)B * N) return;
+    const long b = t / N, p = t - b * N;
+    const float* Xb = X + b * C * N + p;
+    const float* Gb = dXn + b * 17 * N + p;
+    float x[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) x[c] = Xb[(long)c * N];
+    const float g = dz[b * N + p];
+    float dx1[16], h1[16], dm[16];
+    float h1p[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        float s = W[P::b1 + m];
+#pragma unroll
+        for (int c = 0; c < C; ++c) s += W[P::W1 + c * 16 + m] * x[c];
+        h1p[m] = s;
+        h1[m] = fmaxf(s, 0.f);
+    }
+#pragma unroll
+    for (int o = 0; o < 16; ++o) {
+        dx1[o] = Gb[(long)o * N] + W[P::wc + o] * g;
+        float s = W[P::b2 + o];
+#pragma unroll
+        for (int m = 0; m < 16; ++m) s += W[P::W2 + m * 16 + o] * h1[m];
+        dm[o] = s > 0.f ? dx1[o] : 0.f;
+    }
+    float* Vb = V + b * 64 * N + p;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        float s = 0.f;
+#pragma unroll
+        for (int o = 0; o < 16; ++o) s += W[P::W2 + m * 16 + o] * dm[o];
+        const float dh = h1p[m] > 0.f ? s : 0.f;
+        Vb[(long)(16 + m) * N] = dh;
+        h1p[m] = dh;      // reuse as dh1
+    }
+#pragma unroll
+    for (int o = 0; o < 16; ++o) {
+        Vb[(long)o * N] = dx1[o];
+        Vb[(long)(32 + o) * N] = dm[o];
+        Vb[(long)(48 + o) * N] = h1[o];
+    }
+    float* dXb = dX + b * C * N + p;
+    float* dAb = dagg + b * C * N + p;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        float s = 0.f, r = 0.f;
+#pragma unroll
+        for (int m = 0; m < 16; ++m) s += W[P::W1 + c * 16 + m] * h1p[m];
+#pragma unroll
+        for (int o = 0; o < 16; ++o) {
+            s += W[P::Wr + c * 16 + o] * dx1[o];
+            r += W[P::Wl + c * 16 + o] * dx1[o];
+        }
+        dXb[(long)c * N] = s;
+        dAb[(long)c * N] = r;
+    }
+}
+}  // namespace
+
+extern "C" int fpm_kron_gnn_layer_bwd_point(const float* X, int C, int B, int n1max, int n2max, const float* dXn,
+                                            const float* dz, const float* params, float* dX, float* dagg, float* V,
+                                            void* stream) {
+    FPM_CHECK_ARG(C == 1 || C == 17, "gnn_layer_bwd: C must be 1 or 17 (got %d)", C);
+    if (B == 0) return 0;
+    const long N = (long)n1max * n2max;
+    const unsigned grid = (unsigned)(((long)B * N + 255) / 256);
+    hipStream_t st = (hipStream_t)stream;
+    if (C == 1)
+        hipLaunchKernelGGL((gnn_bwd_point_kernel<1>), dim3(grid), dim3(256), 0, st, X, dXn, dz, params, B, N, dX, dagg, V);
+    else
+        hipLaunchKernelGGL((gnn_bwd_point_kernel<17>), dim3(grid), dim3(256), 0, st, X, dXn, dz, params, B, N, dX, dagg,
+                           V);
+    return fpm::check_launch("fpm_kron_gnn_layer_bwd_point");
+}

@@ -341,3 +341,14 @@ def kron_agg(X, C, B, n1max, n2max, tcsr1, tcsr2, q1, q2, n1, n2, adjoint, out):
               ctypes.c_void_p(tcsr1[1]), ctypes.c_void_p(tcsr2[0]), ctypes.c_void_p(tcsr2[1]), ctypes.c_void_p(q1),
               ctypes.c_void_p(q2), _p(n1), _p(n2), int(bool(adjoint)), _p(out), _stream(X))
     return out
+
+
+def gnn_layer_bwd_point(X, C, B, n1max, n2max, dXn, dz, params, dX, dagg, V):
+    """Per-position PYGNNLayer backward (node MLPs + classifier): dX (direct part), dagg, and
+    V = [dx1 | dh1 | dm | h1] (B, 64, N) for the weight-gradient reductions."""
+    _dev(X, dXn, dz, params, dX, dagg, V)
+    for t in (X, dXn, dz, dX, dagg, V):
+        if not t.is_contiguous():
+            raise _lib.FpmError("gnn_layer_bwd_point: contiguous tensors expected")
+    _lib.call("fpm_kron_gnn_layer_bwd_point", _p(X), int(C), int(B), int(n1max), int(n2max), _p(dXn), _p(dz),
+              _p(params), _p(dX), _p(dagg), _p(V), _stream(X))

@@ -108,6 +108,21 @@ class SplineLayerFn(torch.autograd.Function):
         return gx, dW[:C.SPLINE_CELLS], dW[C.SPLINE_CELLS], dbias, gres, None, None, None
 
 
+def _bmm_nn(A, Bm, op):
+    """Batched A (B, M, K) @ Bm (B, K, N) on the library's MFMA GEMM (C = A B^T form: both
+    operands transposed / zero-padded to K % 8 == 0 in the operand dtype); fp32 out."""
+    Bt, M, K = A.shape
+    N = Bm.shape[2]
+    K8 = (K + 7) // 8 * 8
+    Ap = torch.zeros(Bt, M, K8, device=A.device, dtype=op)
+    Ap[:, :, :K] = A
+    Bp = torch.zeros(Bt, N, K8, device=A.device, dtype=op)
+    Bp[:, :, :K] = Bm.transpose(1, 2)
+    out = torch.empty(Bt, M, N, device=A.device, dtype=torch.float32)
+    ops.gemm(Ap, Bp, M, N, K8, K8, K8, batch=Bt, sA=M * K8, sB=N * K8, out_f=out, ldc=N, sC=M * N)
+    return out
+
+
 class AffinityFn(torch.autograd.Function):
     """emb0[b][j][i] = softplus((x1_i o c_b) . x2_j) - 0.5 on the valid block, 0 elsewhere
     (affinity_layer.py:11-19, pad_tensor + transpose at ngm.py:317-321)."""
@@ -122,7 +137,7 @@ class AffinityFn(torch.autograd.Function):
         ops.gemm(x2.detach().to(op).contiguous(), x1c.to(op).contiguous(), n2max, n1max, D, D, D, batch=B,
                  sA=n2max * D, sB=n1max * D, epi=ops.EPI_AFFINITY, out_f=X, ldc=n1max, sC=n1max * n2max,
                  n1=bt.n1, n2=bt.n2)
-        ctx.bt = bt
+        ctx.bt, ctx.dmode = bt, dmode
         ctx.save_for_backward(x1, x2, coef, X)
         return X
 
@@ -137,14 +152,36 @@ class AffinityFn(torch.autograd.Function):
         valid = (j < bt.n2.view(-1, 1, 1)) & (i < bt.n1.view(-1, 1, 1))
         E = X[:, 0]
         dZ = torch.where(valid, gX[:, 0] * -torch.expm1(-(E + 0.5)), torch.zeros((), device=X.device))  # softplus'
-        x1v = x1.view(B, n1max, D)
-        x2v = x2.view(B, n2max, D)
-        x1c = x1v * coef[:, None, :]
-        dx2 = torch.bmm(dZ, x1c)                     # (B, n2max, D)
-        dx1c = torch.bmm(dZ.transpose(1, 2), x2v)    # (B, n1max, D)
-        dx1 = dx1c * coef[:, None, :]
+        x1v = x1.detach().view(B, n1max, D)
+        x2v = x2.detach().view(B, n2max, D)
+        x1c = x1v * coef.detach()[:, None, :]
+        op = _op_dtype(ctx.dmode)
+        dx2 = _bmm_nn(dZ, x1c, op)                        # (B, n2max, D)
+        dx1c = _bmm_nn(dZ.transpose(1, 2), x2v, op)       # (B, n1max, D)
+        dx1 = dx1c * coef.detach()[:, None, :]
         dcoef = (dx1c * x1v).sum(1)
         return dx1.reshape(B * n1max, D), dx2.reshape(B * n2max, D), dcoef, None, None
+
+
+def _outer_sum(U, V):
+    """sum_{b,p} U[b,:,p] (x) V[b,:,p] -> (O, C) for channel-major U (B, O, N), V (B, C, N).
+    A single (O x K) (K x C) product with K = B*N (millions) and O, C <= 17 gets one workgroup
+    from the library; splitting K into 1024-long slices gives B*N/1024 small products in one
+    batched GEMM, then a sum over the slices."""
+    B, O, N = U.shape
+    Cc = V.shape[1]
+    q = N
+    if N > 2048:
+        q = next((d for d in range(2048, 255, -1) if N % d == 0), 0)
+        if q == 0:
+            pad = (-N) % 1024
+            U = F.pad(U, (0, pad))
+            V = F.pad(V, (0, pad))
+            N, q = N + pad, 1024
+    S = N // q
+    Us = U.reshape(B, O, S, q).transpose(1, 2)                 # (B, S, O, q)
+    Vs = V.reshape(B, Cc, S, q).permute(0, 2, 3, 1)            # (B, S, q, C)
+    return torch.matmul(Us, Vs).sum((0, 1))
 
 
 def _gnn_pack(Wl, bl, Wr, W1, b1, W2, b2, wc, bc):
@@ -169,14 +206,14 @@ class GnnLayerFn(torch.autograd.Function):
         ops.sinkhorn(zbuf.transpose(1, 2), g.bt.n1, g.bt.n2, C.GNN_SK_ITER, C.SK_TAU, True,
                      out=Xn[:, 16].transpose(1, 2))
         ctx.g = g
-        ctx.save_for_backward(Xc, Xn, zbuf, Wl, Wr, W1, b1, W2, b2, wc)
+        ctx.save_for_backward(Xc, Xn, zbuf, Wl, bl, Wr, W1, b1, W2, b2, wc, bc)
         return Xn
 
     @staticmethod
     def backward(ctx, gXn):
         g = ctx.g
         bt = g.bt
-        Xc, Xn, zbuf, Wl, Wr, W1, b1, W2, b2, wc = ctx.saved_tensors
+        Xc, Xn, zbuf, Wl, bl, Wr, W1, b1, W2, b2, wc, bc = ctx.saved_tensors
         B, n1max, n2max = bt.B, bt.n1max, bt.n2max
         N = n1max * n2max
         Cin = Xc.shape[1]
@@ -185,27 +222,26 @@ class GnnLayerFn(torch.autograd.Function):
         dz = sinkhorn_bwd(zbuf.transpose(1, 2), gXn[:, 16].transpose(1, 2), bt.n1, bt.n2, C.GNN_SK_ITER,
                           C.SK_TAU, True).transpose(1, 2).reshape(B, N)
         x1 = Xn[:, :16].reshape(B, 16, N)
-        dx1 = gXn[:, :16].reshape(B, 16, N) + wc.reshape(16)[None, :, None] * dz[:, None, :]
-        dwc = torch.einsum("bp,bop->o", dz, x1)[None]
-        dbc = dz.sum().reshape(1)
         Xf = Xc.view(B, Cin, N)
         agg = torch.empty_like(Xc)
         ops.kron_agg(Xc, Cin, B, n1max, n2max, g.s0.csr, g.s1.csr, g.s0.csr[0], g.s1.csr[0], bt.n1, bt.n2, False, agg)
         agg = agg.view(B, Cin, N)
-        h1p = torch.einsum("mc,bcp->bmp", W1, Xf) + b1[None, :, None]
-        h1 = F.relu(h1p)
-        h2p = torch.einsum("om,bmp->bop", W2, h1) + b2[None, :, None]
-        dm = dx1 * (h2p > 0)
-        dW2 = torch.einsum("bop,bmp->om", dm, h1)
+        dz = dz.contiguous()
+        dX = torch.empty(B, Cin, N, device=Xc.device, dtype=torch.float32)
+        dagg = torch.empty(B, Cin, N, device=Xc.device, dtype=torch.float32)
+        V = torch.empty(B, 64, N, device=Xc.device, dtype=torch.float32)
+        ops.gnn_layer_bwd_point(Xc, Cin, B, n1max, n2max, gXn, dz, _gnn_pack(Wl, bl, Wr, W1, b1, W2, b2, wc, bc), dX,
+                                dagg, V)
+        dx1, dh1, dm, h1 = V[:, 0:16], V[:, 16:32], V[:, 32:48], V[:, 48:64]
+        dwc = _outer_sum(dz[:, None], x1)
+        dbc = dz.sum().reshape(1)
+        dW2 = _outer_sum(dm, h1)
         db2 = dm.sum((0, 2))
-        dh1 = torch.einsum("om,bop->bmp", W2, dm) * (h1p > 0)
-        dW1 = torch.einsum("bmp,bcp->mc", dh1, Xf)
+        dW1 = _outer_sum(dh1, Xf)
         db1 = dh1.sum((0, 2))
-        dWl = torch.einsum("bop,bcp->oc", dx1, agg)
+        dWl = _outer_sum(dx1, agg)
         dbl = dx1.sum((0, 2))
-        dWr = torch.einsum("bop,bcp->oc", dx1, Xf)
-        dX = torch.einsum("mc,bmp->bcp", W1, dh1) + torch.einsum("oc,bop->bcp", Wr, dx1)
-        dagg = torch.einsum("oc,bop->bcp", Wl, dx1).contiguous()
+        dWr = _outer_sum(dx1, Xf)
         dXa = torch.empty(B, Cin, n2max, n1max, device=Xc.device, dtype=torch.float32)
         ops.kron_agg(dagg.view(B, Cin, n2max, n1max), Cin, B, n1max, n2max, g.s0.out_csr(), g.s1.out_csr(),
                      g.s0.csr[0], g.s1.csr[0], bt.n1, bt.n2, True, dXa)
@@ -230,7 +266,8 @@ class NodeClsFn(torch.autograd.Function):
         X, w = ctx.saved_tensors
         gT = gs.transpose(1, 2)                                    # (B, n2max, n1max)
         dX = w.reshape(-1)[None, :, None, None] * gT[:, None]
-        dw = torch.einsum("bji,bcji->c", gT, X)[None]
+        B = X.shape[0]
+        dw = _outer_sum(gT.reshape(B, 1, -1), X.reshape(B, X.shape[1], -1))
         db = gs.sum().reshape(1)
         return dX, dw, db, None
 
@@ -299,13 +336,23 @@ class AfauFn(torch.autograd.Function):
         ss, *params = ctx.saved_tensors
         net, bt = ctx.net, ctx.bt
         names = net._afau_names
-        with torch.enable_grad():
-            leaves = [p.detach().requires_grad_(True) for p in params]
-            pm = dict(zip(names, leaves))
-            ks = afau_torch.afau_ks(ss.detach(), bt.n1, bt.n2, lambda k: pm[k])
-            grads = torch.autograd.grad(ks, leaves, gks, allow_unused=True)
-        grads = [torch.zeros_like(p) if gr is None else gr for p, gr in zip(params, grads)]
-        return (None, None, None) + tuple(grads)
+        B, n1max, n2max = ss.shape
+        # pairs are independent in the regressor (per-pair instance norm and max pool), so the
+        # replay runs in pair chunks: the mixed-score MLP's (pairs, 16 heads, n1, n2, 16) hidden
+        # tensor is bounded to ~2^28 values per chunk
+        per = max(1, (1 << 28) // (C.AFAU_HEADS * C.AFAU_MS_HIDDEN * max(1, n1max * n2max)))
+        total = [torch.zeros_like(p) for p in params]
+        leaves = [p.detach().requires_grad_(True) for p in params]
+        pm = dict(zip(names, leaves))
+        for b0 in range(0, B, per):
+            b1 = min(B, b0 + per)
+            with torch.enable_grad():
+                ks = afau_torch.afau_ks(ss[b0:b1].detach(), bt.n1[b0:b1], bt.n2[b0:b1], lambda k: pm[k])
+                grads = torch.autograd.grad(ks, leaves, gks[b0:b1], allow_unused=True)
+            for t, gr in zip(total, grads):
+                if gr is not None:
+                    t += gr
+        return (None, None, None) + tuple(total)
 
 
 def match_cls_train(m, P_, B_):

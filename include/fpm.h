@@ -262,6 +262,14 @@ int fpm_kron_agg(const float* X, int C, int B, int n1max, int n2max, const int* 
                  const int* tptr2, const int* tnbr2, const int* q1, const int* q2, const int* n1, const int* n2,
                  int adjoint, float* out, void* stream);
 
+/* PYGNNLayer node MLPs + classifier, per association node (gnn.py:208-215 transposed): given dXn
+ * (gradient of [x1 || S], (B, 17, n2max, n1max)) and dz (gradient of the classifier logit, i.e.
+ * the Sinkhorn backward of channel 16), writes dX = W1^T dh1 + Wr^T dx1 and dagg = Wl^T dx1
+ * ((B, C, ...)), and V = [dx1 | dh1 | dm | h1] ((B, 64, N)) for the weight-gradient reductions.
+ * params: the forward's packed layer parameters. */
+int fpm_kron_gnn_layer_bwd_point(const float* X, int C, int B, int n1max, int n2max, const float* dXn, const float* dz,
+                                 const float* params, float* dX, float* dagg, float* V, void* stream);
+
 /* ---- host: batched linear sum assignment ------------------------------------------------------
  * Replaces utils/hungarian.py:8-66 (scipy linear_sum_assignment on -s, per pair).  Synchronous,
  * HOST memory, nthreads worker threads.  assign[b][r] = column or -1.  Returns 0 or (pair + 1). */
