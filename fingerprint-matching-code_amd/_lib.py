@@ -40,7 +40,7 @@ SIGNATURES = {
     "fpm_instnorm": (I, [I, P, P, I, I, I, P, P, P, P, F, P, P, I, P, P]),
     "fpm_afau_head": (I, [P, P, I, I, P, P, P, P, P, P, P, P, P, P]),
     "fpm_match_cls_ws_floats": (L, [I, I, I]),
-    "fpm_match_cls_fwd": (I, [P, P, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),
+    "fpm_match_cls_fwd": (I, [I, P, P, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),
     "fpm_lsa_batch_host": (I, [P, L, L, P, P, I, I, P, I]),
     "fpm_lsa_batch_device": (I, [P, L, L, P, P, I, I, I, P, P, P]),
     "fpm_csr_dot_csc_to_dense": (I, [I, P, P, P, P, P, P, L, L, L, P, P]),

@@ -86,6 +86,7 @@ class Net(nn.Module):
         # stream copy.  Measured slower (21.2K -> 19.7K pairs/s: the kernel stalls on PCIe writes
         # on the critical path), so off by default.
         self.zero_copy = os.environ.get("FPM_ZERO_COPY", "0") == "1"
+        self.copy_stream = os.environ.get("FPM_COPY_STREAM", "1") == "1"
         self._keep_feats = False
         self._stage_timing = os.environ.get("FPM_STAGE_TIMING", "0") == "1"
         self.stage_times = {}
@@ -392,11 +393,29 @@ class Net(nn.Module):
             with torch.cuda.stream(side):
                 self._stage_c_device(part, b0, b1, o)
             return r, ev
+        if not self.zero_copy and self.copy_stream:
+            # the D2H copy is a blit kernel: on a stream of its own it does not hold back the next
+            # chunk queued on this compute stream
+            done = torch.cuda.Event()
+            done.record(st)
+            cs = self._copy_stream(dev)
+            cs.wait_event(done)
+            with torch.cuda.stream(cs):
+                self._pinned[b0:b1].copy_(o["ds_mat"][b0:b1], non_blocking=True)
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(cs)
+            return r, ev
         if not self.zero_copy:
             self._pinned[b0:b1].copy_(o["ds_mat"][b0:b1], non_blocking=True)
         ev = torch.cuda.Event(enable_timing=True)
         ev.record(st)
         return r, ev
+
+    def _copy_stream(self, dev):
+        key = "copy:" + str(dev)
+        if key not in self._stream_cache:
+            self._stream_cache[key] = torch.cuda.Stream(dev)
+        return self._stream_cache[key]
 
     def _stage_c_device(self, part, b0, b1, o):
         """Device Hungarian + greedy selection + MatchClassifier of one chunk, queued on the
@@ -408,7 +427,8 @@ class Net(nn.Module):
                         out=o["perm_mat"][b0:b1])
         ops.match_cls(o["s"][b0:b1], o["perm_mat"][b0:b1], wp["mc_w1"], wp["mc_b1"], wp["mc_sc1"], wp["mc_sh1"],
                       wp["mc_w2"], wp["mc_b2"], wp["mc_sc2"], wp["mc_sh2"], wp["mc_fcw"], wp["mc_fcb"],
-                      logits=o["cls_logits"][b0:b1], prob=o["cls_prob"][b0:b1])
+                      logits=o["cls_logits"][b0:b1], prob=o["cls_prob"][b0:b1],
+                      dtype=ops.BF16 if self.dtype_mode == "bf16" else ops.F32)
 
     def _stage_c(self, part, b0, b1, o):
         """Host Hungarian (utils/hungarian.py: LSA of -ds_mat per pair) + greedy selection +
@@ -424,7 +444,8 @@ class Net(nn.Module):
         self._mark("lsa+h2d+select")
         ops.match_cls(o["s"][b0:b1], o["perm_mat"][b0:b1], wp["mc_w1"], wp["mc_b1"], wp["mc_sc1"], wp["mc_sh1"],
                       wp["mc_w2"], wp["mc_b2"], wp["mc_sc2"], wp["mc_sh2"], wp["mc_fcw"], wp["mc_fcb"],
-                      logits=o["cls_logits"][b0:b1], prob=o["cls_prob"][b0:b1])
+                      logits=o["cls_logits"][b0:b1], prob=o["cls_prob"][b0:b1],
+                      dtype=ops.BF16 if self.dtype_mode == "bf16" else ops.F32)
         self._mark("match_cls")
         return dt
 

@@ -201,7 +201,7 @@ def afau_head(gr, gc, B, E, r0w, r0b, r2w, r2b, c0w, c0b, c2w, c2b, ks):
               _p(c2w), _p(c2b), _p(ks), _stream(gr))
 
 
-def match_cls(s, perm, w1, b1, bn1_sc, bn1_sh, w2, b2, bn2_sc, bn2_sh, fcw, fcb, logits=None, prob=None):
+def match_cls(s, perm, w1, b1, bn1_sc, bn1_sh, w2, b2, bn2_sc, bn2_sh, fcw, fcb, logits=None, prob=None, dtype=F32):
     _dev(s, perm)
     if not (s.is_contiguous() and perm.is_contiguous()):
         raise _lib.FpmError("match_cls: s and perm must be contiguous")
@@ -210,7 +210,7 @@ def match_cls(s, perm, w1, b1, bn1_sc, bn1_sh, w2, b2, bn2_sc, bn2_sh, fcw, fcb,
     ws = torch.empty(max(int(nws), 1), device=s.device, dtype=torch.float32)
     logits = logits if logits is not None else torch.empty(B, device=s.device, dtype=torch.float32)
     prob = prob if prob is not None else torch.empty(B, device=s.device, dtype=torch.float32)
-    _lib.call("fpm_match_cls_fwd", _p(s), _p(perm), B, H, W, _p(w1), _p(b1), _p(bn1_sc), _p(bn1_sh), _p(w2), _p(b2),
+    _lib.call("fpm_match_cls_fwd", int(dtype), _p(s), _p(perm), B, H, W, _p(w1), _p(b1), _p(bn1_sc), _p(bn1_sh), _p(w2), _p(b2),
               _p(bn2_sc), _p(bn2_sh), _p(fcw), _p(fcb), _p(ws), _p(logits), _p(prob), _stream(s))
     return logits, prob
 

@@ -130,10 +130,12 @@ int fpm_afau_head(const float* gr, const float* gc, int B, int E, const float* r
                   const float* r2w, const float* r2b, const float* c0w, const float* c0b, const float* c2w,
                   const float* c2b, float* ks, void* stream);
 
-/* ---- MatchClassifier (ngm.py:75-106, applied at :451-455) ------------------------------------- */
+/* ---- MatchClassifier (ngm.py:75-106, applied at :451-455) -------------------------------------
+ * dtype 0: conv2 on fp32 matrix cores (exact fp32 products, parity mode); 1: conv2 operands in
+ * bf16 (fp32 accumulation, the bf16 throughput mode). */
 long fpm_match_cls_ws_floats(int B, int H, int W);
-int fpm_match_cls_fwd(const float* s, const float* perm, int B, int H, int W, const float* w1, const float* b1,
-                      const float* bn1_sc, const float* bn1_sh, const float* w2, const float* b2,
+int fpm_match_cls_fwd(int dtype, const float* s, const float* perm, int B, int H, int W, const float* w1,
+                      const float* b1, const float* bn1_sc, const float* bn1_sh, const float* w2, const float* b2,
                       const float* bn2_sc, const float* bn2_sh, const float* fcw, const float* fcb, float* ws,
                       float* logits, float* prob, void* stream);
 

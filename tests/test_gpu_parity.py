@@ -463,3 +463,22 @@ def test_gemm_big_affinity_epilogue():
         assert (out[b, :r, :c].cpu() - ref[b, :r, :c]).abs().max() < 1e-4
         assert out[b, r:].abs().max().item() == 0 if r < M else True
         assert out[b, :, c:].abs().max().item() == 0 if c < N else True
+
+
+def test_match_cls_bf16_vs_f32(sd):
+    """bf16 conv2 (tap-major K on v_mfma_f32_16x16x16_bf16) against the fp32 path and the oracle's
+    MatchClassifier: reported mode, logits within 2e-2 of the fp32 values (|logit| ~ 0.1-1)."""
+    net = fpm.Net(regression=True, dtype="f32")
+    net.load_state_dict(sd)
+    wp = net.packed(DEV)
+    g = torch.Generator().manual_seed(5)
+    for B, n1, n2 in ((4, 256, 256), (3, 37, 50)):
+        s = torch.randn(B, n1, n2, generator=g)
+        perm = (torch.rand(B, n1, n2, generator=g) < 0.02).float()
+        args = [wp[k] for k in ("mc_w1", "mc_b1", "mc_sc1", "mc_sh1", "mc_w2", "mc_b2", "mc_sc2", "mc_sh2", "mc_fcw",
+                                "mc_fcb")]
+        l32, _ = ops.match_cls(s.to(DEV), perm.to(DEV), *args, dtype=ops.F32)
+        l16, _ = ops.match_cls(s.to(DEV), perm.to(DEV), *args, dtype=ops.BF16)
+        ref = O.match_classifier(s * perm, sd)
+        assert (l32.cpu() - ref).abs().max() < 1e-4
+        assert (l16.cpu() - ref).abs().max() < 2e-2
