@@ -72,11 +72,13 @@ int& gemm_phase_flag() {
 }  // namespace fpm
 
 int& gnn_packed_flag();
+int& gnn_unroll_flag();
 
 extern "C" int fpm_set_tuning(const char* key, int value) {
     int* f = nullptr;
     if (key && !strcmp(key, "gemm_phase")) f = &fpm::gemm_phase_flag();
     else if (key && !strcmp(key, "gnn_packed")) f = &gnn_packed_flag();
+    else if (key && !strcmp(key, "gnn_unroll")) f = &gnn_unroll_flag();
     if (!f) {
         fpm::set_error("fpm_set_tuning: unknown key '%s'", key ? key : "(null)");
         return -1;

@@ -45,7 +45,7 @@ __device__ __forceinline__ void pk_fma_bcast(f2_t& acc, f2_t w, f2_t v, bool hi)
     else asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1]" : "+v"(acc) : "s"(w), "v"(v));
 }
 
-template <int C, bool PACKED>
+template <int C, bool PACKED, int U = 1>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(PACKED ? 5 : 6, 8))) void gnn_layer_kernel(const float* __restrict__ X, int n1max, int n2max,
                                                          const int* __restrict__ ptr1, const int* __restrict__ nbr1,
                                                          const int* __restrict__ ptr2, const int* __restrict__ nbr2,
@@ -90,7 +90,24 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(PACKED ? 5
             for (int c = 0; c < C; ++c) acc[c] += v[c];
         };
         const int nl = nn2 < 64 ? nn2 : 64;
-        for (int k = 0; k < nl; ++k) add_row(nb2[k]);                  // LDS copy of the first 64
+        int k0 = 0;
+        if constexpr (U > 1) {
+            // U neighbour rows' loads issued together (U x C in flight), summed in the same order
+            for (; k0 + U <= nl; k0 += U) {
+                float v[U][C];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const float* row = Xb + (long)nb2[k0 + u] * n1max + i;
+#pragma unroll
+                    for (int c = 0; c < C; ++c) v[u][c] = row[(long)c * N];
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+#pragma unroll
+                    for (int c = 0; c < C; ++c) acc[c] += v[u][c];
+            }
+        }
+        for (int k = k0; k < nl; ++k) add_row(nb2[k]);                 // LDS copy of the first 64
         for (int k = 64; k < nn2; ++k) add_row(nbr2[beg2 + k]);
 
         float* Ti = T + i * TS;
@@ -250,6 +267,16 @@ int& gnn_packed_flag() {
     return on;
 }
 
+// graph-2 neighbour rows loaded U at a time (1, 2 or 3; bit-identical); env FPM_GNN_UNROLL or
+// fpm_set_tuning("gnn_unroll", v)
+int& gnn_unroll_flag() {
+    static int u = [] {
+        const char* e = getenv("FPM_GNN_UNROLL");
+        return e ? atoi(e) : 1;
+    }();
+    return u;
+}
+
 extern "C" int fpm_kron_gnn_layer_fwd(const float* X, int C, int B, int n1max, int n2max, const int* ptr1,
                                       const int* nbr1, const int* ptr2, const int* nbr2, const int* n1, const int* n2,
                                       const float* params, float* Xout, float* zbuf, float* vpart, const float* cls_w,
@@ -263,16 +290,20 @@ extern "C" int fpm_kron_gnn_layer_fwd(const float* X, int C, int B, int n1max, i
     const size_t sh = (size_t)(C == 1 ? 1 : 20) * n1max * 4;
     const int threads = (n1max + 63) / 64 * 64;
     const bool packed = gnn_packed_flag() != 0;
-#define FPM_GNN(C_, P_)                                                                                          \
+    const int un = gnn_unroll_flag();
+#define FPM_GNN(C_, P_, U_)                                                                                      \
     do {                                                                                                         \
         if (sh > 65536)                                                                                          \
-            (void)hipFuncSetAttribute((const void*)gnn_layer_kernel<C_, P_>,                                     \
+            (void)hipFuncSetAttribute((const void*)gnn_layer_kernel<C_, P_, U_>,                                 \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);                      \
-        hipLaunchKernelGGL((gnn_layer_kernel<C_, P_>), grid, dim3(threads), sh, st, X, n1max, n2max, ptr1, nbr1,  \
-                           ptr2, nbr2, n1, n2, params, Xout, zbuf, vpart, cls_w, B);                             \
+        hipLaunchKernelGGL((gnn_layer_kernel<C_, P_, U_>), grid, dim3(threads), sh, st, X, n1max, n2max, ptr1,   \
+                           nbr1, ptr2, nbr2, n1, n2, params, Xout, zbuf, vpart, cls_w, B);                       \
     } while (0)
-    if (C == 1) { if (packed) FPM_GNN(1, true); else FPM_GNN(1, false); }
-    else { if (packed) FPM_GNN(17, true); else FPM_GNN(17, false); }
+    if (C == 1) { if (packed) FPM_GNN(1, true, 1); else FPM_GNN(1, false, 1); }
+    else if (!packed) FPM_GNN(17, false, 1);
+    else if (un == 2) FPM_GNN(17, true, 2);
+    else if (un == 3) FPM_GNN(17, true, 3);
+    else FPM_GNN(17, true, 1);
 #undef FPM_GNN
     return fpm::check_launch("fpm_kron_gnn_layer_fwd");
 }

@@ -18,6 +18,8 @@ operands with fp32 accumulation for the GEMMs; everything else fp32).
 import os
 import time
 
+import numpy as np
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -224,15 +226,26 @@ class Net(nn.Module):
         mh = torch.empty(B * n1max, E, device=dev, dtype=torch.float32)
         ops.gemm(att, wp["row_Wc"], B * n1max, E, HD, HD, HD, bias=wp["row_bc"], out_f=mh, ldc=E)
         gmax = {}
-        for blk, rows, P_ in (("row", B * n1max, n1max), ("col", B * n2max, n2max)):
+        # The column block sees a = one-hot rows and b = zero rows, so k = v = 0 and its attention
+        # output is exactly the combine bias (afau.py:99-142): its result depends on n2 (and the
+        # batch's n2max) only, not on ss.  It is computed once per distinct n2 of the batch and
+        # gathered -- the same arithmetic on the same inputs, so bit-identical to the per-pair run.
+        if os.environ.get("FPM_AFAU_COLDEDUP", "1") == "1":
+            n2u, inv = np.unique(bt.n_host[1].numpy(), return_inverse=True)
+        else:
+            n2u, inv = bt.n_host[1].numpy(), np.arange(B)
+        Bu = len(n2u)
+        n2u_d = torch.as_tensor(n2u, dtype=torch.int32).to(dev, non_blocking=True)
+        for blk, rows, P_ in (("row", B * n1max, n1max), ("col", Bu * n2max, n2max)):
             o1f = torch.empty(rows, E, device=dev, dtype=torch.float32)
             KE = E if op == torch.float32 else C.AFAU_EMB_PAD      # bf16 operand copy: zero-padded K
             o1t = o1f if op == torch.float32 else torch.empty(rows, KE, device=dev, dtype=op)
+            nb_ = B if blk == "row" else Bu
             if blk == "row":
                 ops.instnorm(mh, B, P_, E, wp["row_n1w"], wp["row_n1b"], out_f=o1f,
                              out_t=None if op == torch.float32 else o1t, ldt=KE)
             else:
-                ops.instnorm(None, B, P_, E, wp["col_n1w"], wp["col_n1b"], nvalid=bt.n2, onehot_bias=wp["col_bc"],
+                ops.instnorm(None, Bu, P_, E, wp["col_n1w"], wp["col_n1b"], nvalid=n2u_d, onehot_bias=wp["col_bc"],
                              out_f=o1f, out_t=None if op == torch.float32 else o1t, ldt=KE)
             hbuf = torch.empty(rows, FF, device=dev, dtype=op)
             ops.gemm(o1t, wp[blk + "_W1"], rows, FF, KE, KE, KE, epi=ops.EPI_RELU, bias=wp[blk + "_b1"],
@@ -240,8 +253,12 @@ class Net(nn.Module):
                      ldc=FF)
             ff = torch.empty(rows, E, device=dev, dtype=torch.float32)
             ops.gemm(hbuf, wp[blk + "_W2"], rows, E, FF, FF, FF, bias=wp[blk + "_b2"], out_f=ff, ldc=E)
-            gm = torch.empty(B, E, device=dev, dtype=torch.float32)
-            ops.instnorm(o1f, B, P_, E, wp[blk + "_n2w"], wp[blk + "_n2b"], in2=ff, gmax=gm)
+            gm = torch.empty(nb_, E, device=dev, dtype=torch.float32)
+            ops.instnorm(o1f, nb_, P_, E, wp[blk + "_n2w"], wp[blk + "_n2b"], in2=ff, gmax=gm)
+            if blk == "col" and Bu != B:
+                gm = gm.index_select(0, torch.as_tensor(inv, dtype=torch.long).to(dev, non_blocking=True))
+            elif blk == "col" and Bu == B and not np.array_equal(inv, np.arange(B)):
+                gm = gm.index_select(0, torch.as_tensor(inv, dtype=torch.long).to(dev, non_blocking=True))
             gmax[blk] = gm
         ks = torch.empty(B, device=dev, dtype=torch.float32)
         ops.afau_head(gmax["row"], gmax["col"], B, E, wp["final_row0w"], wp["final_row0b"], wp["final_row2w"],
