@@ -73,12 +73,16 @@ int& gemm_phase_flag() {
 
 int& gnn_packed_flag();
 int& gnn_unroll_flag();
+int& gnn_group_flag();
+int& combine_npb_flag();
 
 extern "C" int fpm_set_tuning(const char* key, int value) {
     int* f = nullptr;
     if (key && !strcmp(key, "gemm_phase")) f = &fpm::gemm_phase_flag();
     else if (key && !strcmp(key, "gnn_packed")) f = &gnn_packed_flag();
     else if (key && !strcmp(key, "gnn_unroll")) f = &gnn_unroll_flag();
+    else if (key && !strcmp(key, "gnn_group")) f = &gnn_group_flag();
+    else if (key && !strcmp(key, "combine_npb")) f = &combine_npb_flag();
     if (!f) {
         fpm::set_error("fpm_set_tuning: unknown key '%s'", key ? key : "(null)");
         return -1;

@@ -45,7 +45,7 @@ __device__ __forceinline__ void pk_fma_bcast(f2_t& acc, f2_t w, f2_t v, bool hi)
     else asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1]" : "+v"(acc) : "s"(w), "v"(v));
 }
 
-template <int C, bool PACKED, int U = 1>
+template <int C, bool PACKED, int U = 1, int G = 1>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(PACKED ? 5 : 6, 8))) void gnn_layer_kernel(const float* __restrict__ X, int n1max, int n2max,
                                                          const int* __restrict__ ptr1, const int* __restrict__ nbr1,
                                                          const int* __restrict__ ptr2, const int* __restrict__ nbr2,
@@ -60,23 +60,31 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(PACKED ? 5
     // reads a neighbour's 17 channels with 4 ds_read_b128 + 1 ds_read_b32
     constexpr int TS = C == 1 ? 1 : 20;
     extern __shared__ __attribute__((aligned(16))) float T[];
-    __shared__ int nb2[64];
-    __shared__ int nnb2, beg2;
+    __shared__ int nb2_[G][64];
+    __shared__ int nnb2_[G], beg2_[G];
 
-    int d, b;
-    if (!pair_block(n2max, B, b, d)) return;
-    const int i = threadIdx.x;
+    // G > 1: G graph-2 nodes per workgroup, one 256-thread group each (n1max <= 256)
+    constexpr int SUBW = G > 1 ? 256 : 1024;
+    const int sub = G > 1 ? (int)threadIdx.x / SUBW : 0;
+    const int i = G > 1 ? (int)threadIdx.x - sub * SUBW : (int)threadIdx.x;
+    int dg, b;
+    if (!pair_block((n2max + G - 1) / G, B, b, dg)) return;
+    const int d = dg * G + sub;
+    const bool active = d < n2max;
+    int* nb2 = nb2_[sub];
+    float* Tg = T + (long)sub * n1max * TS;
     const long N = (long)n1max * n2max;
     const float* Xb = X + (long)b * C * N;
-    if (i == 0) {
+    if (i == 0 && active) {
         const int beg = ptr2[(long)b * n2max + d], end = ptr2[(long)b * n2max + d + 1];
-        nnb2 = end - beg;
-        beg2 = beg;
+        nnb2_[sub] = end - beg;
+        beg2_[sub] = beg;
         for (int k = 0; k < end - beg && k < 64; ++k) nb2[k] = nbr2[beg + k];
     }
     __syncthreads();
-    const int nn2 = nnb2;
-    if (i < n1max) {
+    const int nn2 = active ? nnb2_[sub] : 0;
+    const int beg2 = active ? beg2_[sub] : 0;
+    if (i < n1max && active) {
         // neighbour-outer, channel-inner: C independent loads in flight per neighbour row
         float acc[C];
 #pragma unroll
@@ -110,7 +118,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(PACKED ? 5
         for (int k = k0; k < nl; ++k) add_row(nb2[k]);                 // LDS copy of the first 64
         for (int k = 64; k < nn2; ++k) add_row(nbr2[beg2 + k]);
 
-        float* Ti = T + i * TS;
+        float* Ti = Tg + i * TS;
         if constexpr (C == 17) {
 #pragma unroll
             for (int q = 0; q < 4; ++q)
@@ -121,7 +129,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(PACKED ? 5
         }
     }
     __syncthreads();
-    if (i >= n1max) return;
+    if (i >= n1max || !active) return;
     const int n1b = n1[b], n2b = n2[b];
     const long p = (long)d * n1max + i;
     const int beg = ptr1[(long)b * n1max + i], end = ptr1[(long)b * n1max + i + 1];
@@ -133,7 +141,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(PACKED ? 5
         agg[c] = 0.f;
     }
     for (int e = beg; e < end; ++e) {
-        const float* Ta = T + nbr1[e] * TS;
+        const float* Ta = Tg + nbr1[e] * TS;
         if constexpr (C == 17) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -267,6 +275,16 @@ int& gnn_packed_flag() {
     return on;
 }
 
+// graph-2 nodes per workgroup, processed by parallel 256-thread groups (1, 2, 4; bit-identical);
+// env FPM_GNN_GROUP or fpm_set_tuning("gnn_group", v)
+int& gnn_group_flag() {
+    static int u = [] {
+        const char* e = getenv("FPM_GNN_GROUP");
+        return e ? atoi(e) : 2;
+    }();
+    return u;
+}
+
 // graph-2 neighbour rows loaded U at a time (1, 2 or 3; bit-identical); env FPM_GNN_UNROLL or
 // fpm_set_tuning("gnn_unroll", v)
 int& gnn_unroll_flag() {
@@ -291,19 +309,25 @@ extern "C" int fpm_kron_gnn_layer_fwd(const float* X, int C, int B, int n1max, i
     const int threads = (n1max + 63) / 64 * 64;
     const bool packed = gnn_packed_flag() != 0;
     const int un = gnn_unroll_flag();
-#define FPM_GNN(C_, P_, U_)                                                                                      \
+    const int grp = n1max <= 256 ? gnn_group_flag() : 1;   // default 2: 21% faster at n = 256
+#define FPM_GNN(C_, P_, U_, G_)                                                                                  \
     do {                                                                                                         \
-        if (sh > 65536)                                                                                          \
-            (void)hipFuncSetAttribute((const void*)gnn_layer_kernel<C_, P_, U_>,                                 \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);                      \
-        hipLaunchKernelGGL((gnn_layer_kernel<C_, P_, U_>), grid, dim3(threads), sh, st, X, n1max, n2max, ptr1,   \
+        const size_t sh_ = sh * G_;                                                                              \
+        if (sh_ > 65536)                                                                                         \
+            (void)hipFuncSetAttribute((const void*)gnn_layer_kernel<C_, P_, U_, G_>,                             \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh_);                     \
+        const dim3 g_(pair_grid((n2max + G_ - 1) / G_, B));                                                      \
+        const dim3 t_(G_ > 1 ? 256 * G_ : threads);                                                              \
+        hipLaunchKernelGGL((gnn_layer_kernel<C_, P_, U_, G_>), g_, t_, sh_, st, X, n1max, n2max, ptr1,           \
                            nbr1, ptr2, nbr2, n1, n2, params, Xout, zbuf, vpart, cls_w, B);                       \
     } while (0)
-    if (C == 1) { if (packed) FPM_GNN(1, true, 1); else FPM_GNN(1, false, 1); }
-    else if (!packed) FPM_GNN(17, false, 1);
-    else if (un == 2) FPM_GNN(17, true, 2);
-    else if (un == 3) FPM_GNN(17, true, 3);
-    else FPM_GNN(17, true, 1);
+    if (C == 1) { if (packed) FPM_GNN(1, true, 1, 1); else FPM_GNN(1, false, 1, 1); }
+    else if (!packed) FPM_GNN(17, false, 1, 1);
+    else if (grp == 2) FPM_GNN(17, true, 1, 2);
+    else if (grp == 4) FPM_GNN(17, true, 1, 4);
+    else if (un == 2) FPM_GNN(17, true, 2, 1);
+    else if (un == 3) FPM_GNN(17, true, 3, 1);
+    else FPM_GNN(17, true, 1, 1);
 #undef FPM_GNN
     return fpm::check_launch("fpm_kron_gnn_layer_fwd");
 }

@@ -317,8 +317,8 @@ __global__ void plan_expand_kernel(const int* __restrict__ src, const int* __res
 // out[v] = max_{in-edges e} sum_s basis[e,s] * Y[row(src_e, cell_s)] + Y[root row v] + bias
 //   mode 0: relu(.) ; mode 1: xres[v] + 0.1 * (.)   (+ optional per-pair column scale on out_t)
 // One wave per node, 12 channels per lane (3 x 4 contiguous).
-template <typename T>
-__global__ __launch_bounds__(256) void combine_kernel(const T* __restrict__ Y, const int* __restrict__ cell_off,
+template <typename T, int NPB = 4>
+__global__ __launch_bounds__(64 * NPB) void combine_kernel(const T* __restrict__ Y, const int* __restrict__ cell_off,
                                                       const float* __restrict__ bias,
                                                       const int* __restrict__ dst_ptr, const int4* __restrict__ rows4,
                                                       const float4* __restrict__ basis4, long num_nodes, int nmax,
@@ -328,10 +328,10 @@ __global__ __launch_bounds__(256) void combine_kernel(const T* __restrict__ Y, c
     const int lane = threadIdx.x & 63;
     // graph-per-XCD block order: XCD x = blockIdx % 8 takes graphs x, x+8, ... so a graph's product
     // rows (~3.7 MB at n = 256, each read ~2.4 times by its in-edges) stay in one L2
-    const int bpg = (nmax + 3) / 4;
+    const int bpg = (nmax + NPB - 1) / NPB;
     const int xk = blockIdx.x >> 3;
     const int b = (xk / bpg) * 8 + (blockIdx.x & 7);
-    const int loc = (xk % bpg) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int loc = (xk % bpg) * NPB + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (loc >= nmax || (long)b * nmax >= num_nodes) return;
     const long v = (long)b * nmax + loc;
     const bool valid = loc < nvalid[b];
@@ -500,6 +500,16 @@ __global__ __launch_bounds__(256) void node_rows_sum_kernel(const float* __restr
 
 }  // namespace
 
+// destination nodes (one wave each) per combine workgroup: 4, 8 or 16 (bit-identical); env
+// FPM_COMBINE_NPB or fpm_set_tuning("combine_npb", v)
+int& combine_npb_flag() {
+    static int u = [] {
+        const char* e = getenv("FPM_COMBINE_NPB");
+        return e ? atoi(e) : 4;
+    }();
+    return u;
+}
+
 extern "C" long fpm_spline_plan_bytes(long E, long num_nodes) {
     return plan_layout(E, num_nodes).total;
 }
@@ -601,17 +611,18 @@ extern "C" int fpm_spline_conv_fwd(int dtype, const void* x_op, const void* plan
     }
     {
         const long graphs = (num_nodes + nmax - 1) / nmax;
-        dim3 grid((unsigned)(((graphs + 7) / 8) * 8 * ((nmax + 3) / 4)));
-        if (dtype == 0)
-            hipLaunchKernelGGL((combine_kernel<float>), grid, dim3(256), 0, st, (const float*)y_ws,
-                               (const int*)(w + L.cell_off), bias, (const int*)(w + L.dst_ptr),
-                               (const int4*)(w + L.rows4), (const float4*)(w + L.basis4), num_nodes, nmax, nvalid,
-                               mode, xres, cscale, out_f, (float*)out_t);
-        else
-            hipLaunchKernelGGL((combine_kernel<bf16_t>), grid, dim3(256), 0, st, (const bf16_t*)y_ws,
-                               (const int*)(w + L.cell_off), bias, (const int*)(w + L.dst_ptr),
-                               (const int4*)(w + L.rows4), (const float4*)(w + L.basis4), num_nodes, nmax, nvalid,
-                               mode, xres, cscale, out_f, (bf16_t*)out_t);
+        const int npb = combine_npb_flag();
+#define FPM_COMB(T_, N_)                                                                                         \
+    hipLaunchKernelGGL((combine_kernel<T_, N_>), dim3((unsigned)(((graphs + 7) / 8) * 8 * ((nmax + N_ - 1) / N_))), \
+                       dim3(64 * N_), 0, st, (const T_*)y_ws, (const int*)(w + L.cell_off), bias,                \
+                       (const int*)(w + L.dst_ptr), (const int4*)(w + L.rows4), (const float4*)(w + L.basis4),   \
+                       num_nodes, nmax, nvalid, mode, xres, cscale, out_f, (T_*)out_t)
+        if (dtype == 0) {
+            if (npb == 16) FPM_COMB(float, 16); else if (npb == 8) FPM_COMB(float, 8); else FPM_COMB(float, 4);
+        } else {
+            if (npb == 16) FPM_COMB(bf16_t, 16); else if (npb == 8) FPM_COMB(bf16_t, 8); else FPM_COMB(bf16_t, 4);
+        }
+#undef FPM_COMB
     }
     return check_launch("fpm_spline_conv_fwd");
 }

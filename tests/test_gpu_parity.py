@@ -482,3 +482,24 @@ def test_match_cls_bf16_vs_f32(sd):
         ref = O.match_classifier(s * perm, sd)
         assert (l32.cpu() - ref).abs().max() < 1e-4
         assert (l16.cpu() - ref).abs().max() < 2e-2
+
+
+def test_gnn_kernel_variants_bit_identical(sd):
+    """GNN-layer launch variants (2 graph-2 nodes per workgroup, neighbour-load unroll) and combine
+    workgroup sizes give bit-identical forwards."""
+    pairs = synth.make_batch(17, 3, 64)
+    net = fpm.Net(regression=True, dtype="bf16")
+    net.load_state_dict(sd)
+    bt = DeviceBatch.from_pairs(pairs, DEV)
+    outs = []
+    for key, val in (("gnn_group", 1), ("gnn_group", 2), ("gnn_unroll", 3), ("combine_npb", 16)):
+        prev = ops.set_tuning(key, val)
+        try:
+            r = net.run(bt, chunks=1)
+            torch.cuda.synchronize()
+        finally:
+            ops.set_tuning(key, prev)
+        outs.append(r)
+    for r in outs[1:]:
+        for k in ("s", "ss", "ds_mat", "k_prob"):
+            assert torch.equal(r[k], outs[0][k]), k
