@@ -9,6 +9,7 @@
 // fused with the max-pool over positions), and the 600->8->1 heads + sigmoid.
 // The projections/FFN are MFMA GEMMs through fpm_gemm.
 #include "fpm_common.h"
+#include <cstdlib>
 
 namespace {
 
@@ -46,7 +47,8 @@ __global__ __launch_bounds__(256) void afau_row_attn_kernel(const float* __restr
                                                             const float* __restrict__ mix1w,
                                                             const float* __restrict__ mix1b,
                                                             const float* __restrict__ mix2w,
-                                                            const float* __restrict__ mix2b, T* __restrict__ out) {
+                                                            const float* __restrict__ mix2b, T* __restrict__ out,
+                                                            int use_lut) {
     typedef float f32x4_t __attribute__((ext_vector_type(4)));
     __shared__ AfSmem S;
     const int b = blockIdx.x, i0 = blockIdx.y * 16, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -126,7 +128,7 @@ __global__ __launch_bounds__(256) void afau_row_attn_kernel(const float* __restr
             float sc;
             int s0 = -1;
             float4 bp;
-            if (c >= 0.f && c <= 1.f) {
+            if (use_lut && c >= 0.f && c <= 1.f) {
                 const int bk = min((int)(c * AF_NB), AF_NB - 1);
                 s0 = S.lseg[h][bk];
                 bp = S.lbp[h][bk];
@@ -300,6 +302,14 @@ __global__ __launch_bounds__(64) void afau_head_kernel(const float* __restrict__
 
 }  // namespace
 
+int& afau_lut_flag() {
+    static int v = [] {
+        const char* e = getenv("FPM_AFAU_LUT");
+        return e ? atoi(e) : 2;      // 2 = by dtype
+    }();
+    return v;
+}
+
 extern "C" int fpm_crossset_attn_fwd(int dtype, const float* cost, long c_sb, long c_ld, int B, int n1max, int n2max,
                                      const int* n2, const float* Wv, int emb, const float* mix1w, const float* mix1b,
                                      const float* mix2w, const float* mix2b, void* out, void* stream) {
@@ -308,9 +318,12 @@ extern "C" int fpm_crossset_attn_fwd(int dtype, const float* cost, long c_sb, lo
     dim3 grid(B, (n1max + 15) / 16);
     hipStream_t st = (hipStream_t)stream;
     FPM_CHECK_ARG(n2max <= 640, "crossset_attn: n2max %d > 640", n2max);
+    // fp32 (parity) mode scores with the 16-term sum (the reference's operation order); the LUT is
+    // the bf16 throughput mode's (env FPM_AFAU_LUT / fpm_set_tuning("afau_lut") override)
+    const int lut = afau_lut_flag() != 2 ? afau_lut_flag() : (dtype != 0);
 #define FPM_ATT(TT, TJ_)                                                                                         \
     hipLaunchKernelGGL((afau_row_attn_kernel<TT, TJ_>), grid, dim3(256), 0, st, cost, c_sb, c_ld, n1max, n2max, n2, \
-                       Wv, emb, mix1w, mix1b, mix2w, mix2b, (TT*)out)
+                       Wv, emb, mix1w, mix1b, mix2w, mix2b, (TT*)out, lut)
     if (dtype == 0) { if (n2max <= 256) FPM_ATT(float, 16); else FPM_ATT(float, 40); }
     else { if (n2max <= 256) FPM_ATT(bf16_t, 16); else FPM_ATT(bf16_t, 40); }
 #undef FPM_ATT
