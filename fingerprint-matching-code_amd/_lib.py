@@ -24,6 +24,7 @@ SIGNATURES = {
     "fpm_topk_select": (I, [P, L, L, P, L, P, I, I, I, P, L, L, P, L, L, P]),
     "fpm_gemm": (I, [I, P, L, L, P, P, L, L, I, I, I, I, I, P, P, P, L, L, P, P, P]),
     "fpm_cast_bf16": (I, [P, P, L, P]),
+    "fpm_copy_async": (I, [P, P, L, I, P]),
     "fpm_set_tuning": (I, [ctypes.c_char_p, I]),
     "fpm_spline_plan_bytes": (L, [L, L]),
     "fpm_spline_plan": (I, [P, P, P, L, L, I, P, L, P]),

@@ -110,3 +110,25 @@ extern "C" int fpm_cast_bf16(const float* x, void* y, long n, void* stream) {
     hipLaunchKernelGGL(cast_bf16_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, (bf16_t*)y, n);
     return fpm::check_launch("fpm_cast_bf16");
 }
+
+// Device -> pinned-host copy on a few workgroups.  The runtime's blit copy for this direction
+// launches one 512-thread workgroup per CU for the whole (PCIe-bound) transfer; the transfer needs
+// only enough 16-B stores in flight, so a handful of workgroups keep the CUs for the compute
+// streams.  dst must be device-accessible (pinned host memory); 16-B aligned, bytes % 16 == 0.
+namespace {
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(1024) void copy16_kernel(const u32x4_t* __restrict__ src, u32x4_t* __restrict__ dst, long n) {
+    for (long k = (long)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (long)gridDim.x * blockDim.x)
+        __builtin_nontemporal_store(src[k], dst + k);
+}
+}  // namespace
+
+extern "C" int fpm_copy_async(const void* src, void* dst, long bytes, int nblocks, void* stream) {
+    FPM_CHECK_ARG(((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0 && bytes % 16 == 0,
+                  "copy_async: 16-B aligned pointers and sizes required");
+    if (bytes == 0) return 0;
+    if (nblocks <= 0) nblocks = 16;
+    hipLaunchKernelGGL(copy16_kernel, dim3(nblocks), dim3(1024), 0, (hipStream_t)stream, (const u32x4_t*)src, (u32x4_t*)dst,
+                       bytes / 16);
+    return fpm::check_launch("fpm_copy_async");
+}

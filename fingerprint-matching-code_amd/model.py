@@ -84,11 +84,17 @@ class Net(nn.Module):
         self._stream_cache = {}
         self.n_streams = max(1, int(os.environ.get("FPM_STREAMS", "2")))
         self.tail_splits = int(os.environ.get("FPM_TAIL", "1"))
+        self.head_splits = int(os.environ.get("FPM_HEAD", "0"))
         # FPM_ZERO_COPY=1: soft_topk writes ds_mat straight into pinned host memory instead of a
         # stream copy.  Measured slower (21.2K -> 19.7K pairs/s: the kernel stalls on PCIe writes
         # on the critical path), so off by default.
         self.zero_copy = os.environ.get("FPM_ZERO_COPY", "0") == "1"
         self.copy_stream = os.environ.get("FPM_COPY_STREAM", "1") == "1"
+        # > 0: ds_mat D2H on this many workgroups (fpm_copy_async) instead of the runtime's blit
+        self.copy_blocks = int(os.environ.get("FPM_COPY_BLOCKS", "0"))
+        # the host thread waits for each chunk's ds_mat with a sleeping (not spinning) event wait,
+        # leaving its core to the Hungarian pool
+        self.blocking_wait = os.environ.get("FPM_BLOCKING_WAIT", "1") == "1"
         self._keep_feats = False
         self._stage_timing = os.environ.get("FPM_STAGE_TIMING", "0") == "1"
         self.stage_times = {}
@@ -418,13 +424,16 @@ class Net(nn.Module):
             cs = self._copy_stream(dev)
             cs.wait_event(done)
             with torch.cuda.stream(cs):
-                self._pinned[b0:b1].copy_(o["ds_mat"][b0:b1], non_blocking=True)
-            ev = torch.cuda.Event(enable_timing=True)
+                if self.copy_blocks > 0:
+                    ops.copy_async(self._pinned[b0:b1], o["ds_mat"][b0:b1], self.copy_blocks)
+                else:
+                    self._pinned[b0:b1].copy_(o["ds_mat"][b0:b1], non_blocking=True)
+            ev = torch.cuda.Event(enable_timing=True, blocking=self.blocking_wait)
             ev.record(cs)
             return r, ev
         if not self.zero_copy:
             self._pinned[b0:b1].copy_(o["ds_mat"][b0:b1], non_blocking=True)
-        ev = torch.cuda.Event(enable_timing=True)
+        ev = torch.cuda.Event(enable_timing=True, blocking=self.blocking_wait)
         ev.record(st)
         return r, ev
 
@@ -477,7 +486,7 @@ class Net(nn.Module):
         K = chunks if chunks is not None else self.pipeline_chunks(B)
         if self.compute_ke:
             K = 1          # Ke blocks are padded to per-chunk edge maxima: keep one chunk
-        parts = bt.split(K, self.tail_splits if K > 1 else 0)
+        parts = bt.split(K, self.tail_splits if K > 1 else 0, self.head_splits if K > 1 else 0)
         t0 = time.perf_counter()
         min_pt = torch.minimum(bt.n1, bt.n2).to(torch.float32)
         if gt_perm is None:

@@ -352,3 +352,15 @@ def gnn_layer_bwd_point(X, C, B, n1max, n2max, dXn, dz, params, dX, dagg, V):
             raise _lib.FpmError("gnn_layer_bwd_point: contiguous tensors expected")
     _lib.call("fpm_kron_gnn_layer_bwd_point", _p(X), int(C), int(B), int(n1max), int(n2max), _p(dXn), _p(dz),
               _p(params), _p(dX), _p(dagg), _p(V), _stream(X))
+
+
+def copy_async(dst, src, nblocks=16):
+    """dst.copy_(src) for a device tensor into pinned host memory (or device memory) on a few
+    workgroups of the current stream (fpm_copy_async)."""
+    _dev(src)
+    if not (src.is_contiguous() and dst.is_contiguous()) or src.numel() * src.element_size() != dst.numel() * dst.element_size():
+        raise _lib.FpmError("copy_async: contiguous tensors of equal size expected")
+    if not dst.is_cuda and not dst.is_pinned():
+        raise _lib.FpmError("copy_async: host destination must be pinned")
+    _lib.call("fpm_copy_async", _p(src), _p(dst), src.numel() * src.element_size(), int(nblocks), _stream(src))
+    return dst

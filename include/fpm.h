@@ -61,6 +61,10 @@ int fpm_gemm(int dtype, const void* A, long lda, long sA, const int* a_rows, con
              int N, int K, int batch, int epi, const float* bias, float* Cf, void* Ct, long ldc, long sC,
              const int* n1, const int* n2, void* stream);
 int fpm_cast_bf16(const float* x, void* y, long n, void* stream);
+/* Device -> pinned-host (or device) copy on nblocks workgroups (default 16): the ds_mat hand-off to
+ * the host Hungarian (ngm.py:444 -> utils/hungarian.py:44 .cpu()) without the runtime's
+ * one-workgroup-per-CU blit.  16-B aligned pointers, bytes % 16 == 0. */
+int fpm_copy_async(const void* src, void* dst, long bytes, int nblocks, void* stream);
 
 /* Kernel-variant switches for A/B timing; every variant gives bit-identical results.  Returns the
  * previous value, or -1 (error channel set) for an unknown key.  No reference counterpart.

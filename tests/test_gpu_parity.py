@@ -503,3 +503,12 @@ def test_gnn_kernel_variants_bit_identical(sd):
     for r in outs[1:]:
         for k in ("s", "ss", "ds_mat", "k_prob"):
             assert torch.equal(r[k], outs[0][k]), k
+
+
+def test_copy_async_to_pinned():
+    """fpm_copy_async (few-workgroup D2H into pinned memory; FPM_COPY_BLOCKS switch) copies exactly."""
+    x = torch.randn(3, 77, 64, device=DEV)
+    h = torch.empty(x.shape, pin_memory=True)
+    ops.copy_async(h, x, 8)
+    torch.cuda.synchronize()
+    assert torch.equal(h, x.cpu())
