@@ -74,7 +74,11 @@ class Net(nn.Module):
         if dtype not in ("f32", "bf16"):
             raise ValueError("dtype must be 'f32' or 'bf16'")
         self.dtype_mode = dtype
-        self.lsa_threads = lsa_threads or max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16")), len(os.sched_getaffinity(0))))
+        # Hungarian pool: 2 threads per CPU of the process's share (FPM_LSA_THREADS overrides).  Measured
+        # on the 16-CPU box share: 16 / 32 / 48 threads -> 29-44 / 17-22 / 17-18 ms per 1024 pairs
+        # (the pairs of a chunk differ in cost; idle stragglers at each chunk's join dominate at 1x)
+        share = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16")), len(os.sched_getaffinity(0))))
+        self.lsa_threads = lsa_threads or int(os.environ.get("FPM_LSA_THREADS", str(2 * share)))
         self.chunks = chunks
         # quadratic (edge) affinity Ke (ngm.py:282-289): dead for every output, off by default
         self.compute_ke = compute_ke
