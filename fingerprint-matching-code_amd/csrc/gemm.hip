@@ -74,6 +74,7 @@ int& gemm_phase_flag() {
 int& gnn_packed_flag();
 int& gnn_unroll_flag();
 int& gnn_group_flag();
+int& gnn_group1_flag();
 int& combine_npb_flag();
 int& afau_lut_flag();
 
@@ -83,6 +84,7 @@ extern "C" int fpm_set_tuning(const char* key, int value) {
     else if (key && !strcmp(key, "gnn_packed")) f = &gnn_packed_flag();
     else if (key && !strcmp(key, "gnn_unroll")) f = &gnn_unroll_flag();
     else if (key && !strcmp(key, "gnn_group")) f = &gnn_group_flag();
+    else if (key && !strcmp(key, "gnn_group1")) f = &gnn_group1_flag();
     else if (key && !strcmp(key, "combine_npb")) f = &combine_npb_flag();
     else if (key && !strcmp(key, "afau_lut")) f = &afau_lut_flag();
     if (!f) {

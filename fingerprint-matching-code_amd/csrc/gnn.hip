@@ -285,6 +285,15 @@ int& gnn_group_flag() {
     return u;
 }
 
+// the grouping for the first (1-channel) layer as well: env FPM_GNN_GROUP1 / "gnn_group1"
+int& gnn_group1_flag() {
+    static int u = [] {
+        const char* e = getenv("FPM_GNN_GROUP1");
+        return e ? atoi(e) : 0;
+    }();
+    return u;
+}
+
 // graph-2 neighbour rows loaded U at a time (1, 2 or 3; bit-identical); env FPM_GNN_UNROLL or
 // fpm_set_tuning("gnn_unroll", v)
 int& gnn_unroll_flag() {
@@ -321,7 +330,11 @@ extern "C" int fpm_kron_gnn_layer_fwd(const float* X, int C, int B, int n1max, i
         hipLaunchKernelGGL((gnn_layer_kernel<C_, P_, U_, G_>), g_, t_, sh_, st, X, n1max, n2max, ptr1,           \
                            nbr1, ptr2, nbr2, n1, n2, params, Xout, zbuf, vpart, cls_w, B);                       \
     } while (0)
-    if (C == 1) { if (packed) FPM_GNN(1, true, 1, 1); else FPM_GNN(1, false, 1, 1); }
+    if (C == 1) {
+        if (!packed) FPM_GNN(1, false, 1, 1);
+        else if (grp == 2 && gnn_group1_flag()) FPM_GNN(1, true, 1, 2);
+        else FPM_GNN(1, true, 1, 1);
+    }
     else if (!packed) FPM_GNN(17, false, 1, 1);
     else if (grp == 2) FPM_GNN(17, true, 1, 2);
     else if (grp == 4) FPM_GNN(17, true, 1, 4);

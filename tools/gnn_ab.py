@@ -16,19 +16,21 @@ bt = DeviceBatch.from_pairs(synth.make_batch(3, B, n), dev)
 wp = fpm.Net(regression=True, dtype="bf16").packed(dev)
 plans = [ops.spline_plan(bt.src[s], bt.dst[s], bt.pseudo[s], B * n, n) for s in range(2)]
 csr = [ops.plan_csr(plans[s], bt.E[s], B * n) for s in range(2)]
-X = torch.randn(B, 17, n, n, device=dev)
+C = int(os.environ.get("C", 17))
+X = torch.randn(B, C, n, n, device=dev)
+key_w = "gnn1" if C == 17 else "gnn0"
 ref = None
 for key, val in [(k, int(v)) for k, v in (a.split("=") for a in sys.argv[1:])]:
     prev = ops.set_tuning(key, val)
-    Xn = torch.zeros_like(X)
+    Xn = torch.zeros(B, 17, n, n, device=dev)
     z = torch.zeros(B, n, n, device=dev)
     for _ in range(3):
-        ops.gnn_layer(X, 17, B, n, n, csr[0], csr[1], bt.n1, bt.n2, wp["gnn1"], Xn, z)
+        ops.gnn_layer(X, C, B, n, n, csr[0], csr[1], bt.n1, bt.n2, wp[key_w], Xn, z)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(20):
-        ops.gnn_layer(X, 17, B, n, n, csr[0], csr[1], bt.n1, bt.n2, wp["gnn1"], Xn, z)
+        ops.gnn_layer(X, C, B, n, n, csr[0], csr[1], bt.n1, bt.n2, wp[key_w], Xn, z)
     e1.record()
     torch.cuda.synchronize()
     out = (Xn[:, :16].clone(), z.clone())
