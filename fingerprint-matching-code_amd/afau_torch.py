@@ -25,11 +25,13 @@ def _block(a, bemb, cost, g):
     b1 = g("mixed_score_MHA.mix1_bias")                                        # (H, MS)
     w2 = g("mixed_score_MHA.mix2_weight")                                      # (H, MS, 1)
     b2 = g("mixed_score_MHA.mix2_bias")                                        # (H, 1)
-    # mixed score per head: relu([dot, cost] W1_h + b1_h) W2_h + b2_h
-    cs = cost[:, None]                                                         # (B, 1, R, Cn)
-    h1 = dot[..., None] * w1[None, :, None, None, 0, :] + cs[..., None] * w1[None, :, None, None, 1, :]
-    h1 = F.relu(h1 + b1[None, :, None, None, :])                               # (B, H, R, Cn, MS)
-    mixed = torch.matmul(h1, w2[None, :, None]).squeeze(-1) + b2[None, :, None, :]
+    # mixed score per head: relu([dot, cost] W1_h + b1_h) W2_h + b2_h, in the reference's matmul
+    # form (afau.py:245-262).  Its rounding matters: the regressor's gradient jumps at the ReLU
+    # kinks and the max pool, so a reordered sum (e.g. one hidden unit at a time) lands on other
+    # branches for some entries and moves the FFN gradients by O(10 %).
+    two = torch.stack((dot, cost[:, None].expand_as(dot)), dim=4).transpose(1, 2)   # (B, R, H, Cn, 2)
+    ms1 = torch.matmul(two, w1) + b1[None, None, :, None, :]
+    mixed = (torch.matmul(F.relu(ms1), w2) + b2[None, None, :, None, :]).transpose(1, 2).squeeze(4)
     att = torch.softmax(mixed, dim=3)
     out = torch.matmul(att, v).transpose(1, 2).reshape(B, R, H * D)
     mh = F.linear(out, g("multi_head_combine.weight"), g("multi_head_combine.bias"))
@@ -55,9 +57,17 @@ def afau_ks(ss, n1, n2, P):
             & (idx[None, :, None] < n2.to(dev).view(-1, 1, 1))).to(dt)          # one-hot rows (ngm.py:391-395)
     pre = "encoder_k.layers.0."
     r = _block(row0, col0, ss, lambda k: P(pre + "row_encoding_block." + k))
-    c = _block(col0, row0, ss.transpose(1, 2), lambda k: P(pre + "col_encoding_block." + k))
+    # the column block reads one-hot rows against zero rows (k = v = 0): it depends on n2 only, so
+    # it runs once per distinct n2 and is gathered (gradients sum over the pairs sharing it)
+    n2c = n2.to(dev).view(-1)
+    n2u, inv = torch.unique(n2c, return_inverse=True)
+    col0u = ((idx[None, :, None] == torch.arange(C.UNIV_SIZE, device=dev)[None, None, :])
+             & (idx[None, :, None] < n2u.view(-1, 1, 1))).to(dt)
+    row0u = torch.zeros(n2u.numel(), n1max, C.UNIV_SIZE, device=dev, dtype=dt)
+    costu = torch.zeros(n2u.numel(), n2max, n1max, device=dev, dtype=dt)     # unused: v = 0
+    c = _block(col0u, row0u, costu, lambda k: P(pre + "col_encoding_block." + k))
     gr = r.max(dim=1).values        # pad to UNIV_SIZE with -inf + MaxPool1d (ngm.py:401-404)
-    gc = c.max(dim=1).values
+    gc = c.max(dim=1).values[inv]
     kr = F.linear(F.relu(F.linear(gr, P("final_row.0.weight"), P("final_row.0.bias"))),
                   P("final_row.2.weight"), P("final_row.2.bias")).squeeze(-1)
     kc = F.linear(F.relu(F.linear(gc, P("final_col.0.weight"), P("final_col.0.bias"))),
