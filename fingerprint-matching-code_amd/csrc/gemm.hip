@@ -77,6 +77,7 @@ int& gnn_group_flag();
 int& gnn_group1_flag();
 int& combine_npb_flag();
 int& afau_lut_flag();
+int& sinkhorn_fast_flag();
 
 extern "C" int fpm_set_tuning(const char* key, int value) {
     int* f = nullptr;
@@ -87,6 +88,7 @@ extern "C" int fpm_set_tuning(const char* key, int value) {
     else if (key && !strcmp(key, "gnn_group1")) f = &gnn_group1_flag();
     else if (key && !strcmp(key, "combine_npb")) f = &combine_npb_flag();
     else if (key && !strcmp(key, "afau_lut")) f = &afau_lut_flag();
+    else if (key && !strcmp(key, "sinkhorn_fast")) f = &sinkhorn_fast_flag();
     if (!f) {
         fpm::set_error("fpm_set_tuning: unknown key '%s'", key ? key : "(null)");
         return -1;

@@ -10,6 +10,7 @@
 // dummy_row and rows < cols, output exp(L) on the block and 0 in the padding.
 // Arithmetic runs in log2 units (L2 = L log2 e): every exp/log is one native v_exp_f32 / v_log_f32.
 #include "fpm_common.h"
+#include <cstdlib>
 
 namespace {
 
@@ -25,6 +26,7 @@ struct SinkArgs {
     float tau;
     int dummy_row;
     int contig_j;  // 1: j (column) is the unit-stride dimension of in/out
+    int fast;      // shifted single-pass lse after the first step (sinkhorn_reg_kernel)
 };
 
 __device__ __forceinline__ void lse_combine(float& m, float& s, float mo, float so) {
@@ -53,6 +55,7 @@ __global__ __launch_bounds__(1024) void sinkhorn_reg_kernel(SinkArgs a) {
     __shared__ float red_s[16][NCOL];
     __shared__ float fin[NCOL];
     __shared__ float blk_m[16], blk_s[16];
+    __shared__ int redo_flag;
 
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
@@ -95,10 +98,27 @@ __global__ __launch_bounds__(1024) void sinkhorn_reg_kernel(SinkArgs a) {
     float ud = 0.f;  // potential of the (identical) dummy rows
     const float DUMMY = -100.f * fpm::LOG2E_F;   // the dummy rows' log value, in log2 units
 
+    // Shifted single-pass lse (fast = true, every step after the first): after a normalisation
+    // along one axis every entry is <= 0 in log space, so the other axis' lse can be shifted by its
+    // own previous potential instead of a max pass -- one exp per entry, no max reduction.  A sum
+    // outside [2^-30, 2^30] (unnormalised input, extreme lines) falls back to the max-shifted form.
+    auto ok_s = [](float x) { return x >= 0x1p-30f && x <= 0x1p30f; };
     // potR[e] = lse_f(M - pC) (+ dummy term)
-    auto update_R = [&](bool add_dummy) {
+    auto update_R = [&](bool add_dummy, bool fast) {
 #pragma unroll
         for (int e = 0; e < ER; ++e) {
+            if (fast) {
+                const float sh = pR[e];
+                float s = 0.f;
+#pragma unroll
+                for (int f = 0; f < EC; ++f) s += fpm::fast_exp2(M[e][f] - pC[f] - sh);
+                s = lane32_sum(s);
+                if (add_dummy) s += (float)nd * fpm::fast_exp2(DUMMY - ud - sh);
+                if (ok_s(s)) {
+                    pR[e] = sh + fpm::fast_log2(s);
+                    continue;
+                }
+            }
             float m = -INFINITY;
 #pragma unroll
             for (int f = 0; f < EC; ++f) m = fmaxf(m, M[e][f] - pC[f]);
@@ -116,7 +136,36 @@ __global__ __launch_bounds__(1024) void sinkhorn_reg_kernel(SinkArgs a) {
         }
     };
     // potC[f] = lse_e(M - pR) (+ dummy term): across the 32 thread-rows via LDS
-    auto update_C = [&](bool add_dummy) {
+    auto update_C = [&](bool add_dummy, bool fast) {
+        if (fast) {
+#pragma unroll
+            for (int f = 0; f < EC; ++f) {
+                float s = 0.f;
+#pragma unroll
+                for (int e = 0; e < ER; ++e) s += fpm::fast_exp2(M[e][f] - pR[e] - pC[f]);
+                s += __shfl_xor(s, 32);
+                if ((tid & 63) < 32) red_s[wv][tc + 32 * f] = s;
+                if (tr == 0) fin[tc + 32 * f] = pC[f];            // the old potentials (shifts)
+            }
+            __syncthreads();
+            if (tid < NCOL) {
+                float s = red_s[0][tid];
+                for (int w = 1; w < 16; ++w) s += red_s[w][tid];
+                const float sh = fin[tid];
+                if (add_dummy) s += (float)nd * fpm::fast_exp2(DUMMY - ud - sh);
+                // columns past the valid block carry no entries (only the dummy term, as below)
+                if (tid >= limPC) red_m[0][tid] = add_dummy ? (DUMMY - ud) + lognd : 0.f;
+                else if (ok_s(s)) red_m[0][tid] = sh + fpm::fast_log2(s);
+                else redo_flag = 1;                               // any failure: redo the step
+            }
+            __syncthreads();
+            const bool redo = redo_flag != 0;
+            if (!redo) {
+#pragma unroll
+                for (int f = 0; f < EC; ++f) pC[f] = red_m[0][tc + 32 * f];
+                return;
+            }
+        }
 #pragma unroll
         for (int f = 0; f < EC; ++f) {
             float m = -INFINITY;
@@ -144,6 +193,10 @@ __global__ __launch_bounds__(1024) void sinkhorn_reg_kernel(SinkArgs a) {
         __syncthreads();
 #pragma unroll
         for (int f = 0; f < EC; ++f) pC[f] = fin[tc + 32 * f];
+        if (fast) {   // reset the redo flag (read by every thread above, before this barrier)
+            if (tid == 0) redo_flag = 0;
+            __syncthreads();
+        }
     };
     // ud = lse over valid algorithmic columns of (-100 - v)
     auto update_dummy = [&]() {
@@ -178,12 +231,15 @@ __global__ __launch_bounds__(1024) void sinkhorn_reg_kernel(SinkArgs a) {
         }
     };
 
+    if (tid == 0) redo_flag = 0;
+    __syncthreads();
     for (int it = 0; it < a.iters; ++it) {
+        const bool fast = it > 0 && a.fast;
         if ((it & 1) == 0) {           // row normalisation: update u
-            if (u_on_R) update_R(false); else update_C(false);
+            if (u_on_R) update_R(false, fast); else update_C(false, fast);
             if (nd > 0) update_dummy();
         } else {                       // column normalisation: update v
-            if (u_on_R) update_C(nd > 0); else update_R(nd > 0);
+            if (u_on_R) update_C(nd > 0, fast); else update_R(nd > 0, fast);
         }
     }
     (void)lognd;
@@ -320,6 +376,15 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
 
 }  // namespace
 
+// shifted single-pass lse steps (env FPM_SINKHORN_FAST / fpm_set_tuning("sinkhorn_fast"))
+int& sinkhorn_fast_flag() {
+    static int v = [] {
+        const char* e = getenv("FPM_SINKHORN_FAST");
+        return e ? atoi(e) : 1;
+    }();
+    return v;
+}
+
 extern "C" int fpm_sinkhorn_log_fwd(const float* s, long s_sb, long s_si, long s_sj, float* out,
                                     long o_sb, long o_si, long o_sj, const int* n1, const int* n2,
                                     int B, int n1max, int n2max, int iters, float tau, int dummy_row,
@@ -334,6 +399,7 @@ extern "C" int fpm_sinkhorn_log_fwd(const float* s, long s_sb, long s_si, long s
     a.n1 = n1; a.n2 = n2; a.n1max = n1max; a.n2max = n2max;
     a.iters = iters; a.tau = tau; a.dummy_row = dummy_row;
     a.contig_j = (s_sj == 1) ? 1 : 0;
+    a.fast = sinkhorn_fast_flag();
     FPM_CHECK_ARG(s_sj == 1 || s_si == 1, "sinkhorn: one of the input's row/column strides must be 1");
     int nmax = n1max > n2max ? n1max : n2max;
     hipStream_t st = (hipStream_t)stream;

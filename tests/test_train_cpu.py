@@ -53,3 +53,26 @@ def test_afau_replay_equals_oracle():
     ref = O.afau_ks(ss, n1, n2, sdd)
     ours = afau_torch.afau_ks(ss, n1, n2, lambda k: sdd[k])
     assert (ref - ours).abs().max() < 1e-12
+
+
+def test_afau_replay_gradients_equal_oracle():
+    """The training backward's AFA-U gradients are autograd through fpm.afau_torch: in float64 at
+    the same ss they equal autograd through the oracle's AFA-U (same formulation)."""
+    sd = params.init_params(6)
+    g = torch.Generator().manual_seed(2)
+    n1, n2 = torch.tensor([12, 9, 12]), torch.tensor([10, 12, 12])
+    ss = torch.rand(3, 12, 12, generator=g, dtype=torch.float64)
+    names = [k for k in sd if k.startswith(afau_torch.AFAU_PARAM_PREFIXES)]
+    a = {k: sd[k].double().clone().requires_grad_(True) for k in names}
+    b = {k: sd[k].double().clone().requires_grad_(True) for k in names}
+    sdd = {k: v.double() if v.is_floating_point() else v for k, v in sd.items()}
+    sdd.update(b)
+    w = torch.tensor([0.3, -1.0, 0.7], dtype=torch.float64)
+    (afau_torch.afau_ks(ss, n1, n2, lambda k: a[k]) * w).sum().backward()
+    (O.afau_ks(ss, n1, n2, sdd) * w).sum().backward()
+    for k in names:
+        ga, gb = a[k].grad, b[k].grad
+        if gb is None:
+            assert ga is None or float(ga.abs().max()) == 0.0, k
+            continue
+        assert float((ga - gb).abs().max()) <= 1e-9 * max(1.0, float(gb.abs().max())), k
