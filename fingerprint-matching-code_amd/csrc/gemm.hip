@@ -78,6 +78,7 @@ int& gnn_group1_flag();
 int& combine_npb_flag();
 int& afau_lut_flag();
 int& sinkhorn_fast_flag();
+int& soft_topk_fast_flag();
 
 extern "C" int fpm_set_tuning(const char* key, int value) {
     int* f = nullptr;
@@ -89,6 +90,7 @@ extern "C" int fpm_set_tuning(const char* key, int value) {
     else if (key && !strcmp(key, "combine_npb")) f = &combine_npb_flag();
     else if (key && !strcmp(key, "afau_lut")) f = &afau_lut_flag();
     else if (key && !strcmp(key, "sinkhorn_fast")) f = &sinkhorn_fast_flag();
+    else if (key && !strcmp(key, "topk_fast")) f = &soft_topk_fast_flag();
     if (!f) {
         fpm::set_error("fpm_set_tuning: unknown key '%s'", key ? key : "(null)");
         return -1;

@@ -10,6 +10,7 @@
 // Values are kept in log2 units (L2 = L log2 e; the test L > 0 is unit-free), so each exp/log is
 // one native v_exp_f32 / v_log_f32.
 #include "fpm_common.h"
+#include <cstdlib>
 
 namespace {
 
@@ -29,7 +30,8 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
                                                          const float* __restrict__ kvec, float* __restrict__ out,
                                                          long ob, long old_, int n1max, int n2max, int iters,
                                                          float tau, int* __restrict__ steps_out,
-                                                         float* __restrict__ out2, long ob2, long old2) {
+                                                         float* __restrict__ out2, long ob2, long old2,
+                                                         int fast_cols) {
     __shared__ float sa[16], sb_[16];
     __shared__ int sflag[16];
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -130,8 +132,35 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
         }
         last = 1;
     };
-    auto colstep = [&]() {   // always follows a row step
+    // fast: one pass shifted by the column's log target instead of a max pass (every entry of a
+    // row-normalised L is <= 0, and a column's sum stays within 2^+-30 of its target here; a sum
+    // outside that range falls back).  Used for the column steps before the last fixed step, so
+    // the value the continuation test reads comes from the reference's max-shifted form.
+    auto colstep = [&](bool fast) {   // always follows a row step
         float mnl, mxl;
+        if (fast) {
+            anchors(mnl, mxl);
+            float a0 = 0.f, a1 = 0.f;
+            forq([&](int k, float sv) {
+                float L0, L1;
+                Lpair(sv, mnl, mxl, L0, L1);
+                a0 += fpm::fast_exp2(L0 - lcp0);
+                a1 += fpm::fast_exp2(L1 - lcp1);
+            });
+            a0 = fpm::warp_sum(a0);
+            a1 = fpm::warp_sum(a1);
+            if (lane == 0) { sa[wv] = a0; sb_[wv] = a1; }
+            __syncthreads();
+            a0 = 0.f; a1 = 0.f;
+            for (int w = 0; w < 16; ++w) { a0 += sa[w]; a1 += sb_[w]; }
+            __syncthreads();
+            if (a0 >= 0x1p-30f && a0 <= 0x1p30f && a1 >= 0x1p-30f && a1 <= 0x1p30f) {
+                lse0 = lcp0 + fpm::fast_log2(a0);
+                lse1 = lcp1 + fpm::fast_log2(a1);
+                last = 2;
+                return;
+            }
+        }
         anchors(mnl, mxl);
         float m0 = -INFINITY, m1 = -INFINITY;
         forq([&](int k, float sv) {
@@ -186,11 +215,11 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
 
     int step = 0;
     for (; step < iters; ++step) {
-        if (step & 1) colstep();
+        if (step & 1) colstep(fast_cols && step + 2 < iters);
         else rowstep();
     }
     for (int guard = 0; guard < 64 && any_pos(); ++guard, ++step) {
-        if (step & 1) colstep();
+        if (step & 1) colstep(false);
         else rowstep();
     }
     if (steps_out && tid == 0) steps_out[b] = step;
@@ -310,6 +339,15 @@ __global__ __launch_bounds__(256) void topk_select_kernel(const float* __restric
 
 }  // namespace
 
+// single-pass early column steps (env FPM_TOPK_FAST / fpm_set_tuning("topk_fast"))
+int& soft_topk_fast_flag() {
+    static int v = [] {
+        const char* e = getenv("FPM_TOPK_FAST");
+        return e ? atoi(e) : 1;
+    }();
+    return v;
+}
+
 extern "C" int fpm_soft_topk_fwd(const float* ss, long s_sb, long s_ld, const int* n1, const int* n2,
                                  const float* k, int B, int n1max, int n2max, int iters, float tau,
                                  float* out, long o_sb, long o_ld, int* steps_out, float* out2, long o2_sb,
@@ -321,7 +359,8 @@ extern "C" int fpm_soft_topk_fwd(const float* ss, long s_sb, long s_ld, const in
     hipStream_t st = (hipStream_t)stream;
 #define LAUNCH(NQ, ST) hipLaunchKernelGGL((soft_topk_kernel<NQ, ST>), dim3(B), dim3(1024), 0, st, ss, s_sb, s_ld, \
                                            n1, n2, k, out, o_sb, o_ld, n1max, n2max, iters, tau, steps_out, \
-                                           out2, o2_sb, o2_ld)
+                                           out2, o2_sb, o2_ld, fast)
+    const int fast = soft_topk_fast_flag();
     if (nn <= 1024) LAUNCH(1, false);
     else if (nn <= 4096) LAUNCH(4, false);
     else if (nn <= 16384) LAUNCH(16, false);
