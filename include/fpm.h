@@ -66,11 +66,19 @@ int fpm_cast_bf16(const float* x, void* y, long n, void* stream);
  * one-workgroup-per-CU blit.  16-B aligned pointers, bytes % 16 == 0. */
 int fpm_copy_async(const void* src, void* dst, long bytes, int nblocks, void* stream);
 
-/* Kernel-variant switches for A/B timing; every variant gives bit-identical results.  Returns the
+/* Kernel-variant switches for A/B timing.  Returns the
  * previous value, or -1 (error channel set) for an unknown key.  No reference counterpart.
  *   "gemm_phase" (env FPM_GEMM_PHASE, default 1): 256x256 bf16 GEMM tiles on the phase-pipelined
  *                kernel (1) or the two-stage kernel (0)
- *   "gnn_packed" (env FPM_GNN_PACKED, default 1): GNN-layer MLPs on packed (1) or scalar (0) FMAs */
+ *   "gnn_packed" (env FPM_GNN_PACKED, default 1): GNN-layer MLPs on packed (1) or scalar (0) FMAs
+ *   "gnn_group"  (FPM_GNN_GROUP, default 2): graph-2 nodes per GNN workgroup (1, 2, 4; n1max <= 256)
+ *   "gnn_group1" (FPM_GNN_GROUP1, default 0): the same for the 1-channel first layer
+ *   "gnn_unroll" (FPM_GNN_UNROLL, default 1): graph-2 neighbour rows loaded 1, 2 or 3 at a time
+ *   "combine_npb" (FPM_COMBINE_NPB, default 4): destination nodes per SplineConv combine workgroup
+ * Switches whose variants round differently (results within fp32 rounding, not bit-identical):
+ *   "sinkhorn_fast" (FPM_SINKHORN_FAST, default 1): shifted single-pass lse after the first step
+ *   "topk_fast" (FPM_TOPK_FAST, default 1): shifted single-pass early soft top-k column steps
+ *   "afau_lut" (FPM_AFAU_LUT, default 2 = by dtype): AFA-U score lookup table (1) or 16-term sum (0) */
 int fpm_set_tuning(const char* key, int value);
 
 /* ---- SplineConv message passing ---------------------------------------------------------------
