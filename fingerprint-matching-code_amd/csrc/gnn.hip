@@ -63,10 +63,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(PACKED ? 5
     __shared__ int nb2_[G][64];
     __shared__ int nnb2_[G], beg2_[G];
 
-    // G > 1: G graph-2 nodes per workgroup, one 256-thread group each (n1max <= 256)
-    constexpr int SUBW = G > 1 ? 256 : 1024;
-    const int sub = G > 1 ? (int)threadIdx.x / SUBW : 0;
-    const int i = G > 1 ? (int)threadIdx.x - sub * SUBW : (int)threadIdx.x;
+    // G > 1: G graph-2 nodes per workgroup, one thread group of blockDim / G each
+    const int subw = G > 1 ? (int)blockDim.x / G : (int)blockDim.x;
+    const int sub = G > 1 ? (int)threadIdx.x / subw : 0;
+    const int i = G > 1 ? (int)threadIdx.x - sub * subw : (int)threadIdx.x;
     int dg, b;
     if (!pair_block((n2max + G - 1) / G, B, b, dg)) return;
     const int d = dg * G + sub;
@@ -318,7 +318,8 @@ extern "C" int fpm_kron_gnn_layer_fwd(const float* X, int C, int B, int n1max, i
     const int threads = (n1max + 63) / 64 * 64;
     const bool packed = gnn_packed_flag() != 0;
     const int un = gnn_unroll_flag();
-    const int grp = n1max <= 256 ? gnn_group_flag() : 1;   // default 2: 21% faster at n = 256
+    // default 2 (21% faster at n = 256, 13% at n = 100; slower as a 1024-thread workgroup at n = 512)
+    const int grp = gnn_group_flag() * threads <= 512 ? gnn_group_flag() : 1;
 #define FPM_GNN(C_, P_, U_, G_)                                                                                  \
     do {                                                                                                         \
         const size_t sh_ = sh * G_;                                                                              \
@@ -326,7 +327,7 @@ extern "C" int fpm_kron_gnn_layer_fwd(const float* X, int C, int B, int n1max, i
             (void)hipFuncSetAttribute((const void*)gnn_layer_kernel<C_, P_, U_, G_>,                             \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh_);                     \
         const dim3 g_(pair_grid((n2max + G_ - 1) / G_, B));                                                      \
-        const dim3 t_(G_ > 1 ? 256 * G_ : threads);                                                              \
+        const dim3 t_(threads * G_);                                                                             \
         hipLaunchKernelGGL((gnn_layer_kernel<C_, P_, U_, G_>), g_, t_, sh_, st, X, n1max, n2max, ptr1,           \
                            nbr1, ptr2, nbr2, n1, n2, params, Xout, zbuf, vpart, cls_w, B);                       \
     } while (0)
