@@ -295,7 +295,8 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
     const bool u_on_A = (a.contig_j != 0) == (!transposed);
     const float* in = a.in + (long)b * a.in_sb;
     const long sA = a.contig_j ? a.in_si : a.in_sj, sC = a.contig_j ? a.in_sj : a.in_si;
-    auto val = [&](int ia, int ic) { return (in[ia * sA + ic * sC] / a.tau) * fpm::LOG2E_F; };
+    const float vscale = fpm::LOG2E_F / a.tau;   // one multiply per element read (not a division)
+    auto val = [&](int ia, int ic) { return in[ia * sA + ic * sC] * vscale; };
     (void)scale;
     for (int k = tid; k < SK_MAXN; k += 1024) { potA[k] = 0.f; potC[k] = 0.f; }
     if (tid == 0) ud_sh = 0.f;
@@ -306,6 +307,7 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
         const float ud = ud_sh;
         for (int ia = wv; ia < limA; ia += 16) {
             float m = -INFINITY, s = 0.f;
+#pragma unroll 8
             for (int ic = lane; ic < limC; ic += 64) lse_push(m, s, val(ia, ic) - potC[ic]);
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) {
@@ -326,6 +328,7 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
             const int ic = c0 + (groups == 1 ? tid : tid % cpad), grp = groups == 1 ? 0 : tid / cpad;
             float m = -INFINITY, s = 0.f;
             if (ic < limC && grp < groups)
+#pragma unroll 8
                 for (int ia = grp; ia < limA; ia += groups) lse_push(m, s, val(ia, ic) - potA[ia]);
             red_m[tid] = m;
             red_s[tid] = s;
