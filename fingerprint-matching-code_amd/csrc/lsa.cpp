@@ -410,15 +410,136 @@ __attribute__((target("avx512f,avx512dq"))) int lsap_solve_dense512(int nr, int 
     return 0;
 }
 
-// 0 scalar, 1 AVX2, 2 AVX-512 (FPM_LSA_SCALAR=1 / FPM_LSA_AVX2=1 force the narrower paths)
+// Same solver reading float32 costs straight from the caller's rows (cost = -s, converted to
+// double per lane as scipy does, so every reduced cost is bit-identical), with the remaining-set
+// as a bit mask, and ONE pass per Dijkstra step: each lane tracks its minimum together with the
+// tie keys of the holders (largest scan position among unassigned holders, smallest position
+// among all), which select the same column as the scalar tie rule without a second scan.
+// The float rows hold s (cost = -s); visited rows / columns are kept as lists.
+__attribute__((target("avx512f,avx512dq,avx512vl,avx512bw"))) int lsap_solve_f512(int nr, int nc, const float* cost, long ld,
+                                                                                 std::vector<int>& col4row) {
+    const int ncp = (nc + 7) & ~7;
+    std::vector<double> u(nr, 0.0), v(ncp, 0.0), spc(ncp);
+    std::vector<unsigned char> remb(ncp / 8);
+    std::vector<int> path(ncp, -1);
+    std::vector<int> row4col(ncp, -1), remaining(nc), pos(ncp, 0);   // ncp: read 8 lanes at a time
+    std::vector<int> rows_v, cols_v;     // rows / columns visited by this row's search
+    col4row.assign(nr, -1);
+    const __m512d vinf = _mm512_set1_pd(INFINITY);
+    const __m512i lane = _mm512_set_epi64(7, 6, 5, 4, 3, 2, 1, 0);
+    const __m512i one = _mm512_set1_epi64(1);
+    const unsigned char tailm = (unsigned char)((nc & 7) ? ((1u << (nc & 7)) - 1) : 0xff);
+    for (int cur = 0; cur < nr; ++cur) {
+        double minVal = 0.0;
+        int i = cur;
+        int num = nc;
+        for (int it = 0; it < nc; ++it) {
+            remaining[it] = nc - it - 1;
+            pos[nc - it - 1] = it;
+        }
+        for (int q = 0; q < ncp / 8; ++q) remb[q] = 0xff;
+        remb[ncp / 8 - 1] = tailm;
+        for (int j = 0; j < ncp; ++j) spc[j] = INFINITY;
+        rows_v.clear();
+        cols_v.clear();
+        int sink = -1;
+        while (sink == -1) {
+            rows_v.push_back(i);
+            const float* srow = cost + (long)i * ld;
+            const __m512d vmv = _mm512_set1_pd(minVal), vui = _mm512_set1_pd(u[i]);
+            const __m256i vi = _mm256_set1_epi32(i);
+            // one pass: relax the reduced costs and, per lane, track the minimum with its holders'
+            // tie keys -- the largest scan position among unassigned holders (bu) and the smallest
+            // position among all holders (bf) -- which decide ties as the scalar loop does
+            const __m256i m1 = _mm256_set1_epi32(-1), big = _mm256_set1_epi32(0x7fffffff);
+            __m512d vlow[2] = {vinf, vinf};
+            __m256i bu[2] = {m1, m1}, bf[2] = {big, big};
+#define FPM_LSA_STEP(jj, a)                                                                                   \
+    {                                                                                                         \
+        const int j_ = (jj);                                                                                  \
+        const __mmask8 m = remb[j_ >> 3];                                                                     \
+        const __m512d c = _mm512_cvtps_pd(_mm256_maskz_loadu_ps(m, srow + j_));                              \
+        const __m512d r = _mm512_sub_pd(_mm512_sub_pd(_mm512_sub_pd(vmv, c), vui), _mm512_loadu_pd(&v[j_])); \
+        __m512d sv = _mm512_loadu_pd(&spc[j_]);                                                               \
+        const __mmask8 lt = _mm512_mask_cmp_pd_mask(m, r, sv, _CMP_LT_OQ);                                    \
+        sv = _mm512_mask_blend_pd(lt, sv, r);                                                                 \
+        _mm512_storeu_pd(&spc[j_], sv);                                                                       \
+        _mm256_mask_storeu_epi32(&path[j_], lt, vi);                                                          \
+        const __mmask8 nl = _mm512_mask_cmp_pd_mask(m, sv, vlow[a], _CMP_LT_OQ);                              \
+        const __mmask8 eq = _mm512_mask_cmp_pd_mask(m, sv, vlow[a], _CMP_EQ_OQ);                              \
+        const __m256i P = _mm256_loadu_si256((const __m256i*)&pos[j_]);                                       \
+        const __mmask8 un = _mm256_cmpeq_epi32_mask(_mm256_loadu_si256((const __m256i*)&row4col[j_]), m1);    \
+        const __m256i uk = _mm256_mask_mov_epi32(m1, un, P);                                                  \
+        vlow[a] = _mm512_mask_blend_pd(nl, vlow[a], sv);                                                      \
+        bu[a] = _mm256_mask_max_epi32(_mm256_mask_mov_epi32(bu[a], nl, uk), eq, bu[a], uk);                   \
+        bf[a] = _mm256_mask_min_epi32(_mm256_mask_mov_epi32(bf[a], nl, P), eq, bf[a], P);                     \
+    }
+            int jj = 0;
+            for (; jj + 16 <= ncp; jj += 16) {
+                FPM_LSA_STEP(jj, 0)
+                FPM_LSA_STEP(jj + 8, 1)
+            }
+            if (jj < ncp) FPM_LSA_STEP(jj, 0)
+#undef FPM_LSA_STEP
+            // merge the two accumulators lane-wise, then across lanes
+            {
+                const __mmask8 lo1 = _mm512_cmp_pd_mask(vlow[1], vlow[0], _CMP_LT_OQ);
+                const __mmask8 eq1 = _mm512_cmp_pd_mask(vlow[1], vlow[0], _CMP_EQ_OQ);
+                vlow[0] = _mm512_mask_blend_pd(lo1, vlow[0], vlow[1]);
+                bu[0] = _mm256_mask_max_epi32(_mm256_mask_mov_epi32(bu[0], lo1, bu[1]), eq1, bu[0], bu[1]);
+                bf[0] = _mm256_mask_min_epi32(_mm256_mask_mov_epi32(bf[0], lo1, bf[1]), eq1, bf[0], bf[1]);
+            }
+            const double lowest = _mm512_reduce_min_pd(vlow[0]);
+            if (lowest == INFINITY) return -1;
+            const __mmask8 at = _mm512_cmp_pd_mask(vlow[0], _mm512_set1_pd(lowest), _CMP_EQ_OQ);
+            alignas(32) int bua[8], bfa[8];
+            _mm256_store_si256((__m256i*)bua, bu[0]);
+            _mm256_store_si256((__m256i*)bfa, bf[0]);
+            int pu = -1, pf = 0x7fffffff;
+            for (int q = 0; q < 8; ++q)
+                if (at & (1 << q)) {
+                    pu = std::max(pu, bua[q]);
+                    pf = std::min(pf, bfa[q]);
+                }
+            const int j = remaining[pu >= 0 ? pu : pf];
+            minVal = lowest;
+            remb[j >> 3] &= (unsigned char)~(1u << (j & 7));
+            const int p = pos[j], last = remaining[--num];
+            remaining[p] = last;
+            pos[last] = p;
+            if (row4col[j] == -1) sink = j;
+            else i = row4col[j];
+            cols_v.push_back(j);
+        }
+        u[cur] += minVal;
+        for (int r : rows_v)
+            if (r != cur) u[r] += minVal - spc[col4row[r]];
+        for (int c : cols_v) v[c] -= minVal - spc[c];
+        int j = sink;
+        while (true) {
+            const int r = path[j];
+            row4col[j] = r;
+            std::swap(col4row[r], j);
+            if (r == cur) break;
+        }
+    }
+    return 0;
+}
+
+
+// 0 scalar, 1 AVX2, 2 AVX-512 dense scan, 3 AVX-512 float rows + one-pass ties (default where
+// available).  FPM_LSA_SCALAR=1 / FPM_LSA_AVX2=1 / FPM_LSA_DENSE512=1 force the older paths.
 int lsa_isa() {
 #if defined(__x86_64__)
     static int isa = -1;
     if (isa < 0) {
         const char* e = getenv("FPM_LSA_SCALAR");
         const char* a = getenv("FPM_LSA_AVX2");
+        const char* d = getenv("FPM_LSA_DENSE512");
+        const bool f512 = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512dq");
+        const bool vlbw = __builtin_cpu_supports("avx512vl") && __builtin_cpu_supports("avx512bw");
         if (e && e[0] == '1') isa = 0;
-        else if (__builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512dq") && !(a && a[0] == '1')) isa = 2;
+        else if (f512 && !(a && a[0] == '1')) isa = (vlbw && !(d && d[0] == '1')) ? 3 : 2;
         else isa = __builtin_cpu_supports("avx2") ? 1 : 0;
     }
     return isa;
@@ -434,6 +555,35 @@ int lsa_pair(const float* s, long ld, int n1, int n2, int* assign, int n1max) {
     if (n1 <= 0 || n2 <= 0) return 0;
     const bool tr = n2 < n1;
     const int nr = tr ? n2 : n1, nc = tr ? n1 : n2;
+#if defined(__x86_64__)
+    if (lsa_isa() == 3) {
+        // s's float rows (or its transpose's) are the cost rows; cost = -s inside the scan
+        for (int i = 0; i < n1; ++i)
+            for (int j = 0; j < n2; ++j) {
+                const float x = s[(long)i * ld + j];
+                if (x != x || x == INFINITY) return -2;     // cost NaN or -inf (scipy raises)
+            }
+        std::vector<float> st;
+        const float* rows = s;
+        long lds = ld;
+        if (tr) {
+            st.resize((size_t)nr * nc);
+            for (int i = 0; i < n1; ++i)
+                for (int j = 0; j < n2; ++j) st[(size_t)j * nc + i] = s[(long)i * ld + j];
+            rows = st.data();
+            lds = nc;
+        }
+        std::vector<int> c4r;
+        const int rc = lsap_solve_f512(nr, nc, rows, lds, c4r);
+        if (rc) return rc;
+        if (!tr) {
+            for (int i = 0; i < nr; ++i) assign[i] = c4r[i];
+        } else {
+            for (int j = 0; j < nr; ++j) assign[c4r[j]] = j;
+        }
+        return 0;
+    }
+#endif
     std::vector<double> cost((size_t)nr * nc);
     for (int i = 0; i < n1; ++i)
         for (int j = 0; j < n2; ++j) {

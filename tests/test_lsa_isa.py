@@ -1,0 +1,71 @@
+"""Every host-LSAP code path (scalar, AVX2, AVX-512 dense scan, AVX-512 float rows with one-pass
+ties) returns scipy's assignment (utils/hungarian.py:8-66 -> scipy.optimize.linear_sum_assignment
+on -s).  The path is chosen once per process from the environment, so each runs in a subprocess."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+SCRIPT = r"""
+import sys
+import numpy as np
+import scipy.optimize as opt
+import torch
+sys.path.insert(0, %r)
+from fpm import ops
+
+def ref(s, n1, n2):
+    r, c = opt.linear_sum_assignment(s[:n1, :n2] * -1)
+    a = -np.ones(s.shape[0], np.int32)
+    a[r] = c
+    return a
+
+rng = np.random.default_rng(7)
+cases = []
+for mode in ("rand", "ties", "zeros", "sparse", "peaked"):
+    B, n1max, n2max = 12, 45, 41
+    s = np.zeros((B, n1max, n2max), np.float32)
+    n1 = rng.integers(1, n1max + 1, B).astype(np.int32)
+    n2 = rng.integers(1, n2max + 1, B).astype(np.int32)
+    for b in range(B):
+        shp = (n1[b], n2[b])
+        if mode == "rand":
+            blk = rng.random(shp)
+        elif mode == "ties":
+            blk = rng.integers(0, 3, shp)
+        elif mode == "zeros":
+            blk = np.zeros(shp)
+        elif mode == "sparse":
+            blk = rng.random(shp) ** 8
+            blk[blk < 0.3] = 0
+        else:   # ds_mat-like: a few large entries per row over a tiny floor
+            blk = rng.random(shp) * 1e-3
+            k = min(shp)
+            blk[rng.permutation(shp[0])[:k], rng.permutation(shp[1])[:k]] += rng.random(k)
+        s[b, :n1[b], :n2[b]] = blk
+    cases.append((s, n1, n2))
+s = rng.random((3, 130, 130)).astype(np.float32) ** 4   # more than one 16-column block, ragged tail
+cases.append((s, np.array([130, 129, 97], np.int32), np.array([130, 121, 130], np.int32)))
+bad = 0
+for s, n1, n2 in cases:
+    out = ops.lsa_batch_host(torch.from_numpy(s), torch.from_numpy(n1), torch.from_numpy(n2), nthreads=3)
+    for b in range(s.shape[0]):
+        bad += int(not np.array_equal(out[b].numpy(), ref(s[b], n1[b], n2[b])))
+print("mismatches", bad)
+sys.exit(1 if bad else 0)
+""" % REPO
+
+
+@pytest.mark.parametrize("isa", ["default", "FPM_LSA_DENSE512", "FPM_LSA_AVX2", "FPM_LSA_SCALAR"])
+def test_lsa_paths_match_scipy(isa, tmp_path):
+    env = dict(os.environ)
+    for k in ("FPM_LSA_DENSE512", "FPM_LSA_AVX2", "FPM_LSA_SCALAR"):
+        env.pop(k, None)
+    if isa != "default":
+        env[isa] = "1"
+    r = subprocess.run([sys.executable, "-c", SCRIPT], env=env, cwd=str(tmp_path), capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr

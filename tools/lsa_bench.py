@@ -1,4 +1,4 @@
-"""Host-LSA micro-benchmark on ds_mat-like inputs (soft top-k output of the oracle at n=256).
+"""Host-LSA micro-benchmark on ds_mat-like inputs (soft top-k output of the oracle, n = $N, 256).
 
     python tools/lsa_bench.py [label]        (FPM_LSA_SCALAR=1 selects the scalar solver)
 """
@@ -14,9 +14,15 @@ from fpm import ops, params, synth  # noqa: E402
 import oracle as O  # noqa: E402
 
 torch.set_num_threads(16)
-ds = O.forward(synth.make_batch(0, 4, 256), params.init_params(0))["ds_mat"].numpy()
+N = int(os.environ.get("N", 256))
+cache = "/tmp/lsa_bench_ds_%d.npy" % N
+if os.path.exists(cache):
+    ds = np.load(cache)
+else:
+    ds = O.forward(synth.make_batch(0, 4, N), params.init_params(0))["ds_mat"].numpy()
+    np.save(cache, ds)
 big = torch.from_numpy(np.tile(ds, (256, 1, 1)).copy())
-n = torch.full((1024,), 256, dtype=torch.int32)
+n = torch.full((1024,), N, dtype=torch.int32)
 label = sys.argv[1] if len(sys.argv) > 1 else "default"
 for th in (1, 16):
     m = 64 if th == 1 else 1024
