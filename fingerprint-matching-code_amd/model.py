@@ -30,6 +30,18 @@ from . import params as P
 from .batch import DeviceBatch
 
 
+def host_cpu_share():
+    """CPUs this process may use for the host Hungarian pool: OMP_NUM_THREADS (16 per GPU on the
+    pool) capped by the affinity mask.  torch.distributed.run exports OMP_NUM_THREADS=1 when the
+    variable was unset; under it (LOCAL_WORLD_SIZE present) a share of 1 is read as that default
+    and replaced by the affinity mask split over the node's ranks (at most 16 each)."""
+    n_aff = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+    if omp <= 1 and "LOCAL_WORLD_SIZE" in os.environ:
+        omp = min(16, n_aff // max(1, int(os.environ["LOCAL_WORLD_SIZE"])))
+    return max(1, min(omp, n_aff))
+
+
 class _Node(nn.Module):
     pass
 
@@ -77,7 +89,7 @@ class Net(nn.Module):
         # Hungarian pool: 2 threads per CPU of the process's share (FPM_LSA_THREADS overrides).  Measured
         # on the 16-CPU box share: 16 / 32 / 48 threads -> 29-44 / 17-22 / 17-18 ms per 1024 pairs
         # (the pairs of a chunk differ in cost; idle stragglers at each chunk's join dominate at 1x)
-        share = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16")), len(os.sched_getaffinity(0))))
+        share = host_cpu_share()
         self.lsa_threads = lsa_threads or int(os.environ.get("FPM_LSA_THREADS", str(2 * share)))
         self.chunks = chunks
         # quadratic (edge) affinity Ke (ngm.py:282-289): dead for every output, off by default

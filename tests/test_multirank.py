@@ -73,3 +73,17 @@ def test_two_rank_sharding(tmp_path):
         n = torch.full((total,), 12, dtype=torch.int32)
         ref = ops.lsa_batch_host(_mats(total, 12), n, n, 1).numpy()
         np.testing.assert_array_equal(got, ref)
+
+
+def test_host_cpu_share_under_torchrun(monkeypatch):
+    """torch.distributed.run's OMP_NUM_THREADS=1 default must not shrink the Hungarian pool to
+    2 threads per rank: the affinity mask is split over the node's ranks instead."""
+    from fpm.model import host_cpu_share
+    n_aff = len(os.sched_getaffinity(0))
+    monkeypatch.setenv("OMP_NUM_THREADS", "16")
+    monkeypatch.delenv("LOCAL_WORLD_SIZE", raising=False)
+    assert host_cpu_share() == min(16, n_aff)
+    monkeypatch.setenv("OMP_NUM_THREADS", "1")
+    assert host_cpu_share() == 1                      # an explicit single-thread request outside torchrun
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "2")
+    assert host_cpu_share() == max(1, min(16, n_aff // 2))
