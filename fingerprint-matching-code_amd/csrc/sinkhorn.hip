@@ -283,6 +283,8 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
     __shared__ float potA[SK_MAXN], potC[SK_MAXN];
     __shared__ float red_m[1024], red_s[1024];
     __shared__ float ud_sh;
+    __shared__ float newC[SK_MAXN];
+    __shared__ int redo_sh;
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int n1b = a.n1[b], n2b = a.n2[b];
     const bool transposed = n1b > n2b;
@@ -299,13 +301,38 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
     auto val = [&](int ia, int ic) { return in[ia * sA + ic * sC] * vscale; };
     (void)scale;
     for (int k = tid; k < SK_MAXN; k += 1024) { potA[k] = 0.f; potC[k] = 0.f; }
-    if (tid == 0) ud_sh = 0.f;
+    if (tid == 0) { ud_sh = 0.f; redo_sh = 0; }
     __syncthreads();
 
+    // Shifted single-pass lse (fast, every step after the first; as in sinkhorn_reg_kernel): after
+    // a normalisation along one axis every entry is <= 0, so the other axis' lse is shifted by the
+    // line's previous potential -- one exp and one add per element, a plain sum reduction.  A sum
+    // outside [2^-30, 2^30] falls back to the online max-rescaled form (per row on the c side; the
+    // whole step on the a side, like the register kernel).
+    auto ok_s = [](float x) { return x >= 0x1p-30f && x <= 0x1p30f; };
     // potA[ia] = lse_c(val - potC[c]) (+ nd * exp(DUMMY - ud)): one wave per ia, lanes along c
-    auto along_c = [&](bool add_dummy) {
+    auto along_c = [&](bool add_dummy, bool fast) {
         const float ud = ud_sh;
         for (int ia = wv; ia < limA; ia += 16) {
+            if (fast) {
+                const float sh = potA[ia];
+                float s0 = 0.f, s1 = 0.f;
+                int ic = lane;
+#pragma unroll 4
+                for (; ic + 64 < limC; ic += 128) {
+                    s0 += fpm::fast_exp2(val(ia, ic) - potC[ic] - sh);
+                    s1 += fpm::fast_exp2(val(ia, ic + 64) - potC[ic + 64] - sh);
+                }
+                if (ic < limC) s0 += fpm::fast_exp2(val(ia, ic) - potC[ic] - sh);
+                float s = s0 + s1;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+                if (add_dummy) s += (float)nd * fpm::fast_exp2(DUMMY - ud - sh);
+                if (ok_s(s)) {                        // wave-uniform (s is reduced over the wave)
+                    if (lane == 0) potA[ia] = sh + fpm::fast_log2(s);
+                    continue;
+                }
+            }
             float m = -INFINITY, s = 0.f;
 #pragma unroll 8
             for (int ic = lane; ic < limC; ic += 64) lse_push(m, s, val(ia, ic) - potC[ic]);
@@ -320,10 +347,44 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
         __syncthreads();
     };
     // potC[ic] = lse_a(val - potA[a]) (+ dummy): thread groups along a, threads along c (coalesced)
-    auto along_a = [&](bool add_dummy) {
+    auto along_a = [&](bool add_dummy, bool fast) {
         const float ud = ud_sh;
         const int cpad = (limC + 63) / 64 * 64;
         const int groups = cpad >= 1024 ? 1 : 1024 / cpad;
+        if (fast) {
+            for (int c0 = 0; c0 < limC; c0 += 1024) {
+                const int ic = c0 + (groups == 1 ? tid : tid % cpad), grp = groups == 1 ? 0 : tid / cpad;
+                const float sh = ic < limC ? potC[ic] : 0.f;
+                float s0 = 0.f, s1 = 0.f;
+                if (ic < limC && grp < groups) {
+                    int ia = grp;
+#pragma unroll 4
+                    for (; ia + groups < limA; ia += 2 * groups) {
+                        s0 += fpm::fast_exp2(val(ia, ic) - potA[ia] - sh);
+                        s1 += fpm::fast_exp2(val(ia + groups, ic) - potA[ia + groups] - sh);
+                    }
+                    if (ia < limA) s0 += fpm::fast_exp2(val(ia, ic) - potA[ia] - sh);
+                }
+                float s = s0 + s1;
+                red_s[tid] = s;
+                __syncthreads();
+                if (grp == 0 && ic < limC) {
+                    for (int g = 1; g < groups; ++g) s += red_s[tid + g * cpad];
+                    if (add_dummy) s += (float)nd * fpm::fast_exp2(DUMMY - ud - sh);
+                    if (ok_s(s)) newC[ic] = sh + fpm::fast_log2(s);
+                    else redo_sh = 1;
+                }
+                __syncthreads();
+            }
+            const bool redo = redo_sh != 0;
+            __syncthreads();                                  // every thread has read the flag
+            if (!redo) {
+                for (int k = tid; k < limC; k += 1024) potC[k] = newC[k];
+                __syncthreads();
+                return;
+            }
+            if (tid == 0) redo_sh = 0;                        // read again only after the barriers below
+        }
         for (int c0 = 0; c0 < limC; c0 += 1024) {
             const int ic = c0 + (groups == 1 ? tid : tid % cpad), grp = groups == 1 ? 0 : tid / cpad;
             float m = -INFINITY, s = 0.f;
@@ -359,11 +420,12 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
     };
 
     for (int it = 0; it < a.iters; ++it) {
+        const bool fast = it > 0 && a.fast;
         if ((it & 1) == 0) {           // row normalisation: update u
-            if (u_on_A) along_c(false); else along_a(false);
+            if (u_on_A) along_c(false, fast); else along_a(false, fast);
             if (nd > 0) update_dummy();
         } else {                       // column normalisation: update v
-            if (u_on_A) along_a(nd > 0); else along_c(nd > 0);
+            if (u_on_A) along_a(nd > 0, fast); else along_c(nd > 0, fast);
         }
     }
 

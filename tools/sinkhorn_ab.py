@@ -11,7 +11,8 @@ import oracle as O  # noqa: E402
 
 dev = torch.device("cuda", 0)
 g = torch.Generator().manual_seed(0)
-cases = ((128, 256, 20, False), (64, 256, 10, True), (128, 128, 20, False), (128, 512, 20, False))
+cases = ((128, 256, 20, False), (64, 256, 10, True), (128, 128, 20, False), (128, 512, 20, False),
+         (64, 512, 10, True))
 for B, n, iters, ragged in cases[int(os.environ.get("FIRST", 0)):]:
     s = torch.randn(B, n, n, generator=g) * 0.3
     n1 = torch.full((B,), n, dtype=torch.int32)
