@@ -280,7 +280,8 @@ __device__ __forceinline__ void lse_push(float& m, float& s, float x) {
 }
 
 __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
-    __shared__ float potA[SK_MAXN], potC[SK_MAXN];
+    __shared__ __attribute__((aligned(16))) float potA[SK_MAXN], potC[SK_MAXN];
+    __shared__ float4 red4[1024];
     __shared__ float red_m[1024], red_s[1024];
     __shared__ float ud_sh;
     __shared__ float newC[SK_MAXN];
@@ -299,6 +300,14 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
     const long sA = a.contig_j ? a.in_si : a.in_sj, sC = a.contig_j ? a.in_sj : a.in_si;
     const float vscale = fpm::LOG2E_F / a.tau;   // one multiply per element read (not a division)
     auto val = [&](int ia, int ic) { return in[ia * sA + ic * sC] * vscale; };
+    // 16-B loads along c for the fast steps: unit-stride c, 16-B aligned rows, whole quads
+    // (a.fast == 2 keeps the scalar loads: A/B switch)
+    const bool vec = sC == 1 && (sA & 3) == 0 && ((unsigned long)in & 15) == 0 && (limC & 3) == 0 &&
+                     a.fast == 1;
+    auto e4 = [&](float4 v, float4 p, float sh) {       // sum of exp2(v * vscale - p - sh) over 4
+        return fpm::fast_exp2(v.x * vscale - p.x - sh) + fpm::fast_exp2(v.y * vscale - p.y - sh) +
+               fpm::fast_exp2(v.z * vscale - p.z - sh) + fpm::fast_exp2(v.w * vscale - p.w - sh);
+    };
     (void)scale;
     for (int k = tid; k < SK_MAXN; k += 1024) { potA[k] = 0.f; potC[k] = 0.f; }
     if (tid == 0) { ud_sh = 0.f; redo_sh = 0; }
@@ -314,7 +323,26 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
     auto along_c = [&](bool add_dummy, bool fast) {
         const float ud = ud_sh;
         for (int ia = wv; ia < limA; ia += 16) {
-            if (fast) {
+            if (fast && vec) {
+                const float sh = potA[ia];
+                const float* row = in + (long)ia * sA;
+                float s0 = 0.f, s1 = 0.f;
+                int ic = 4 * lane;
+#pragma unroll 2
+                for (; ic + 256 < limC; ic += 512) {
+                    s0 += e4(*(const float4*)(row + ic), *(const float4*)&potC[ic], sh);
+                    s1 += e4(*(const float4*)(row + ic + 256), *(const float4*)&potC[ic + 256], sh);
+                }
+                if (ic < limC) s0 += e4(*(const float4*)(row + ic), *(const float4*)&potC[ic], sh);
+                float s = s0 + s1;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+                if (add_dummy) s += (float)nd * fpm::fast_exp2(DUMMY - ud - sh);
+                if (ok_s(s)) {
+                    if (lane == 0) potA[ia] = sh + fpm::fast_log2(s);
+                    continue;
+                }
+            } else if (fast) {
                 const float sh = potA[ia];
                 float s0 = 0.f, s1 = 0.f;
                 int ic = lane;
@@ -351,7 +379,45 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
         const float ud = ud_sh;
         const int cpad = (limC + 63) / 64 * 64;
         const int groups = cpad >= 1024 ? 1 : 1024 / cpad;
-        if (fast) {
+        if (fast && vec) {
+            // thread = (column quad q, row group grp); float4 partial sums, combined over groups
+            const int nq = limC >> 2, qpad = (nq + 63) / 64 * 64;
+            const int groups4 = qpad >= 1024 ? 1 : 1024 / qpad;
+            for (int q0 = 0; q0 < nq; q0 += 1024) {
+                const int q = q0 + (groups4 == 1 ? tid : tid % qpad), grp = groups4 == 1 ? 0 : tid / qpad;
+                const int ic = 4 * q;
+                float4 sh = make_float4(0.f, 0.f, 0.f, 0.f), acc = sh;
+                if (q < nq) sh = *(const float4*)&potC[ic];
+                if (q < nq && grp < groups4) {
+#pragma unroll 4
+                    for (int ia = grp; ia < limA; ia += groups4) {
+                        const float4 v = *(const float4*)(in + (long)ia * sA + ic);
+                        const float pa = potA[ia];
+                        acc.x += fpm::fast_exp2(v.x * vscale - pa - sh.x);
+                        acc.y += fpm::fast_exp2(v.y * vscale - pa - sh.y);
+                        acc.z += fpm::fast_exp2(v.z * vscale - pa - sh.z);
+                        acc.w += fpm::fast_exp2(v.w * vscale - pa - sh.w);
+                    }
+                }
+                red4[tid] = acc;
+                __syncthreads();
+                if (grp == 0 && q < nq) {
+                    for (int g = 1; g < groups4; ++g) {
+                        const float4 o = red4[tid + g * qpad];
+                        acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
+                    }
+                    const float sv[4] = {acc.x, acc.y, acc.z, acc.w}, hv[4] = {sh.x, sh.y, sh.z, sh.w};
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        float sk = sv[k];
+                        if (add_dummy) sk += (float)nd * fpm::fast_exp2(DUMMY - ud - hv[k]);
+                        if (ok_s(sk)) newC[ic + k] = hv[k] + fpm::fast_log2(sk);
+                        else redo_sh = 1;
+                    }
+                }
+                __syncthreads();
+            }
+        } else if (fast) {
             for (int c0 = 0; c0 < limC; c0 += 1024) {
                 const int ic = c0 + (groups == 1 ? tid : tid % cpad), grp = groups == 1 ? 0 : tid / cpad;
                 const float sh = ic < limC ? potC[ic] : 0.f;
@@ -376,6 +442,8 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
                 }
                 __syncthreads();
             }
+        }
+        if (fast) {
             const bool redo = redo_sh != 0;
             __syncthreads();                                  // every thread has read the flag
             if (!redo) {

@@ -22,7 +22,7 @@ for B, n, iters, ragged in cases[int(os.environ.get("FIRST", 0)):]:
         n2[1::3] = n - 50
     sd, n1d, n2d = s.to(dev), n1.to(dev), n2.to(dev)
     outs = {}
-    for fast in (0, 1):
+    for fast in (0, 1, 2):
         prev = ops.set_tuning("sinkhorn_fast", fast)
         out = ops.sinkhorn(sd, n1d, n2d, iters, 0.01, True)
         torch.cuda.synchronize()
@@ -36,6 +36,7 @@ for B, n, iters, ragged in cases[int(os.environ.get("FIRST", 0)):]:
         ops.set_tuning("sinkhorn_fast", prev)
         print("B=%d n=%d iters=%d ragged=%s fast=%d %.4f ms" % (B, n, iters, ragged, fast, e0.elapsed_time(e1) / 10))
     ref = O.pygm_sinkhorn(s[:4].double(), n1[:4].tolist(), n2[:4].tolist(), dummy_row=True, max_iter=iters, tau=0.01)
-    print("   max|fast-slow| %.3g   vs f64: slow %.3g fast %.3g" % (
-        float((outs[1] - outs[0]).abs().max()), float((outs[0][:4].double() - ref).abs().max()),
-        float((outs[1][:4].double() - ref).abs().max())))
+    print("   max|fast-slow| %.3g  max|fast2-fast| %.3g   vs f64: slow %.3g fast %.3g fast2 %.3g" % (
+        float((outs[1] - outs[0]).abs().max()), float((outs[2] - outs[1]).abs().max()),
+        float((outs[0][:4].double() - ref).abs().max()), float((outs[1][:4].double() - ref).abs().max()),
+        float((outs[2][:4].double() - ref).abs().max())))
