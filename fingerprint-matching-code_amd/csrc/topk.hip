@@ -82,19 +82,38 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
     const float dscale = fpm::LOG2E_F / tau;   // distances / tau, in log2 units
     // visit every q of this thread: register-resident values (unrolled), then LDS-resident ones
     // (runtime loop: bounded code size and register pressure)
+    // f(q, value) with q the flat index i * n2b + j of the valid block.  STREAM: a dense block
+    // (ld == n2b, 16-B aligned, N % 4 == 0) is read as float4 quads q = 4 (tid + 1024 t) + 0..3;
+    // otherwise (i, j) advance by 1024 entries per step without a division.
+    const bool dense4 = STREAM && ld == n2b && (N & 3) == 0 && ((unsigned long)S & 15) == 0;
     auto forq = [&](auto&& f) {
         if (STREAM) {
-            for (int k = 0; tid + 1024 * k < N; ++k) {
-                const int q = tid + 1024 * k, i = q / n2b, j = q - i * n2b;
-                f(k, S[i * ld + j]);
+            if (dense4) {
+                const float4* S4 = (const float4*)S;
+                for (int t = tid; 4 * t < N; t += 1024) {
+                    const float4 v = S4[t];
+                    f(4 * t, v.x);
+                    f(4 * t + 1, v.y);
+                    f(4 * t + 2, v.z);
+                    f(4 * t + 3, v.w);
+                }
+                return;
+            }
+            const int di = 1024 / n2b, dj = 1024 - di * n2b;
+            int i = tid / n2b, j = tid - i * n2b;
+            for (int q = tid; q < N; q += 1024) {
+                f(q, S[i * ld + j]);
+                i += di;
+                j += dj;
+                if (j >= n2b) { j -= n2b; ++i; }
             }
             return;
         }
 #pragma unroll
         for (int k = 0; k < NQR; ++k)
-            if (tid + 1024 * k < N) f(k, sr[k]);
+            if (tid + 1024 * k < N) f(tid + 1024 * k, sr[k]);
         for (int k = NQR; k < NQ; ++k)
-            if (tid + 1024 * k < N) f(k, sl[(k - NQR) * 1024 + tid]);
+            if (tid + 1024 * k < N) f(tid + 1024 * k, sl[(k - NQR) * 1024 + tid]);
     };
     const float kk = kvec[b];
     const float lcp0 = fpm::fast_log2((float)N - kk);   // log(col_prob[:,0]) = log(n1*n2 - k)
@@ -238,8 +257,7 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
     }
     int n2o = n2b;
     asm volatile("" : "+v"(n2o));   // recompute (i, j) here rather than keep NQ addresses live
-    forq([&](int k, float sv) {
-        int q = tid + 1024 * k;
+    forq([&](int q, float sv) {
         int i = q / n2o, j = q - i * n2o;
         float L0, L1;
         Lpair(sv, mnl, mxl, L0, L1);

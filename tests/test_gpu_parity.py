@@ -75,6 +75,22 @@ def test_soft_topk_vs_oracle_large():
     assert (out - ref).abs().max() < 1e-4
 
 
+def test_soft_topk_stream_vs_oracle():
+    """n = 512 (the streaming soft top-k): a dense pair (float4 reads) and ragged pairs (row-strided
+    reads) against the oracle."""
+    g = torch.Generator().manual_seed(9)
+    B, n = 3, 512
+    n1s, n2s = [512, 480, 512], [512, 512, 437]
+    ss = torch.rand(B, n, n, generator=g) ** 6
+    for b in range(B):
+        ss[b, n1s[b]:, :] = 0
+        ss[b, :, n2s[b]:] = 0
+    k = torch.tensor([120.5, 40.0, 300.0])
+    ref = O.soft_topk(ss, k, n1s, n2s, 10, 0.01)
+    out = ops.soft_topk(ss.to(DEV), _i32(n1s), _i32(n2s), k.to(DEV), 10, 0.01).cpu()
+    assert (out - ref).abs().max() < 1e-4
+
+
 def test_soft_topk_host_mapped_output():
     """The kernel's optional second output (pinned host memory, written over PCIe) equals the
     device output bit for bit, zero padding included."""

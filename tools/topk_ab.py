@@ -10,7 +10,7 @@ from fpm import ops  # noqa: E402
 
 dev = torch.device("cuda", 0)
 g = torch.Generator().manual_seed(0)
-B, n = 128, 256
+B, n = int(os.environ.get("B", 128)), int(os.environ.get("N", 256))
 s = torch.randn(B, n, n, generator=g) * 0.3
 nn_ = torch.full((B,), n, dtype=torch.int32, device=dev)
 ss = ops.sinkhorn(s.to(dev), nn_, nn_, 10, 0.01, True)
