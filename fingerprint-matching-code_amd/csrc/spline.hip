@@ -77,8 +77,9 @@ PlanLayout plan_layout(long E, long num_nodes) {
 __global__ __launch_bounds__(256) void plan_edge_kernel(const int* __restrict__ src, const int* __restrict__ dst,
                                                         const float* __restrict__ pseudo, long E, int* mask,
                                                         int* indeg, int* dslot, float* basis_e, int* grp_e) {
-    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= E) return;
+    const long e0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = e0 < E;
+    const long e = live ? e0 : E - 1;
     int f[2];
     float fr[2];
 #pragma unroll
@@ -99,9 +100,20 @@ __global__ __launch_bounds__(256) void plan_edge_kernel(const int* __restrict__ 
         b4[s] = b;
         bits |= 1 << fpm::spline_cell(g, s);
     }
+    // the source's cell mask: OR the bits of the lanes that share the source (edge lists are
+    // grouped by source, so runs are contiguous) into the run's first lane, one atomic per run
+    const int key = live ? src[e] : -1;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int kb = __shfl_down(key, o), bb = __shfl_down(bits, o);
+        if (lane + o < 64 && kb == key) bits |= bb;
+    }
+    const int kprev = __shfl_up(key, 1);
+    if (!live) return;
     grp_e[e] = g;
     *(float4*)(basis_e + 4 * e) = make_float4(b4[0], b4[1], b4[2], b4[3]);
-    atomicOr(&mask[src[e]], bits);
+    if (lane == 0 || kprev != key) atomicOr(&mask[key], bits);
     dslot[e] = atomicAdd(&indeg[dst[e]], 1);
 }
 
