@@ -284,11 +284,19 @@ __global__ __launch_bounds__(256) void topk_select_kernel(const float* __restric
     const float* D = ds + (long)b * sb;
     const int* A = assign + (long)b * asb;
     float* P = perm + (long)b * pb;
-    for (int idx = tid; idx < n1max * n2max; idx += 256) {
-        int i = idx / n2max, j = idx - i * n2max;
-        P[i * pld + j] = 0.f;
-        if (lsa_out) lsa_out[(long)b * lb + i * lld + j] = 0.f;
-    }
+    // zero both outputs: 16-B stores over dense blocks, row-wise (no division) otherwise
+    auto zero_block = [&](float* Z, long zld) {
+        if (zld == n2max && (n2max & 3) == 0 && ((unsigned long)Z & 15) == 0) {
+            float4* Z4 = (float4*)Z;
+            const long n4 = (long)n1max * n2max / 4;
+            for (long t = tid; t < n4; t += 256) Z4[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+        } else {
+            for (int i = 0; i < n1max; ++i)
+                for (int j = tid; j < n2max; j += 256) Z[i * zld + j] = 0.f;
+        }
+    };
+    zero_block(P, pld);
+    if (lsa_out) zero_block(lsa_out + (long)b * lb, lld);
     for (int r = tid; r < 1024; r += 256) { rowt[r] = 0; colt[r] = 0; }
     int n = 1;
     while (n < n1max) n <<= 1;

@@ -75,7 +75,7 @@ def test_soft_topk_vs_oracle_large():
     assert (out - ref).abs().max() < 1e-4
 
 
-def test_soft_topk_stream_vs_oracle():
+def test_soft_topk_stream_dense_and_ragged_vs_oracle():
     """n = 512 (the streaming soft top-k): a dense pair (float4 reads) and ragged pairs (row-strided
     reads) against the oracle."""
     g = torch.Generator().manual_seed(9)
