@@ -286,7 +286,11 @@ int fpm_kron_gnn_layer_bwd_point(const float* X, int C, int B, int n1max, int n2
 
 /* ---- host: batched linear sum assignment ------------------------------------------------------
  * Replaces utils/hungarian.py:8-66 (scipy linear_sum_assignment on -s, per pair).  Synchronous,
- * HOST memory, nthreads worker threads.  assign[b][r] = column or -1.  Returns 0 or (pair + 1). */
+ * HOST memory, nthreads worker threads.  assign[b][r] = column or -1.  Returns 0 or (pair + 1).
+ * Solver path chosen once per process from the CPU: AVX-512 F/DQ/VL/BW -> float cost rows read
+ * in place with the tie rule resolved in the scan pass (default); FPM_LSA_DENSE512=1 / FPM_LSA_AVX2=1
+ * / FPM_LSA_SCALAR=1 force the older dense-scan or scalar solvers.  All paths return scipy's
+ * assignment bit for bit (tests/test_lsa_isa.py). */
 int fpm_lsa_batch_host(const float* s, long sb, long ld, const int* n1, const int* n2, int B, int n1max, int* assign,
                        int nthreads);
 
