@@ -88,10 +88,33 @@ def cpu_baseline(n, npairs, seed, sd):
     pairs = make_pairs(seed + 7919, 0, npairs, n, 1)
     O.forward(pairs[:1], sd)                   # warm-up
     t = time.perf_counter()
-    O.forward(pairs, sd)
+    ref = O.forward(pairs, sd)
     dt = time.perf_counter() - t
     return {"value": npairs / dt, "unit": "pairs/s", "cores": cores, "kind": "port",
-            "sample": "%d pairs, n=%d, fp32 oracle forward incl. scipy Hungarian (1 process)" % (npairs, n)}
+            "sample": "%d pairs, n=%d, fp32 oracle forward incl. scipy Hungarian (1 process)" % (npairs, n)}, pairs, ref
+
+
+def parity_vs_oracle(pairs, ref, sd, dev, dtypes):
+    """The GPU forward (each compute mode) on the CPU baseline's own sample, against the oracle's
+    outputs for it: max|d| per output and perm_mat agreement (SURVEY §8(d) parity gate: fp32 gated
+    at 1e-4, bf16 reported).  Checker only: runs after the timed region."""
+    import torch
+    import fpm
+    from fpm.batch import DeviceBatch
+    out = {}
+    for dt in dtypes:
+        net = fpm.Net(regression=True, backbone=False, dtype=dt)
+        net.load_state_dict(sd)
+        res = net.run(DeviceBatch.from_pairs(pairs, dev))
+        torch.cuda.synchronize()
+        d = {k: float((res[k].float().cpu() - ref[k]).abs().max()) for k in ("ss", "ds_mat", "k_prob", "cls_prob")}
+        P, R = res["perm_mat"].cpu(), ref["perm_mat"]
+        d["perm_entries_agree"] = float((P == R).float().mean())
+        d["perm_matches_kept"] = float((P * R).sum() / R.sum().clamp(min=1))
+        d["perm_pairs_identical"] = float(np.mean([torch.equal(P[b], R[b]) for b in range(P.shape[0])]))
+        out[dt] = d
+    out["pairs"] = len(pairs)
+    return out
 
 
 def bench_graph_build(kp, bt, dev, args):
@@ -148,7 +171,10 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-pairs", type=int, default=32)
+    ap.add_argument("--parity-pairs", type=int, default=8, help="pairs of the CPU sample re-run on the GPU "
+                    "modes for the parity_vs_oracle report")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-f32-line", action="store_true", help="skip the fp32-mode C3 line")
     ap.add_argument("--lsa-threads", type=int, default=0)
     ap.add_argument("--gen-workers", type=int, default=16)
     ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4", "c5"],
@@ -167,8 +193,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print("note: WORLD_SIZE=%d, --gpus=%d" % (world, args.gpus), file=sys.stderr)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: start one rank per GPU as children (nothing has touched the GPU yet) and
+        # exit with their status, so --gpus N never silently measures one GPU
+        import subprocess
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+               "--master-addr", "127.0.0.1", "--master-port", str(29500 + os.getpid() % 1000),
+               os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
+    if world != args.gpus:
+        raise SystemExit("bench: WORLD_SIZE=%d but --gpus=%d" % (world, args.gpus))
 
     # inputs first (forked workers must not inherit a GPU context)
     t_gen = time.perf_counter()
@@ -196,7 +230,7 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     sd = params.init_params(args.seed)
-    net = fpm.Net(regression=True, dtype=args.dtype, lsa_threads=args.lsa_threads or None)
+    net = fpm.Net(regression=True, backbone=False, dtype=args.dtype, lsa_threads=args.lsa_threads or None)
     net.load_state_dict(sd)
     if args.config == "c4":
         bt = DeviceBatch.from_probe_gallery(probe, gallery, dev)
@@ -218,28 +252,37 @@ def main():
     torch.cuda.synchronize()
     lib = _lib.load()
     import ctypes
-    lib.fpm_profile_read(None, None, None)     # drop warm-up records
+
+    def timed(model, batch, steps, tag):
+        """``steps`` forwards bracketed by barrier + synchronize -> (wall s, gpu-stage s, lsa s)."""
+        g_s = l_s = 0.0
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            model.run(batch)
+            lt = model.last_timing
+            g_s += lt["gpu_stage_s"]
+            l_s += lt["lsa_s"]
+            log("%s step: gpu-stage %.3fs lsa %.3fs enqueue %.3fs first-chunk %.3fs total %.3fs" % (
+                tag, lt["gpu_stage_s"], lt["lsa_s"], lt["enqueue_s"], lt["first_chunk_wait_s"], lt["total_s"]))
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        barrier()
+        return t1 - t0, g_s, l_s
+
+    # the headline: K steps with the library's profiling off
+    elapsed, gpu_s, lsa_s = timed(net, bt, args.steps, "")
+    # the roofline: the same K steps again, every product-GEMM launch bracketed by HIP events on its
+    # own stream (fpm_profile_*); its wall rate is reported beside the headline
+    lib.fpm_profile_read(None, None, None)     # drop earlier records
     lib.fpm_profile_enable(1)
-    gpu_s = lsa_s = 0.0
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        net.run(bt)
-        gpu_s += net.last_timing["gpu_stage_s"]
-        lsa_s += net.last_timing["lsa_s"]
-        lt = net.last_timing
-        log("step: gpu-stage %.3fs lsa %.3fs enqueue %.3fs first-chunk %.3fs total %.3fs" % (
-            lt["gpu_stage_s"], lt["lsa_s"], lt["enqueue_s"], lt["first_chunk_wait_s"], lt["total_s"]))
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    barrier()
+    elapsed_prof, _, _ = timed(net, bt, args.steps, "profiled")
     lib.fpm_profile_enable(0)
     ms = ctypes.c_double()
     fl = ctypes.c_double()
     cnt = ctypes.c_int()
     _lib.call("fpm_profile_read", ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(cnt))
-    elapsed = t1 - t0
     # the same kernel without the second stream's kernels sharing the CUs (one extra, untimed
     # forward on one stream): its isolated rate, reported beside the in-pipeline one
     iso_ms = ctypes.c_double()
@@ -253,11 +296,37 @@ def main():
     lib.fpm_profile_enable(0)
     net.n_streams = saved_streams
     _lib.call("fpm_profile_read", ctypes.byref(iso_ms), ctypes.byref(iso_fl), ctypes.byref(iso_cnt))
-    elapsed, gpu_s, lsa_s = reduce_max([elapsed, gpu_s, lsa_s], world)
+    elapsed, gpu_s, lsa_s, elapsed_prof = reduce_max([elapsed, gpu_s, lsa_s, elapsed_prof], world)
     pairs_total = (args.gallery if args.config == "c4" else args.batch * world) * args.steps
     value = pairs_total / elapsed
     peak = 2500.0 if args.dtype == "bf16" else 157.3
     achieved = (fl.value / (ms.value / 1e3)) / 1e12 if ms.value > 0 else 0.0
+
+    # the fp32 (parity) mode on the same C3 batch beside the bf16 headline
+    f32_line = None
+    if args.dtype == "bf16" and args.config == "c3" and not args.no_f32_line:
+        net32 = fpm.Net(regression=True, backbone=False, dtype="f32", lsa_threads=args.lsa_threads or None)
+        net32.load_state_dict(sd)
+        net32.run(bt)
+        k32 = max(1, min(args.steps, 3))
+        e32, g32, _ = timed(net32, bt, k32, "f32")
+        e32, g32 = reduce_max([e32, g32], world)
+        f32_line = {"value": args.batch * world * k32 / e32, "unit": "pairs/s", "dtype": "f32", "steps": k32,
+                    "ms_per_step": e32 / k32 * 1e3, "gpu_stage_pairs_per_s": args.batch * world * k32 / g32}
+        del net32
+        torch.cuda.empty_cache()
+
+    # strong scaling: BASELINE's global batch (args.batch pairs) split over the ranks; each rank runs
+    # the first batch/world pairs of its own shard (same graph-size distribution)
+    strong = None
+    if world > 1 and args.config != "c4":
+        share = max(1, args.batch // world)
+        sub = bt.split_range(0, share)
+        net.run(sub)
+        es, gs_, _ = timed(net, sub, args.steps, "strong")
+        es, gs_ = reduce_max([es, gs_], world)
+        strong = {"global_batch": share * world, "pairs_per_gpu": share, "value": share * world * args.steps / es,
+                  "unit": "pairs/s", "ms_per_step": es / args.steps * 1e3, "scaling": "strong"}
 
     # HBM bytes per launch of the same kernel from the committed rocprofv3 PMC pass (FETCH_SIZE x2 +
     # WRITE_SIZE, separate passes; tools/pmc_gemm.sh -> profiles/r01_pmc_product_gemm.json)
@@ -273,11 +342,18 @@ def main():
         log("graph build: %s" % json.dumps(graph_build))
 
     if rank == 0:
-        cpu = None
+        cpu = parity = None
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline ...")
-            cpu = cpu_baseline(args.n, args.cpu_pairs, args.seed, sd)
+            cpu, cpu_pairs, cpu_ref = cpu_baseline(args.n, args.cpu_pairs, args.seed, sd)
             log("cpu baseline %.3f pairs/s" % cpu["value"])
+            if args.config != "c4":
+                # the GPU modes on the baseline's own sample against the oracle's outputs for it
+                parity = parity_vs_oracle(cpu_pairs[:args.parity_pairs], {k: v[:args.parity_pairs] for k, v in
+                                                                          cpu_ref.items() if torch.is_tensor(v)
+                                                                          and v.dim() >= 1 and v.shape[0] == len(cpu_pairs)},
+                                          sd, dev, ["bf16", "f32"] if args.dtype == "bf16" else [args.dtype])
+                log("parity vs oracle: %s" % json.dumps(parity))
         res = {
             "metric": "graph-match pairs/sec @ n=256 kpts, batch=1024, 1 & 8 GPU",
             "value": value,
@@ -312,7 +388,11 @@ def main():
                          "algorithmic_flops_per_launch": fl.value / max(cnt.value, 1),
                          "isolated_achieved": (iso_fl.value / (iso_ms.value / 1e3)) / 1e12 if iso_ms.value > 0 else 0.0,
                          "isolated_avg_launch_ms": iso_ms.value / max(iso_cnt.value, 1)},
+            "value_profiled": pairs_total / elapsed_prof,
             "cpu_baseline": cpu,
+            "parity_vs_oracle": parity,
+            "f32_line": f32_line,
+            "strong_scaling": strong,
             "input_gen_s": t_gen,
             "graph_build": graph_build,
         }

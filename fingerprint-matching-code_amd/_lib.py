@@ -22,6 +22,7 @@ SIGNATURES = {
     "fpm_sinkhorn_log_fwd": (I, [P, L, L, L, P, L, L, L, P, P, I, I, I, I, F, I, P]),
     "fpm_soft_topk_fwd": (I, [P, L, L, P, P, P, I, I, I, I, F, P, L, L, P, P, L, L, P]),
     "fpm_topk_select": (I, [P, L, L, P, L, P, I, I, I, P, L, L, P, L, L, P]),
+    "fpm_greedy_perm": (I, [P, L, I, P, I, I, I, P, L, L, P]),
     "fpm_gemm": (I, [I, P, L, L, P, P, L, L, I, I, I, I, I, P, P, P, L, L, P, P, P]),
     "fpm_cast_bf16": (I, [P, P, L, P]),
     "fpm_copy_async": (I, [P, P, L, I, P]),

@@ -52,27 +52,45 @@ class DeviceBatch:
             a, b = bounds[0], bounds[1]
             if b - a >= 2:
                 bounds.insert(1, (a + b) // 2)
-        parts = []
-        for c in range(len(bounds) - 1):
-            b0, b1 = bounds[c], bounds[c + 1]
-            if b1 <= b0:
-                continue
-            xs, ws, ss, ds, ps = [], [], [], [], []
-            for side in range(2):
-                nm = self.nmax[side]
-                e0, e1 = int(self.edge_off[side][b0]), int(self.edge_off[side][b1])
-                xs.append(self.x[side][b0 * nm:b1 * nm])
-                ws.append(self.w[side][b0:b1])
-                ss.append((self.src[side][e0:e1] - b0 * nm).contiguous())
-                ds.append((self.dst[side][e0:e1] - b0 * nm).contiguous())
-                ps.append(self.pseudo[side][e0:e1])
-            eo = [self.edge_off[side][b0:b1 + 1] - self.edge_off[side][b0] for side in range(2)]
-            sub = DeviceBatch(b1 - b0, self.n_host[0][b0:b1], self.n_host[1][b0:b1], xs, ws, ss, ds, ps, self.device,
-                              nmax=self.nmax, edge_off=eo, shared0=self.shared0)
-            sub.pair_range = (b0, b1)
-            parts.append(sub)
+        parts = [self.split_range(bounds[c], bounds[c + 1]) for c in range(len(bounds) - 1)
+                 if bounds[c + 1] > bounds[c]]
         self._splits[key] = parts
         return parts
+
+    def split_range(self, b0, b1):
+        """Pairs [b0, b1) as a sub-batch (views of x/w, renumbered edge copies) that keeps this
+        batch's padded sizes; ``pair_range`` records where it sits in the parent."""
+        if self.edge_off is None:
+            raise ValueError("split_range() needs per-pair edge offsets")
+        if not 0 <= b0 < b1 <= self.B:
+            raise ValueError("split_range: bad pair range [%d, %d) of %d" % (b0, b1, self.B))
+        xs, ws, ss, ds, ps = [], [], [], [], []
+        for side in range(2):
+            nm = self.nmax[side]
+            e0, e1 = int(self.edge_off[side][b0]), int(self.edge_off[side][b1])
+            xs.append(self.x[side][b0 * nm:b1 * nm])
+            ws.append(self.w[side][b0:b1])
+            ss.append((self.src[side][e0:e1] - b0 * nm).contiguous())
+            ds.append((self.dst[side][e0:e1] - b0 * nm).contiguous())
+            ps.append(self.pseudo[side][e0:e1])
+        eo = [self.edge_off[side][b0:b1 + 1] - self.edge_off[side][b0] for side in range(2)]
+        sub = DeviceBatch(b1 - b0, self.n_host[0][b0:b1], self.n_host[1][b0:b1], xs, ws, ss, ds, ps, self.device,
+                          nmax=self.nmax, edge_off=eo, shared0=self.shared0)
+        sub.pair_range = (b0, b1)
+        return sub
+
+    def to(self, device, non_blocking=True):
+        """The same batch on another device (peer copies of features, edges and counts); keeps the
+        padded sizes, so a shard computed there equals its slice of the parent batch bit for bit."""
+        device = torch.device(device)
+        if device == self.device:
+            return self
+        mv = lambda ts: [t.to(device, non_blocking=non_blocking) for t in ts]
+        out = DeviceBatch(self.B, self.n_host[0], self.n_host[1], mv(self.x), mv(self.w), mv(self.src), mv(self.dst),
+                          mv(self.pseudo), device, nmax=self.nmax, edge_off=self.edge_off, shared0=self.shared0)
+        if hasattr(self, "pair_range"):
+            out.pair_range = self.pair_range
+        return out
 
     @property
     def n1(self):

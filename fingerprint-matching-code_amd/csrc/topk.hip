@@ -268,6 +268,9 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
 #undef SVAL
 }
 
+// largest n1max / n2max of the selection kernels (the Sinkhorn / soft top-k bound)
+constexpr int kSelMax = 2048;
+
 // Greedy top-k over Hungarian matches: prod = x * ds; argsort(prod, desc); accept (r,c) while
 // row r and column c are free until round(k) (half-to-even) are accepted.  Positive entries are
 // exactly the matched ones (pairwise row/col disjoint), taken in descending value; the
@@ -277,9 +280,9 @@ __global__ __launch_bounds__(256) void topk_select_kernel(const float* __restric
                                                           const float* __restrict__ kvec, int n1max, int n2max,
                                                           float* __restrict__ perm, long pb, long pld,
                                                           float* __restrict__ lsa_out, long lb, long lld) {
-    __shared__ float val[512];
-    __shared__ int key[512];
-    __shared__ unsigned char rowt[1024], colt[1024];
+    __shared__ float val[kSelMax];
+    __shared__ int key[kSelMax];
+    __shared__ unsigned char rowt[kSelMax], colt[kSelMax];
     const int b = blockIdx.x, tid = threadIdx.x;
     const float* D = ds + (long)b * sb;
     const int* A = assign + (long)b * asb;
@@ -297,7 +300,7 @@ __global__ __launch_bounds__(256) void topk_select_kernel(const float* __restric
     };
     zero_block(P, pld);
     if (lsa_out) zero_block(lsa_out + (long)b * lb, lld);
-    for (int r = tid; r < 1024; r += 256) { rowt[r] = 0; colt[r] = 0; }
+    for (int r = tid; r < kSelMax; r += 256) { rowt[r] = 0; colt[r] = 0; }
     int n = 1;
     while (n < n1max) n <<= 1;
     for (int r = tid; r < n; r += 256) {
@@ -363,6 +366,59 @@ __global__ __launch_bounds__(256) void topk_select_kernel(const float* __restric
     }
 }
 
+
+// greedy_perm(x, top_indices, ks) (soft_topk.py:56-77) for an arbitrary candidate order: walk
+// top_indices[b][0..T) and accept (row, col) = (idx / n2max, idx % n2max) while the row and the
+// column of x still sum to < 1, until round(ks[b]) (half-to-even) are accepted.  x is updated in
+// place like the reference's; its initial row / column sums are taken into account.  One
+// workgroup per pair: the sums are built in parallel, the walk is serial (it is order dependent)
+// with the next 256 candidates staged in LDS.
+__global__ __launch_bounds__(256) void greedy_perm_kernel(const long* __restrict__ top, long tsb, int T,
+                                                          const float* __restrict__ kvec, int n1max, int n2max,
+                                                          float* __restrict__ x, long xb, long xld) {
+    __shared__ float rows[kSelMax], cols[kSelMax];
+    __shared__ long cand[256];
+    __shared__ int done;
+    const int b = blockIdx.x, tid = threadIdx.x;
+    float* X = x + (long)b * xb;
+    for (int r = tid; r < n1max; r += 256) {
+        float a = 0.f;
+        for (int c = 0; c < n2max; ++c) a += X[r * xld + c];
+        rows[r] = a;
+    }
+    for (int c = tid; c < n2max; c += 256) {
+        float a = 0.f;
+        for (int r = 0; r < n1max; ++r) a += X[r * xld + c];
+        cols[c] = a;
+    }
+    if (tid == 0) done = 0;
+    __syncthreads();
+    const int K = (int)rintf(kvec[b]);
+    int matched = 0;                      // meaningful in thread 0 only
+    for (int t0 = 0; t0 < T; t0 += 256) {
+        if (tid < 256 && t0 + tid < T) cand[tid] = top[(long)b * tsb + t0 + tid];
+        __syncthreads();
+        if (tid == 0) {
+            const int tn = min(256, T - t0);
+            for (int t = 0; t < tn && matched < K; ++t) {
+                const long q = cand[t];
+                const long r = q / n2max, c = q - r * n2max;
+                if (q < 0 || r >= n1max) continue;
+                if (cols[c] < 1.f && rows[r] < 1.f) {
+                    const float old = X[r * xld + c];
+                    X[r * xld + c] = 1.f;
+                    rows[r] += 1.f - old;
+                    cols[c] += 1.f - old;
+                    ++matched;
+                }
+            }
+            if (matched >= K) done = 1;
+        }
+        __syncthreads();
+        if (done) break;
+    }
+}
+
 }  // namespace
 
 // single-pass early column steps (env FPM_TOPK_FAST / fpm_set_tuning("topk_fast"))
@@ -399,9 +455,20 @@ extern "C" int fpm_soft_topk_fwd(const float* ss, long s_sb, long s_ld, const in
 extern "C" int fpm_topk_select(const float* ds, long d_sb, long d_ld, const int* assign, long a_sb,
                                const float* k, int B, int n1max, int n2max, float* perm, long p_sb, long p_ld,
                                float* lsa_out, long l_sb, long l_ld, void* stream) {
-    FPM_CHECK_ARG(n1max <= 512 && n2max <= 1024, "topk_select: n1max<=512, n2max<=1024 required");
+    FPM_CHECK_ARG(n1max > 0 && n2max > 0 && n1max <= kSelMax && n2max <= kSelMax,
+                  "topk_select: 0 < n1max, n2max <= %d required (got %d, %d)", kSelMax, n1max, n2max);
     if (B == 0) return 0;
     hipLaunchKernelGGL(topk_select_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, ds, d_sb, d_ld, assign, a_sb,
                        k, n1max, n2max, perm, p_sb, p_ld, lsa_out, l_sb, l_ld);
     return fpm::check_launch("fpm_topk_select");
+}
+
+extern "C" int fpm_greedy_perm(const long* top_idx, long t_sb, int T, const float* k, int B, int n1max, int n2max,
+                               float* x, long x_sb, long x_ld, void* stream) {
+    FPM_CHECK_ARG(B >= 0 && T >= 0 && n1max > 0 && n2max > 0 && n1max <= kSelMax && n2max <= kSelMax,
+                  "greedy_perm: 0 < n1max, n2max <= %d required (got %d, %d)", kSelMax, n1max, n2max);
+    if (B == 0) return 0;
+    hipLaunchKernelGGL(greedy_perm_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, top_idx, t_sb, T, k, n1max,
+                       n2max, x, x_sb, x_ld);
+    return fpm::check_launch("fpm_greedy_perm");
 }

@@ -4,12 +4,15 @@ Drop-in for the reference's ``Net`` (``src/model/ngm.py:117-491``): same constru
 (``Net(regression=False)``), same ``forward(data_dict, regression=True) -> data_dict`` writing
 ``ds_mat``, ``perm_mat``, ``ks_loss``, ``ks_error``, ``cls_loss``, ``cls_prob``, ``k_prob``
 (ngm.py:479-487), and the same state_dict names/shapes (so ``utils/models_sl.load_model`` works).
-The forward starts from per-graph node features (``data_dict['node_features']`` /
-``['global_features']``, or a prebuilt ``data_dict['fpm_batch']``), or -- with
-``Net(backbone=True)`` -- from the reference's ``images`` / ``Ps`` / ``ns`` keys: ResNet-18 on
-MIOpen (``fpm.backbone``), then the fused normalise + feature_align + concat kernel
+Like the reference's ``Net`` (ngm.py:226-249), the default constructor carries the ResNet-18
+backbone (``node_layers.*`` / ``edge_layers.*`` state_dict names), so the reference's
+``images`` / ``Ps`` / ``ns`` data_dict (``evaluate_binary_classifier.py:77-97``) works as is:
+ResNet-18 on MIOpen (``fpm.backbone``), then the fused normalise + feature_align + concat kernel
 (``fpm_feature_align_fwd``); missing ``pyg_graphs`` are built on the device from ``Ps``
-(Delaunay, ``fpm.graphs``).  Every compute stage runs in ``libfpm_hip.so``; the
+(Delaunay, ``fpm.graphs``).  A data_dict that already holds per-graph node features
+(``node_features`` / ``global_features``, or a prebuilt ``fpm_batch``) skips the backbone;
+``Net(backbone=False)`` builds the matcher alone (its state_dict then has no backbone keys).
+Every compute stage runs in ``libfpm_hip.so``; the
 Hungarian step runs on host threads (``fpm_lsa_batch_host``) as the reference's does.
 
 ``dtype``: ``"f32"`` (parity mode: fp32 MFMA, matches the CPU oracle) or ``"bf16"`` (bf16 MFMA
@@ -31,11 +34,15 @@ from .batch import DeviceBatch
 
 
 def host_cpu_share():
-    """CPUs this process may use for the host Hungarian pool: OMP_NUM_THREADS (16 per GPU on the
-    pool) capped by the affinity mask.  torch.distributed.run exports OMP_NUM_THREADS=1 when the
-    variable was unset; under it (LOCAL_WORLD_SIZE present) a share of 1 is read as that default
-    and replaced by the affinity mask split over the node's ranks (at most 16 each)."""
+    """CPUs this process may use for the host Hungarian pool.  ``FPM_CPU_SHARE`` sets it explicitly
+    (``FPM_LSA_THREADS`` sets the pool size itself, default 2 per CPU of the share).  Otherwise:
+    OMP_NUM_THREADS (16 per GPU on the pool) capped by the affinity mask; under
+    torch.distributed.run (LOCAL_WORLD_SIZE present), whose launcher exports OMP_NUM_THREADS=1 when
+    the variable was unset, a share of 1 is read as that default and replaced by the affinity mask
+    split over the node's ranks (at most 16 each) -- set FPM_CPU_SHARE=1 to really run on one CPU."""
     n_aff = len(os.sched_getaffinity(0))
+    if os.environ.get("FPM_CPU_SHARE"):
+        return max(1, min(int(os.environ["FPM_CPU_SHARE"]), n_aff))
     omp = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
     if omp <= 1 and "LOCAL_WORLD_SIZE" in os.environ:
         omp = min(16, n_aff // max(1, int(os.environ["LOCAL_WORLD_SIZE"])))
@@ -65,7 +72,7 @@ def _build_tree(root, sd):
 
 class Net(nn.Module):
     def __init__(self, regression=False, dtype="f32", seed=0, lsa_threads=None, chunks=None, compute_ke=False,
-                 backbone=False, lsa=None):
+                 backbone=True, lsa=None):
         super().__init__()
         _build_tree(self, P.init_params(seed))
         if backbone:
@@ -416,7 +423,7 @@ class Net(nn.Module):
             ks.copy_(gt_ks[b0:b1] / min_pt[b0:b1])
         self._mark("afau")
         k_used = gt_ks[b0:b1] if self.training else ks * min_pt[b0:b1]
-        ops.soft_topk(o["ss"][b0:b1], part.n1, part.n2, k_used.contiguous(), C.SK_ITER_NUM, self.tau,
+        ops.soft_topk_fwd(o["ss"][b0:b1], part.n1, part.n2, k_used.contiguous(), C.SK_ITER_NUM, self.tau,
                       out=o["ds_mat"][b0:b1], steps=o["sk_steps"][b0:b1],
                       out_host=self._pinned[b0:b1] if self.zero_copy else None)
         o["_kk"][b0:b1].copy_(ks * min_pt[b0:b1])
@@ -582,8 +589,8 @@ class Net(nn.Module):
         global max-pool + channel L2-norm + bilinear feature_align + [U || F] concat.
         Returns (node feature rows 2 x (B*nmax, 768) with zero padding rows, globals 2 x (B, 512))."""
         if not hasattr(self, "node_layers"):
-            raise NotImplementedError("image input needs the backbone: construct Net(backbone=True) "
-                                      "(or pass data_dict['node_features'] / ['global_features'])")
+            raise NotImplementedError("image input needs the backbone: this Net was built with backbone=False "
+                                      "(pass data_dict['node_features'] / ['global_features'] instead)")
         dev = dev or torch.device("cuda", torch.cuda.current_device())
         if self._backbone_dev != dev:
             for m in (self.node_layers, self.edge_layers):

@@ -52,7 +52,7 @@ def sinkhorn(s, n1, n2, iters, tau, dummy_row=True, out=None, n1max=None, n2max=
     return out
 
 
-def soft_topk(ss, n1, n2, k, iters=10, tau=0.01, out=None, steps=None, out_host=None):
+def soft_topk_fwd(ss, n1, n2, k, iters=10, tau=0.01, out=None, steps=None, out_host=None):
     """``out_host``: optional pinned host tensor written by the kernel as well (zero-copy D2H of
     ds_mat for the host Hungarian)."""
     _dev(ss, n1, n2, k)
@@ -364,3 +364,125 @@ def copy_async(dst, src, nblocks=16):
         raise _lib.FpmError("copy_async: host destination must be pinned")
     _lib.call("fpm_copy_async", _p(src), _p(dst), src.numel() * src.element_size(), int(nblocks), _stream(src))
     return dst
+
+
+# ---- reference-signature mirrors (SURVEY §8(b) "Python layer") ----------------------------------
+# Same names, argument order and meaning as the reference's operators, on the HIP kernels above, so
+# code written against src/model/sinkhorn.py, src/model/soft_topk.py and utils/hungarian.py runs
+# unchanged on device tensors.  Net.forward itself uses the fused kernels directly.
+def _counts(n, B, full, dev):
+    """nrows / ncols as the kernels take them: int32 on ``dev``; None -> the unpadded size."""
+    if n is None:
+        return torch.full((B,), int(full), dtype=torch.int32, device=dev)
+    return torch.as_tensor(n).reshape(-1).to(device=dev, dtype=torch.int32)
+
+
+class Sinkhorn(torch.nn.Module):
+    """``Sinkhorn(max_iter=10, tau=1., epsilon=1e-4, log_forward=True, batched_operation=False)``
+    (``src/model/sinkhorn.py:7-87``), whose ``forward_log`` is ``pygmtools.sinkhorn``: log-domain
+    alternating row / column normalisation of ``s / tau`` on each pair's valid block, dummy rows
+    when asked, pairs with n1 > n2 run transposed.  Differentiable (``fpm_sinkhorn_log_bwd``).
+    ``epsilon`` and ``batched_operation`` do not change the log-domain result and are accepted
+    for signature parity."""
+
+    def __init__(self, max_iter=10, tau=1., epsilon=1e-4, log_forward=True, batched_operation=False):
+        super().__init__()
+        if not log_forward:
+            # forward_ori is deprecated in the reference (sinkhorn.py:53-54); only the log form is built
+            raise NotImplementedError("Sinkhorn(log_forward=False) is not built: use the log-domain forward")
+        self.max_iter, self.tau, self.epsilon = max_iter, tau, epsilon
+        self.log_forward, self.batched_operation = log_forward, batched_operation
+
+    def forward(self, s, nrows=None, ncols=None, dummy_row=False):
+        return self.forward_log(s, nrows, ncols, dummy_row)
+
+    def forward_log(self, s, nrows=None, ncols=None, dummy_row=False):
+        _dev(s)
+        matrix_input = s.dim() == 2
+        if matrix_input:
+            s = s.unsqueeze(0)
+        if s.dim() != 3:
+            raise ValueError("input data shape not understood: %s" % (tuple(s.shape),))
+        B, n1max, n2max = s.shape
+        n1 = _counts(nrows, B, n1max, s.device)
+        n2 = _counts(ncols, B, n2max, s.device)
+        sf = s.float()
+        if sf.requires_grad and torch.is_grad_enabled():
+            from .train import SinkhornFn
+            out = SinkhornFn.apply(sf, n1, n2, int(self.max_iter), float(self.tau), bool(dummy_row))
+        else:
+            out = sinkhorn(sf.detach(), n1, n2, int(self.max_iter), float(self.tau), bool(dummy_row))
+        out = out.to(s.dtype)
+        return out.squeeze(0) if matrix_input else out
+
+
+def greedy_perm(x, top_indices, ks):
+    """``greedy_perm(x, top_indices, ks)`` (``src/model/soft_topk.py:56-77``): walk each pair's
+    candidate order and accept (idx // n2max, idx % n2max) while its row and column of ``x`` still
+    sum to < 1, until ``round(ks[b])`` (half-to-even) are accepted.  ``x`` is updated in place and
+    returned (fpm_greedy_perm)."""
+    _dev(x, top_indices)
+    if x.dim() != 3 or x.dtype != torch.float32 or x.stride(2) != 1:
+        raise _lib.FpmError("greedy_perm: x must be a (b, n1, n2) float32 tensor with unit column stride")
+    B, n1max, n2max = x.shape
+    top = top_indices.reshape(B, -1).to(torch.int64).contiguous()
+    k = torch.as_tensor(ks).reshape(-1).to(device=x.device, dtype=torch.float32).contiguous()
+    if k.numel() != B:
+        raise _lib.FpmError("greedy_perm: ks must hold one count per pair")
+    _lib.call("fpm_greedy_perm", _p(top), top.stride(0), int(top.shape[1]), _p(k), B, n1max, n2max, _p(x),
+              x.stride(0), x.stride(1), _stream(x))
+    return x
+
+
+def soft_topk(scores, ks, max_iter=10, tau=1., nrows=None, ncols=None, return_prob=False):
+    """``soft_topk(scores, ks, max_iter, tau, nrows, ncols, return_prob)``
+    (``src/model/soft_topk.py:8-53``): the 2-column marginal Sinkhorn incl. ``Sinkhorn_m``'s
+    data-dependent continuation (fpm_soft_topk_fwd), then the reference's own hard output:
+    candidates in descending order of P(top-k) over the pair's flattened valid block
+    (q = i * n2 + j, padded to max(nrows) * max(ncols) with zeros), decoded with the box width
+    like the reference's greedy_perm.  Ties keep ascending flat index (the reference's argsort is
+    unstable, quirk A.10(v)).  Returns x, or (x, soft matrix) with ``return_prob``.  The soft
+    matrix is differentiable in ``scores`` (fpm_soft_topk_bwd)."""
+    _dev(scores)
+    B, n1max, n2max = scores.shape
+    n1 = _counts(nrows, B, n1max, scores.device)
+    n2 = _counts(ncols, B, n2max, scores.device)
+    k = torch.as_tensor(ks).reshape(-1).to(device=scores.device, dtype=torch.float32)
+    sf = scores.float()
+    if sf.requires_grad and torch.is_grad_enabled():
+        from .train import SoftTopkFn
+        out_s = SoftTopkFn.apply(sf, k, n1, n2, int(max_iter), float(tau))
+    else:
+        out_s = soft_topk_fwd(sf.detach().contiguous(), n1, n2, k.contiguous(), int(max_iter), float(tau))
+    # the reference's output[:, :, 1]: (b, max(nrows) * max(ncols)), pair b's block row-major first
+    L = int(n1.max()) * int(n2.max())
+    q = torch.arange(L, device=scores.device)
+    n2l = n2.long()[:, None]
+    valid = q[None, :] < (n1.long() * n2.long())[:, None]
+    flat = out_s.detach()[torch.arange(B, device=scores.device)[:, None],
+                          torch.where(valid, q[None, :] // n2l, 0), torch.where(valid, q[None, :] % n2l, 0)]
+    flat = torch.where(valid, flat, torch.zeros((), device=scores.device))
+    top = torch.argsort(flat, dim=-1, descending=True, stable=True)
+    x = greedy_perm(torch.zeros(B, n1max, n2max, device=scores.device), top, k)
+    x = x.to(scores.dtype)
+    return (x, out_s.to(scores.dtype)) if return_prob else x
+
+
+def hungarian(s, n1=None, n2=None, nproc=1):
+    """``hungarian(s, n1, n2, nproc)`` (``utils/hungarian.py:8-66``): the optimal assignment
+    maximising ``s`` on each pair's valid block (scipy ``linear_sum_assignment`` of ``-s``, same
+    tie rules) -> 0/1 matrix of ``s``'s shape, dtype and device.  Solved on the host LSA pool
+    (fpm_lsa_batch_host, ``nproc`` threads) as the reference solves it on the host."""
+    matrix_input = s.dim() == 2
+    if matrix_input:
+        s = s.unsqueeze(0)
+    elif s.dim() != 3:
+        raise ValueError("input data shape not understood: %s" % (tuple(s.shape),))
+    B, n1max, n2max = s.shape
+    host = s.detach().to("cpu", torch.float32).contiguous()
+    a = lsa_batch_host(host, _counts(n1, B, n1max, "cpu"), _counts(n2, B, n2max, "cpu"), max(1, int(nproc)))
+    perm = torch.zeros(B, n1max, n2max, dtype=torch.float32)
+    r = torch.nonzero(a >= 0)
+    perm[r[:, 0], r[:, 1], a[r[:, 0], r[:, 1]].long()] = 1.0
+    perm = perm.to(device=s.device, dtype=s.dtype)
+    return perm.squeeze(0) if matrix_input else perm

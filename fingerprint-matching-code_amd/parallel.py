@@ -1,0 +1,170 @@
+"""Pair-sharded forward over several GPUs of one process.
+
+Replaces the reference's ``DataParallel`` (``src/parallel/data_parallel.py:6-17``,
+``scatter_gather.py:6-91``) at its call site (``train.py:147-148``): the caller keeps one module
+and one ``forward(data_dict) -> data_dict`` call; underneath, the batch is cut into contiguous
+pair ranges, one per device, and every device runs the whole matcher forward on its range:
+
+  * one host thread and one set of HIP streams per device (``Net.run`` on a per-device replica
+    that shares the parameters and packs them once per device);
+  * no collective: pairs are independent, shards keep the parent batch's padded
+    sizes, so the gathered outputs equal the single-device forward bit for bit;
+  * one shared host Hungarian pool (``fpm_lsa_batch_host``) consumes every device's pinned
+    ``ds_mat`` copies, one batch at a time, with the process's whole CPU share;
+  * one gather: every shard's outputs are copied into the caller's ``data_dict`` on
+    ``output_device`` (peer copies over xGMI), as ``DataParallel.gather`` does.
+
+Multi-process (one process per GPU, torch.distributed.run) is what ``bench.py --gpus N`` uses;
+this class is the single-process product API.  The device list may repeat a device
+(``devices=[0, 0]``): the shards then run concurrently on that device, which is how the sharded
+path is tested on a one-GPU box.
+"""
+import copy
+import threading
+
+import torch
+import torch.nn as nn
+
+from .batch import DeviceBatch
+from .model import host_cpu_share
+
+
+def _replica(net):
+    """A Net sharing ``net``'s parameters, with its own packed weights, pinned buffer and streams."""
+    r = copy.copy(net)
+    r._pack, r._pack_key, r._pinned = None, None, None
+    r._stream_cache = {}
+    r.stage_times = {}
+    r.last_timing = {}
+    return r
+
+
+def shard_bounds(B, n_shards):
+    """Contiguous pair ranges [(b0, b1)] of a B-pair batch over ``n_shards`` devices (empty ranges
+    dropped); the first ``B % n_shards`` shards hold one pair more."""
+    n_shards = max(1, int(n_shards))
+    q, r = divmod(int(B), n_shards)
+    out, b0 = [], 0
+    for g in range(n_shards):
+        b1 = b0 + q + (1 if g < r else 0)
+        if b1 > b0:
+            out.append((b0, b1))
+        b0 = b1
+    return out
+
+
+class ShardedNet(nn.Module):
+    """``ShardedNet(net, devices=None, output_device=None)``: ``net`` (an ``fpm.Net``) run pair-sharded
+    over ``devices`` (default: every visible GPU).  ``forward(data_dict, regression=True)`` writes the
+    reference's output keys, gathered on ``output_device`` (default ``devices[0]``)."""
+
+    OUT_KEYS = ("ds_mat", "perm_mat", "k_prob", "cls_prob")
+
+    def __init__(self, net, devices=None, output_device=None, lsa_threads=None):
+        super().__init__()
+        self.module = net
+        if devices is None:
+            devices = list(range(torch.cuda.device_count()))
+        self.devices = [torch.device("cuda", d) if isinstance(d, int) else torch.device(d) for d in devices]
+        if not self.devices:
+            raise ValueError("ShardedNet needs at least one device")
+        self.output_device = torch.device(output_device) if output_device is not None else self.devices[0]
+        if isinstance(output_device, int):
+            self.output_device = torch.device("cuda", output_device)
+        self._replicas = [_replica(net) for _ in self.devices]
+        # one shared Hungarian pool: each device's batch uses the whole share in turn
+        threads = lsa_threads or 2 * host_cpu_share()
+        for r in self._replicas:
+            r.lsa_threads = threads
+        self.last_timing = {}
+
+    def train(self, mode=True):
+        if mode:
+            raise NotImplementedError("ShardedNet is the inference forward; train through fpm.Net")
+        return super().train(False)
+
+    def _run_shard(self, g, part, gt, label, results, errors):
+        dev = self.devices[g]
+        try:
+            with torch.cuda.device(dev):
+                rep = self._replicas[g]
+                rep.regression, rep.training = self.module.regression, False
+                results[g] = rep.run(part, gt_perm=gt, label=label)
+                torch.cuda.current_stream(dev).synchronize()
+        except BaseException as e:            # surfaced on the calling thread
+            errors[g] = e
+
+    def run(self, bt, gt_perm=None, label=None):
+        """Sharded ``Net.run`` over a DeviceBatch ``bt`` -> dict of gathered outputs."""
+        bounds = shard_bounds(bt.B, len(self.devices))
+        if len(bounds) == 1 and self.devices[0] == bt.device:
+            return self._replicas[0].run(bt, gt_perm=gt_perm, label=label)
+        parts = []
+        if bt.edge_off is None:
+            raise ValueError("ShardedNet needs a batch with per-pair edge offsets")
+        for g, (b0, b1) in enumerate(bounds):
+            sub = bt.split_range(b0, b1)
+            parts.append(sub.to(self.devices[g]))
+        results, errors = [None] * len(parts), [None] * len(parts)
+        gts = [None if gt_perm is None else torch.as_tensor(gt_perm)[b0:b1] for b0, b1 in bounds]
+        labels = [None if label is None else torch.as_tensor(label).reshape(-1)[b0:b1] for b0, b1 in bounds]
+        threads = [threading.Thread(target=self._run_shard, args=(g, parts[g], gts[g], labels[g], results, errors))
+                   for g in range(len(parts))]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+        for e in errors:
+            if e is not None:
+                raise e
+        return self._gather(bt, bounds, results, gt_perm, label)
+
+    def _gather(self, bt, bounds, results, gt_perm, label):
+        od = self.output_device
+        B = bt.B
+        res = {}
+        for k in self.OUT_KEYS + ("s", "ss", "lsa"):
+            shape = (B,) + tuple(results[0][k].shape[1:])
+            out = torch.empty(shape, device=od, dtype=results[0][k].dtype)
+            for (b0, b1), r in zip(bounds, results):
+                out[b0:b1].copy_(r[k], non_blocking=True)
+            res[k] = out
+        torch.cuda.synchronize(od)
+        # the losses over the whole batch, as Net.run computes them (ngm.py:458-477)
+        net = self.module
+        ks = res["k_prob"]
+        min_pt = torch.minimum(bt.n1, bt.n2).to(device=od, dtype=torch.float32)
+        gt_ks = min_pt if gt_perm is None else \
+            torch.as_tensor(gt_perm).to(od).reshape(B, -1).sum(-1).to(torch.float32)
+        logits = torch.cat([r["cls_logits"].to(od) for r in results]) if "cls_logits" in results[0] else None
+        if label is not None and logits is not None:
+            res["cls_loss"] = nn.functional.binary_cross_entropy_with_logits(
+                logits, torch.as_tensor(label).to(od).view(-1).float())
+        else:
+            res["cls_loss"] = torch.tensor(0.0, device=od)
+        if net.regression:
+            res["ks_loss"] = nn.functional.mse_loss(ks, gt_ks / min_pt) * net.k_factor
+            res["ks_error"] = nn.functional.l1_loss(ks * min_pt, gt_ks)
+        else:
+            res["ks_loss"] = 0.0
+            res["ks_error"] = 0.0
+        self.last_timing = {"shards": [r_.last_timing for r_ in self._replicas[:len(bounds)]],
+                            "bounds": bounds}
+        return res
+
+    def forward(self, data_dict, regression=True):
+        """Reference signature (ngm.py:205): reads the same data_dict as ``Net.forward`` and writes
+        ``ds_mat``, ``perm_mat``, ``ks_loss``, ``ks_error``, ``cls_loss``, ``cls_prob``, ``k_prob``."""
+        od = self.output_device
+        bt = data_dict.get("fpm_batch")
+        if bt is None:
+            with torch.cuda.device(od):
+                bt = self._replicas[0]._batch_from_dict(data_dict, od)
+        res = self.run(bt, gt_perm=data_dict.get("gt_perm_mat"), label=data_dict.get("label"))
+        self.last_outputs = res
+        data_dict.update({k: res[k] for k in ("ds_mat", "perm_mat", "ks_loss", "ks_error", "cls_loss", "cls_prob",
+                                              "k_prob")})
+        return data_dict
+
+
+__all__ = ["ShardedNet", "shard_bounds", "DeviceBatch"]

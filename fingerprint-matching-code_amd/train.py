@@ -287,17 +287,18 @@ class SinkhornFn(torch.autograd.Function):
     """Sinkhorn(max_iter, tau)(s, n1, n2, dummy_row=True) (sinkhorn.py:85-87, ngm.py:371)."""
 
     @staticmethod
-    def forward(ctx, s, n1, n2, iters, tau):
+    def forward(ctx, s, n1, n2, iters, tau, dummy_row=True):
         sc = s.detach().contiguous()
-        out = ops.sinkhorn(sc, n1, n2, iters, tau, True)
+        out = ops.sinkhorn(sc, n1, n2, iters, tau, dummy_row)
         ctx.save_for_backward(sc, n1, n2)
-        ctx.iters, ctx.tau = iters, tau
+        ctx.iters, ctx.tau, ctx.dummy_row = iters, tau, bool(dummy_row)
         return out
 
     @staticmethod
     def backward(ctx, g):
         sc, n1, n2 = ctx.saved_tensors
-        return sinkhorn_bwd(sc, g.contiguous(), n1, n2, ctx.iters, ctx.tau, True), None, None, None, None
+        ds = sinkhorn_bwd(sc, g.contiguous(), n1, n2, ctx.iters, ctx.tau, ctx.dummy_row)
+        return ds, None, None, None, None, None
 
 
 class SoftTopkFn(torch.autograd.Function):
@@ -309,7 +310,7 @@ class SoftTopkFn(torch.autograd.Function):
         ssc = ss.detach().contiguous()
         kc = k.detach().float().contiguous()
         steps = torch.empty(B, device=ss.device, dtype=torch.int32)
-        out = ops.soft_topk(ssc, n1, n2, kc, iters, tau, steps=steps)
+        out = ops.soft_topk_fwd(ssc, n1, n2, kc, iters, tau, steps=steps)
         ctx.save_for_backward(ssc, kc, steps, n1, n2)
         ctx.tau = tau
         return out

@@ -31,7 +31,8 @@ int fpm_device_sync(void);
  * Replaces Sinkhorn.forward_log -> pygmtools.sinkhorn (src/model/sinkhorn.py:85-87), used by
  * PYGNNLayer (src/model/gnn.py:221, 20 iterations) and Net.forward (ngm.py:371, 10 iterations).
  * out[b] = exp(L) on the valid block [:n1[b], :n2[b]] of the (n1max, n2max) box, 0 elsewhere.
- * Any strides; n1max, n2max <= 256 (VGPR-resident block). */
+ * Any strides.  n1max, n2max <= 256 run VGPR-resident (one workgroup per pair); larger boxes, up
+ * to 2048, stream the block through L2 (same arithmetic, fpm_sinkhorn_log_fwd picks the variant). */
 int fpm_sinkhorn_log_fwd(const float* s, long s_sb, long s_si, long s_sj, float* out, long o_sb, long o_si,
                          long o_sj, const int* n1, const int* n2, int B, int n1max, int n2max, int iters,
                          float tau, int dummy_row, void* stream);
@@ -45,12 +46,20 @@ int fpm_soft_topk_fwd(const float* ss, long s_sb, long s_ld, const int* n1, cons
                       float* out2, long o2_sb, long o2_ld, void* stream);
 
 /* ---- greedy top-k selection -------------------------------------------------------------------
- * Replaces argsort(x * ss_out) + greedy_perm (ngm.py:445-449, soft_topk.py:56-77).
+ * Replaces argsort(x * ss_out) + greedy_perm (ngm.py:445-449, soft_topk.py:56-77).  n1max, n2max <= 2048.
  * assign[b][r] = column matched to row r by the LSA (or -1); perm receives the 0/1 matrix;
  * lsa_out (optional) receives the dense LSA matrix x. */
 int fpm_topk_select(const float* ds, long d_sb, long d_ld, const int* assign, long a_sb, const float* k, int B,
                     int n1max, int n2max, float* perm, long p_sb, long p_ld, float* lsa_out, long l_sb, long l_ld,
                     void* stream);
+
+/* ---- greedy_perm for an arbitrary candidate order ---------------------------------------------
+ * Replaces greedy_perm(x, top_indices, ks) (src/model/soft_topk.py:56-77) as called inside
+ * soft_topk (:40-41).  top_idx[b][0..T) (int64, flat indices into the (n1max, n2max) box, decoded
+ * as idx / n2max, idx % n2max like the reference); x is updated in place (rows / columns whose sum
+ * is >= 1 are taken).  k[b] is rounded half-to-even.  n1max, n2max <= 2048. */
+int fpm_greedy_perm(const long* top_idx, long t_sb, int T, const float* k, int B, int n1max, int n2max, float* x,
+                    long x_sb, long x_ld, void* stream);
 
 /* ---- generic MFMA GEMM with fused epilogue ----------------------------------------------------
  * C[b][r][n] = epi(sum_k A[b][row(r)][k] * B[b][n][k] (+ bias[n])), row(r) = a_rows ? a_rows[r] : r.

@@ -10,7 +10,7 @@ import scipy.optimize as opt
 import torch
 
 import fpm  # noqa: F401
-from fpm import _lib
+from fpm import _lib, params
 
 from conftest import REPO
 
@@ -93,7 +93,7 @@ def test_lsa_host_golden():
 
 def test_state_dict_names():
     """Parameter names/shapes follow Net.__init__ (ngm.py:118-202) incl. PyG/torch module names."""
-    net = fpm.Net(regression=True)
+    net = fpm.Net(regression=True, backbone=False)
     sd = net.state_dict()
     assert sd["message_pass_node_features.mp_network.convs.0.weight"].shape == (25, 768, 768)
     assert sd["message_pass_node_features.mp_network.convs.1.root"].shape == (768, 768)
@@ -109,6 +109,24 @@ def test_state_dict_names():
     assert sd["final_row.0.weight"].shape == (8, 600)
     assert sd["match_cls.conv.4.weight"].shape == (32, 16, 3, 3)
     assert sd["match_cls.conv.6.running_var"].shape == (32,)
-    net2 = fpm.Net(regression=True, seed=3)
+    net2 = fpm.Net(regression=True, backbone=False, seed=3)
     net2.load_state_dict(sd)
     assert torch.equal(net2.state_dict()["vertex_affinity.A.bias"], sd["vertex_affinity.A.bias"])
+
+
+def test_default_net_carries_backbone():
+    """Net() like the reference's (ngm.py:118, 226-249): regression off, ResNet-18 backbone
+    parameters under the reference names; a full reference-named state_dict loads strictly."""
+    from fpm.backbone import backbone_state_dict
+    net = fpm.Net()
+    assert not net.regression
+    sd = net.state_dict()
+    assert sd["node_layers.0.weight"].shape == (64, 3, 7, 7)
+    assert sd["edge_layers.0.1.bn2.running_var"].shape == (512,)
+    assert "vertex_affinity.A.weight" in sd
+    full = dict(params.init_params(2))
+    full.update(backbone_state_dict(2))
+    net.load_state_dict(full)
+    assert torch.equal(net.state_dict()["node_layers.4.0.conv1.weight"], full["node_layers.4.0.conv1.weight"])
+    bare = fpm.Net(backbone=False)
+    assert not any(k.startswith(("node_layers.", "edge_layers.")) for k in bare.state_dict())

@@ -195,7 +195,7 @@ def test_forward_from_keypoints_equals_host_graphs():
             P[side][b, :n] = p32
             pr.append(g)
         pairs.append(tuple(pr))
-    net = fpm.Net(regression=True)
+    net = fpm.Net(regression=True, backbone=False)
     net.load_state_dict(sd)
     host = DeviceBatch.from_pairs(pairs, DEV)
     dev = DeviceBatch.from_keypoints([torch.from_numpy(P[0]).to(DEV), torch.from_numpy(P[1]).to(DEV)],

@@ -90,7 +90,7 @@ def test_lsa_device_on_forward_ds_mat(n, B):
     import fpm
     from fpm import ops, params, synth
     from fpm.batch import DeviceBatch
-    net = fpm.Net(regression=True, dtype="bf16", lsa="host")
+    net = fpm.Net(regression=True, backbone=False, dtype="bf16", lsa="host")
     net.load_state_dict(params.init_params(2))
     bt = DeviceBatch.from_pairs(synth.make_batch(4, B, n), DEV)
     res = net.run(bt)
@@ -110,7 +110,7 @@ def test_forward_device_lsa_equals_host_lsa():
     bt = DeviceBatch.from_pairs(pairs, DEV)
     outs = []
     for mode in ("host", "device"):
-        net = fpm.Net(regression=True, lsa=mode)
+        net = fpm.Net(regression=True, backbone=False, lsa=mode)
         net.load_state_dict(sd)
         outs.append(net.run(bt, chunks=3))
     for k in ("ds_mat", "perm_mat", "k_prob", "cls_prob"):

@@ -78,6 +78,7 @@ def test_two_rank_sharding(tmp_path):
 def test_host_cpu_share_under_torchrun(monkeypatch):
     """torch.distributed.run's OMP_NUM_THREADS=1 default must not shrink the Hungarian pool to
     2 threads per rank: the affinity mask is split over the node's ranks instead."""
+    monkeypatch.delenv("FPM_CPU_SHARE", raising=False)
     from fpm.model import host_cpu_share
     n_aff = len(os.sched_getaffinity(0))
     monkeypatch.setenv("OMP_NUM_THREADS", "16")
@@ -87,3 +88,7 @@ def test_host_cpu_share_under_torchrun(monkeypatch):
     assert host_cpu_share() == 1                      # an explicit single-thread request outside torchrun
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "2")
     assert host_cpu_share() == max(1, min(16, n_aff // 2))
+    monkeypatch.setenv("FPM_CPU_SHARE", "1")          # explicit limit honoured under torchrun too
+    assert host_cpu_share() == 1
+    monkeypatch.setenv("FPM_CPU_SHARE", "3")
+    assert host_cpu_share() == min(3, n_aff)

@@ -1,0 +1,131 @@
+"""Reference-signature operator mirrors (SURVEY §8(b) "Python layer"): ``fpm.ops.Sinkhorn``,
+``soft_topk``, ``greedy_perm`` and ``hungarian`` called exactly as the reference calls
+``src/model/sinkhorn.py:46-87``, ``src/model/soft_topk.py:8,56`` and ``utils/hungarian.py:8``
+(``src/loss_func.py:158`` calls ``hungarian(s, n1, n2)`` the same way), checked against the
+reference-generated goldens and the oracle."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import fpm  # noqa: F401
+from fpm import ops
+import oracle as O
+
+from conftest import GOLDEN
+
+DEV = torch.device("cuda", 0)
+
+
+# ------------------------------------------------------------------------------ hungarian (host)
+def test_hungarian_mirror_golden():
+    """hungarian(s, n1, n2) == the reference's scipy result (golden, incl. a tie column)."""
+    z = np.load(os.path.join(GOLDEN, "hungarian_greedy.npz"))
+    s = torch.from_numpy(z["s"])
+    x = ops.hungarian(s, torch.from_numpy(z["n1"]), torch.from_numpy(z["n2"]))
+    assert x.dtype == s.dtype and x.shape == s.shape
+    np.testing.assert_array_equal(x.numpy(), z["x"])
+    # matrix input (utils/hungarian.py:22-24) and nproc > 1
+    x0 = ops.hungarian(s[0], nproc=4)
+    assert x0.shape == s[0].shape
+    np.testing.assert_array_equal(x0.numpy(), ops.hungarian(s[:1])[0].numpy())
+
+
+def test_hungarian_mirror_vs_scipy_rectangular():
+    from scipy.optimize import linear_sum_assignment
+    g = torch.Generator().manual_seed(4)
+    s = torch.rand(4, 12, 15, generator=g)
+    n1, n2 = torch.tensor([12, 9, 12, 5]), torch.tensor([15, 15, 7, 5])
+    x = ops.hungarian(s, n1, n2, nproc=2)
+    for b in range(4):
+        r, c = linear_sum_assignment(-s[b, :n1[b], :n2[b]].numpy())
+        ref = np.zeros((12, 15), np.float32)
+        ref[r, c] = 1
+        np.testing.assert_array_equal(x[b].numpy(), ref)
+
+
+def test_hungarian_mirror_rejects_bad_rank():
+    with pytest.raises(ValueError):
+        ops.hungarian(torch.zeros(2, 2, 2, 2))
+
+
+# ------------------------------------------------------------------------------ device mirrors
+@pytest.mark.gpu
+def test_greedy_perm_mirror_golden():
+    """greedy_perm(x, top_indices, ks) with the reference's own argsort order (golden ``top``)."""
+    z = np.load(os.path.join(GOLDEN, "hungarian_greedy.npz"))
+    x = torch.zeros(z["s"].shape, device=DEV)
+    out = ops.greedy_perm(x, torch.from_numpy(z["top"]).to(DEV), torch.from_numpy(z["ks"]).to(DEV))
+    assert out is x
+    np.testing.assert_array_equal(out.cpu().numpy(), z["perm"])
+
+
+@pytest.mark.gpu
+def test_greedy_perm_mirror_respects_initial_x():
+    """Rows / columns already holding a 1 in x are skipped, like the reference's sum test."""
+    x = torch.zeros(1, 3, 3, device=DEV)
+    x[0, 0, 1] = 1
+    top = torch.tensor([[1, 0, 4, 8, 5]], device=DEV)       # (0,1) taken; (0,0) row 0 busy
+    ops.greedy_perm(x, top, torch.tensor([2.0], device=DEV))
+    ref = torch.zeros(3, 3)
+    ref[0, 1] = 1                                            # the initial entry
+    ref[2, 2] = 1                                            # idx 8; idx 4 = (1,1): column 1 busy; idx 5: column 2
+    assert torch.equal(x[0].cpu(), ref)
+
+
+@pytest.mark.gpu
+def test_soft_topk_mirror_golden():
+    """soft_topk(scores, ks, max_iter, tau, nrows, ncols, return_prob=True) -> (x, soft) equal to the
+    reference's outputs (golden; c1 has ragged pairs)."""
+    z = np.load(os.path.join(GOLDEN, "soft_topk.npz"))
+    for i in range(int(z["ncases"])):
+        g = lambda k: z["c%d_%s" % (i, k)]
+        sc = torch.from_numpy(g("scores")).to(DEV)
+        x, ss = ops.soft_topk(sc, torch.from_numpy(g("ks")).to(DEV), 10, 0.01, torch.from_numpy(g("n1")),
+                              torch.from_numpy(g("n2")), True)
+        np.testing.assert_allclose(ss.cpu().numpy(), g("ss_out"), atol=1e-5, rtol=0)
+        np.testing.assert_array_equal(x.cpu().numpy(), g("x"))
+        x_only = ops.soft_topk(sc, torch.from_numpy(g("ks")).to(DEV), 10, 0.01, torch.from_numpy(g("n1")),
+                               torch.from_numpy(g("n2")))
+        assert torch.equal(x_only, x)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dummy_row", [True, False])
+def test_sinkhorn_mirror_reference_order(dummy_row):
+    """Sinkhorn(max_iter, tau)(s, nrows, ncols, dummy_row) as gnn.py:221 / ngm.py:371 call it."""
+    g = torch.Generator().manual_seed(8)
+    n1s, n2s = (12, 9, 12), (12, 12, 7)
+    s = torch.randn(3, 12, 12, generator=g) * 0.3
+    sk = ops.Sinkhorn(max_iter=20, tau=0.05)
+    out = sk(s.to(DEV), torch.tensor(n1s), torch.tensor(n2s), dummy_row=dummy_row).cpu()
+    ref = O.pygm_sinkhorn(s.double(), n1s, n2s, dummy_row=dummy_row, max_iter=20, tau=0.05)
+    assert (out.double() - ref).abs().max() < 1e-4
+    # no sizes: the full box (sinkhorn.py:66-67 "assume the batched matrices are not padded")
+    full = sk(s.to(DEV)).cpu()
+    ref_full = O.pygm_sinkhorn(s.double(), (12,) * 3, (12,) * 3, dummy_row=False, max_iter=20, tau=0.05)
+    assert (full.double() - ref_full).abs().max() < 1e-4
+    # matrix input
+    m = sk(s[0].to(DEV)).cpu()
+    assert m.shape == (12, 12) and torch.equal(m, full[0])
+
+
+@pytest.mark.gpu
+def test_sinkhorn_mirror_backward():
+    """The mirror is differentiable (fpm_sinkhorn_log_bwd) and its gradient matches autograd
+    through the oracle."""
+    g = torch.Generator().manual_seed(9)
+    n1s, n2s = (10, 7), (10, 10)
+    s = torch.randn(2, 10, 10, generator=g) * 0.3
+    w = torch.randn(2, 10, 10, generator=g)
+    sd = s.to(DEV).requires_grad_(True)
+    (ops.Sinkhorn(10, 0.1)(sd, torch.tensor(n1s), torch.tensor(n2s), True) * w.to(DEV)).sum().backward()
+    sr = s.double().requires_grad_(True)
+    (O.pygm_sinkhorn(sr, n1s, n2s, dummy_row=True, max_iter=10, tau=0.1) * w.double()).sum().backward()
+    assert (sd.grad.cpu().double() - sr.grad).abs().max() < 1e-4 * max(1.0, float(sr.grad.abs().max()))
+
+
+def test_log_forward_false_not_built():
+    with pytest.raises(NotImplementedError):
+        ops.Sinkhorn(log_forward=False)

@@ -1,0 +1,100 @@
+"""Pair-sharded forward in the product API (``fpm.parallel.ShardedNet``): contiguous
+pair ranges, one host thread + streams per device, one shared Hungarian pool, one gather.  On the
+one-GPU box the device list repeats cuda:0 (shards run concurrently on it); the gathered outputs
+must equal the single-device forward bit for bit."""
+import numpy as np
+import pytest
+import torch
+
+import fpm
+from fpm import params, synth
+from fpm.batch import DeviceBatch
+from fpm.parallel import ShardedNet, shard_bounds
+
+DEV = torch.device("cuda", 0)
+
+
+def test_shard_bounds():
+    assert shard_bounds(1024, 8) == [(i * 128, (i + 1) * 128) for i in range(8)]
+    assert shard_bounds(10, 4) == [(0, 3), (3, 6), (6, 8), (8, 10)]
+    assert shard_bounds(2, 4) == [(0, 1), (1, 2)]            # empty shards dropped
+    b = shard_bounds(10001, 8)
+    assert b[0][0] == 0 and b[-1][1] == 10001 and all(x[1] == y[0] for x, y in zip(b, b[1:]))
+    assert max(e - s for s, e in b) - min(e - s for s, e in b) <= 1
+
+
+def test_batch_split_range_keeps_padding():
+    """A shard keeps the parent's padded sizes and renumbers its edges from 0 (host-only check on
+    CPU tensors)."""
+    pairs = synth.make_batch(3, 5, [20, 24, 18, 24, 22], n2=[24, 19, 24, 21, 24])
+    bt = DeviceBatch.from_pairs(pairs, torch.device("cpu"))
+    sub = bt.split_range(1, 4)
+    assert sub.B == 3 and sub.nmax == bt.nmax and sub.pair_range == (1, 4)
+    for side in range(2):
+        e0 = int(bt.edge_off[side][1])
+        e1 = int(bt.edge_off[side][4])
+        nm = bt.nmax[side]
+        assert torch.equal(sub.src[side], bt.src[side][e0:e1] - nm)
+        assert torch.equal(sub.x[side], bt.x[side][nm:4 * nm])
+    with pytest.raises(ValueError):
+        bt.split_range(3, 3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,devices", [("bf16", [0, 0]), ("f32", [0, 0, 0])])
+def test_sharded_equals_single_device(dtype, devices):
+    sd = params.init_params(7)
+    pairs = synth.make_batch(41, 7, [48, 40, 44, 48, 30, 48, 47], n2=[48, 48, 44, 41, 48, 36, 48])
+    net = fpm.Net(regression=True, dtype=dtype, backbone=False)
+    net.load_state_dict(sd)
+    bt = DeviceBatch.from_pairs(pairs, DEV)
+    ref = net.run(bt)
+    sh = ShardedNet(net, devices=devices)
+    out = sh.run(bt)
+    for k in ("s", "ss", "ds_mat", "perm_mat", "k_prob", "cls_prob"):
+        assert out[k].device == DEV
+        assert torch.equal(out[k], ref[k]), k
+    assert float(out["ks_loss"]) == pytest.approx(float(ref["ks_loss"]), abs=1e-7)
+    assert len(sh.last_timing["bounds"]) == len(devices)
+
+
+@pytest.mark.gpu
+def test_sharded_forward_data_dict():
+    """The reference call shape: ShardedNet(net)(data_dict) -> data_dict with the reference keys,
+    equal to Net(data_dict) (gt_perm_mat / label sliced per shard, losses over the whole batch)."""
+    sd = params.init_params(5)
+    pairs = synth.make_batch(42, 5, 40, n2=[40, 33, 40, 38, 40])
+    B = len(pairs)
+
+    def dd():
+        d = {"ns": [torch.tensor([p[s]["n"] for p in pairs]) for s in range(2)], "pyg_graphs": [],
+             "node_features": [], "global_features": []}
+
+        class G:
+            pass
+        for side in range(2):
+            g = G()
+            offs = np.cumsum([0] + [p[side]["n"] for p in pairs])
+            g.edge_index = torch.from_numpy(np.concatenate([p[side]["edge_index"] + offs[b]
+                                                            for b, p in enumerate(pairs)], 1))
+            g.edge_attr = torch.from_numpy(np.concatenate([p[side]["pseudo"] for p in pairs]))
+            g.ptr = torch.from_numpy(offs)
+            d["pyg_graphs"].append(g)
+            d["node_features"].append(torch.from_numpy(np.concatenate([p[side]["x"] for p in pairs])))
+            d["global_features"].append(torch.from_numpy(np.stack([p[side]["w"] for p in pairs])))
+        gt = torch.zeros(B, 40, 40)
+        for b in range(B):
+            m = min(pairs[b][0]["n"], pairs[b][1]["n"])
+            gt[b, range(m), range(m)] = 1
+        d["gt_perm_mat"] = gt
+        d["label"] = torch.tensor([1.0, 0.0, 1.0, 1.0, 0.0])
+        return d
+
+    net = fpm.Net(regression=True, backbone=False)
+    net.load_state_dict(sd)
+    ref = net(dd())
+    out = ShardedNet(net, devices=[0, 0])(dd())
+    for k in ("ds_mat", "perm_mat", "k_prob", "cls_prob"):
+        assert torch.equal(out[k], ref[k]), k
+    for k in ("ks_loss", "ks_error", "cls_loss"):
+        assert float(out[k]) == pytest.approx(float(ref[k]), rel=1e-6, abs=1e-7), k

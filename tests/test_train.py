@@ -86,7 +86,7 @@ def test_soft_topk_bwd_vs_autograd(n1s, n2s, kf):
     out = O.soft_topk(sl, k, n1s, n2s, 10, 0.01)
     (out * dd).sum().backward()
     steps = torch.empty(B, dtype=torch.int32, device=DEV)
-    ops.soft_topk(ss32.to(DEV), _i32(n1s), _i32(n2s), k.float().to(DEV), 10, 0.01, steps=steps)
+    ops.soft_topk_fwd(ss32.to(DEV), _i32(n1s), _i32(n2s), k.float().to(DEV), 10, 0.01, steps=steps)
     dss = ops.soft_topk_bwd(ss32.to(DEV), _i32(n1s), _i32(n2s), k.float().to(DEV), steps, 0.01, dd.float().to(DEV))
     assert _rel(dss, sl.grad) < 1e-3
 
@@ -103,7 +103,7 @@ def test_soft_topk_bwd_tied_anchors():
     sl = ss.float().double().clone().requires_grad_(True)
     (O.soft_topk(sl, k, [n], [n], 10, 0.01) * dd).sum().backward()
     steps = torch.empty(1, dtype=torch.int32, device=DEV)
-    ops.soft_topk(ss.float().to(DEV), _i32([n]), _i32([n]), k.float().to(DEV), 10, 0.01, steps=steps)
+    ops.soft_topk_fwd(ss.float().to(DEV), _i32([n]), _i32([n]), k.float().to(DEV), 10, 0.01, steps=steps)
     dss = ops.soft_topk_bwd(ss.float().to(DEV), _i32([n]), _i32([n]), k.float().to(DEV), steps, 0.01,
                             dd.float().to(DEV))
     assert _rel(dss, sl.grad) < 1e-3
@@ -229,7 +229,7 @@ def _gt(pairs):
 
 def _train_step_compare(pairs, sd, labels):
     gt, n1, n2 = _gt(pairs)
-    net = fpm.Net(regression=True, dtype="f32")
+    net = fpm.Net(regression=True, backbone=False, dtype="f32")
     net.load_state_dict(sd)
     net.to(DEV).train()
     bt = DeviceBatch.from_pairs(pairs, DEV)
@@ -337,7 +337,7 @@ def test_train_step_bf16_finite(sd):
     """bf16 operand mode: the step runs and every gradient is finite (reported, not gated)."""
     pairs = synth.make_batch(23, 2, 48)
     gt, n1, n2 = _gt(pairs)
-    net = fpm.Net(regression=True, dtype="bf16")
+    net = fpm.Net(regression=True, backbone=False, dtype="bf16")
     net.load_state_dict(sd)
     net.to(DEV).train()
     out = net({"fpm_batch": DeviceBatch.from_pairs(pairs, DEV), "gt_perm_mat": gt, "label": torch.ones(2)})

@@ -13,7 +13,7 @@ from fpm.batch import DeviceBatch  # noqa: E402
 B, n = int(os.environ.get("B", 128)), int(os.environ.get("N", 256))
 dev = torch.device("cuda", 0)
 bt = DeviceBatch.from_pairs(synth.make_batch(3, B, n), dev)
-wp = fpm.Net(regression=True, dtype="bf16").packed(dev)
+wp = fpm.Net(regression=True, backbone=False, dtype="bf16").packed(dev)
 plans = [ops.spline_plan(bt.src[s], bt.dst[s], bt.pseudo[s], B * n, n) for s in range(2)]
 csr = [ops.plan_csr(plans[s], bt.E[s], B * n) for s in range(2)]
 C = int(os.environ.get("C", 17))

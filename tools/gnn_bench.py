@@ -14,7 +14,7 @@ B, n = int(os.environ.get("B", 128)), int(os.environ.get("N", 256))
 dev = torch.device("cuda", 0)
 pairs = synth.make_batch(3, B, n)
 bt = DeviceBatch.from_pairs(pairs, dev)
-net = fpm.Net(regression=True, dtype="bf16")
+net = fpm.Net(regression=True, backbone=False, dtype="bf16")
 wp = net.packed(dev)
 plans = [ops.spline_plan(bt.src[s], bt.dst[s], bt.pseudo[s], B * n, n) for s in range(2)]
 csr = [ops.plan_csr(plans[s], bt.E[s], B * n) for s in range(2)]

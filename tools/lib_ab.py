@@ -21,7 +21,7 @@ if sys.argv[1] != "-":
 dev = torch.device("cuda", 0)
 B, n = 128, 256
 bt = DeviceBatch.from_pairs(synth.make_batch(5, B, n), dev)
-net = fpm.Net(regression=True, dtype="bf16")
+net = fpm.Net(regression=True, backbone=False, dtype="bf16")
 net.load_state_dict(params.init_params(0))
 g = torch.Generator(device="cpu").manual_seed(3)
 ss = torch.rand(B, n, n, generator=g) ** 6

@@ -10,7 +10,7 @@ from fpm.batch import DeviceBatch
 dev = torch.device("cuda", 0)
 n = int(os.environ.get("N", "256"))
 B = int(os.environ.get("B", "256"))
-net = fpm.Net(regression=True, dtype="bf16", lsa="host")
+net = fpm.Net(regression=True, backbone=False, dtype="bf16", lsa="host")
 net.load_state_dict(params.init_params(0))
 bt = DeviceBatch.from_pairs(synth.make_batch(0, B, n), dev)
 ds = net.run(bt)["ds_mat"].contiguous()

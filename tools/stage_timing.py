@@ -11,7 +11,7 @@ import torch, fpm
 from fpm import params
 from fpm.batch import DeviceBatch
 dev = torch.device("cuda", 0)
-net = fpm.Net(regression=True, dtype=dt)
+net = fpm.Net(regression=True, backbone=False, dtype=dt)
 net.load_state_dict(params.init_params(0))
 bt = DeviceBatch.from_pairs(pairs, dev)
 log("on device")

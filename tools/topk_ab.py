@@ -19,12 +19,12 @@ res = {}
 for fast in (0, 1, 0, 1):
     prev = ops.set_tuning("topk_fast", fast)
     steps = torch.empty(B, dtype=torch.int32, device=dev)
-    out = ops.soft_topk(ss, nn_, nn_, k, 10, 0.01, steps=steps)
+    out = ops.soft_topk_fwd(ss, nn_, nn_, k, 10, 0.01, steps=steps)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(10):
-        ops.soft_topk(ss, nn_, nn_, k, 10, 0.01, out=out, steps=steps)
+        ops.soft_topk_fwd(ss, nn_, nn_, k, 10, 0.01, out=out, steps=steps)
     e1.record()
     torch.cuda.synchronize()
     res[fast] = (out.cpu(), steps.cpu())

@@ -40,7 +40,7 @@ def main():
     gt = torch.zeros(B, n, n, device=dev)
     gt[:, torch.arange(n), torch.arange(n)] = 1.0
     label = (torch.arange(B, device=dev) % 2).float()
-    net = fpm.Net(regression=True, dtype=args.dtype)
+    net = fpm.Net(regression=True, backbone=False, dtype=args.dtype)
     net.load_state_dict(sd)
     net.to(dev).train()
     opt = torch.optim.AdamW([p for p in net.parameters() if p.requires_grad], lr=1e-4, weight_decay=1e-4)
