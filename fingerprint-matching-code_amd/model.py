@@ -537,7 +537,7 @@ class Net(nn.Module):
         outs, events = [], []
         for c, part in enumerate(parts):
             st = streams[c % len(streams)]
-            b0, b1 = getattr(part, "pair_range", (0, B))
+            b0, b1 = (0, B) if part is bt else part.pair_range     # a chunk's range inside bt
             with torch.cuda.stream(st):
                 r, ev = self._stage_a(part, b0, b1, o, keep_feats, gt_ks, min_pt, st, gc)
             outs.append(r)
@@ -547,7 +547,7 @@ class Net(nn.Module):
         for c, (part, ev) in enumerate(zip(parts, events)):
             if device_lsa:
                 break
-            b0, b1 = getattr(part, "pair_range", (0, B))
+            b0, b1 = (0, B) if part is bt else part.pair_range     # a chunk's range inside bt
             ev.synchronize()
             t_first = t_first or time.perf_counter()
             with torch.cuda.stream(streams[c % len(streams)]):

@@ -29,6 +29,12 @@ def _dev(*ts):
             raise _lib.FpmError("fpm op called with a CPU tensor: the HIP path has no CPU fallback")
 
 
+def _shape(t, shape, what):
+    """Host-side operand check before a launch: ``t`` must cover ``shape`` exactly."""
+    if t is not None and tuple(t.shape) != tuple(int(x) for x in shape):
+        raise _lib.FpmError("%s: tensor of shape %s where %s is required" % (what, tuple(t.shape), tuple(shape)))
+
+
 def _code(t):
     if t.dtype == torch.float32:
         return F32
@@ -46,6 +52,9 @@ def sinkhorn(s, n1, n2, iters, tau, dummy_row=True, out=None, n1max=None, n2max=
     n2max = n2max or s.shape[2]
     if out is None:
         out = torch.empty(B, n1max, n2max, device=s.device, dtype=torch.float32)
+    _shape(out, (B, n1max, n2max), "sinkhorn out")
+    _shape(n1, (B,), "sinkhorn n1")
+    _shape(n2, (B,), "sinkhorn n2")
     _lib.call("fpm_sinkhorn_log_fwd", _p(s), s.stride(0), s.stride(1), s.stride(2), _p(out), out.stride(0),
               out.stride(1), out.stride(2), _p(n1), _p(n2), B, n1max, n2max, int(iters), float(tau),
               int(bool(dummy_row)), _stream(s))
@@ -59,6 +68,9 @@ def soft_topk_fwd(ss, n1, n2, k, iters=10, tau=0.01, out=None, steps=None, out_h
     B, n1max, n2max = ss.shape
     if out is None:
         out = torch.empty(B, n1max, n2max, device=ss.device, dtype=torch.float32)
+    _shape(out, (B, n1max, n2max), "soft_topk out")
+    for t, w in ((n1, "n1"), (n2, "n2"), (k, "k"), (steps, "steps")):
+        _shape(t, (B,), "soft_topk " + w)
     if out_host is not None and (out_host.is_cuda or not out_host.is_pinned() or tuple(out_host.shape) != (B, n1max, n2max)):
         raise _lib.FpmError("soft_topk: out_host must be a pinned host tensor of shape (B, n1max, n2max)")
     _lib.call("fpm_soft_topk_fwd", _p(ss), ss.stride(0), ss.stride(1), _p(n1), _p(n2), _p(k), B, n1max, n2max,
@@ -71,6 +83,10 @@ def soft_topk_fwd(ss, n1, n2, k, iters=10, tau=0.01, out=None, steps=None, out_h
 def topk_select(ds, assign, k, lsa_out=None, out=None):
     _dev(ds, assign, k)
     B, n1max, n2max = ds.shape
+    _shape(assign, (B, n1max), "topk_select assign")
+    _shape(k, (B,), "topk_select k")
+    _shape(out, (B, n1max, n2max), "topk_select out")
+    _shape(lsa_out, (B, n1max, n2max), "topk_select lsa_out")
     perm = out if out is not None else torch.empty(B, n1max, n2max, device=ds.device, dtype=torch.float32)
     _lib.call("fpm_topk_select", _p(ds), ds.stride(0), ds.stride(1), _p(assign), assign.stride(0), _p(k), B,
               n1max, n2max, _p(perm), perm.stride(0), perm.stride(1), _p(lsa_out),
@@ -170,6 +186,10 @@ def edge_diff_padded(x, src, dst, pair, row, nrows, cscale=None):
 
 def gnn_layer(X, C, B, n1max, n2max, csr1, csr2, n1, n2, params, Xout, zbuf, vpart=None, cls_w=None):
     _dev(X, n1, n2, params, Xout, zbuf, vpart, cls_w)
+    _shape(X, (B, C, n2max, n1max), "gnn_layer X")
+    _shape(Xout, (B, 17, n2max, n1max), "gnn_layer Xout")
+    _shape(zbuf, (B, n2max, n1max), "gnn_layer zbuf")
+    _shape(vpart, (B, n2max, n1max), "gnn_layer vpart")
     _lib.call("fpm_kron_gnn_layer_fwd", _p(X), C, B, n1max, n2max, ctypes.c_void_p(csr1[0]),
               ctypes.c_void_p(csr1[1]), ctypes.c_void_p(csr2[0]), ctypes.c_void_p(csr2[1]), _p(n1), _p(n2),
               _p(params), _p(Xout), _p(zbuf), _p(vpart), _p(cls_w), _stream(X))
@@ -177,6 +197,9 @@ def gnn_layer(X, C, B, n1max, n2max, csr1, csr2, n1, n2, params, Xout, zbuf, vpa
 
 def node_classifier(X, B, n1max, n2max, w, b, out, vpart=None):
     _dev(X, w, b, out, vpart)
+    _shape(X, (B, 17, n2max, n1max), "node_classifier X")
+    _shape(out, (B, n1max, n2max), "node_classifier out")
+    _shape(vpart, (B, n2max, n1max), "node_classifier vpart")
     _lib.call("fpm_node_classifier", _p(X), B, n1max, n2max, _p(w), _p(b), _p(vpart), _p(out), _stream(X))
 
 

@@ -450,7 +450,11 @@ def forward(pairs, sd, regression=True, training=False, gt_perm=None, labels=Non
     k_used = gt_ks.view(-1) if training else ks.view(-1) * min_pt
     ds = soft_topk(ss, k_used, n1, n2, SK_ITER, TAU)
     x = hungarian(ds, n1, n2).to(dtype)
-    top = torch.argsort(x.mul(ds).reshape(B, -1), descending=True, dim=-1)
+    # ngm.py:445-447 sorts with torch's unstable argsort; soft top-k probabilities saturate at exactly
+    # 1.0, so several matches tie and the reference's pick among them is sort-implementation defined
+    # (quirk A.10(v)).  The oracle fixes that order to ascending flat index (a stable sort), the
+    # order the HIP selector uses, so perm_mat parity is checked on one well-defined instance.
+    top = torch.argsort(x.mul(ds).reshape(B, -1), descending=True, dim=-1, stable=True)
     perm = greedy_perm(torch.zeros_like(ds), top, ks.view(-1) * min_pt)
     logits = match_classifier(s * perm, sd, training=training)
     cls_prob = torch.sigmoid(logits)

@@ -76,8 +76,14 @@ def test_greedy_perm_mirror_respects_initial_x():
 
 @pytest.mark.gpu
 def test_soft_topk_mirror_golden():
-    """soft_topk(scores, ks, max_iter, tau, nrows, ncols, return_prob=True) -> (x, soft) equal to the
-    reference's outputs (golden; c1 has ragged pairs)."""
+    """soft_topk(scores, ks, max_iter, tau, nrows, ncols, return_prob=True) -> (x, soft): the soft
+    matrix equals the reference's (golden; c1 has ragged pairs).  Its hard x is a greedy walk over an
+    argsort of the soft matrix, whose top entries saturate at exactly 1.0 (7-26 tied entries per
+    pair in these cases), so which tied entries the reference picks depends on torch's unstable CPU
+    sort order (quirk A.10(v); tools/soft_topk_hard_check.py).  Checked instead: x is a partial
+    permutation with the reference's match count, and the soft values it selects equal the
+    reference's selection value for value.  The walk itself is pinned exactly by
+    test_greedy_perm_mirror_golden (reference order given)."""
     z = np.load(os.path.join(GOLDEN, "soft_topk.npz"))
     for i in range(int(z["ncases"])):
         g = lambda k: z["c%d_%s" % (i, k)]
@@ -85,7 +91,11 @@ def test_soft_topk_mirror_golden():
         x, ss = ops.soft_topk(sc, torch.from_numpy(g("ks")).to(DEV), 10, 0.01, torch.from_numpy(g("n1")),
                               torch.from_numpy(g("n2")), True)
         np.testing.assert_allclose(ss.cpu().numpy(), g("ss_out"), atol=1e-5, rtol=0)
-        np.testing.assert_array_equal(x.cpu().numpy(), g("x"))
+        xr, xh, sref = g("x"), x.cpu().numpy(), g("ss_out")
+        for b in range(xr.shape[0]):
+            assert xh[b].sum() == xr[b].sum()
+            assert xh[b].sum(0).max() <= 1 and xh[b].sum(1).max() <= 1
+            np.testing.assert_allclose(np.sort(sref[b][xh[b] > 0]), np.sort(sref[b][xr[b] > 0]), atol=1e-6)
         x_only = ops.soft_topk(sc, torch.from_numpy(g("ks")).to(DEV), 10, 0.01, torch.from_numpy(g("n1")),
                                torch.from_numpy(g("n2")))
         assert torch.equal(x_only, x)
