@@ -94,6 +94,17 @@ def cpu_baseline(n, npairs, seed, sd):
             "sample": "%d pairs, n=%d, fp32 oracle forward incl. scipy Hungarian (1 process)" % (npairs, n)}, pairs, ref
 
 
+def tie_equivalent(P, R, ds, tol=1e-5):
+    """perm_mat P selects as many matches as the oracle's R, and the oracle's ds_mat values at P's
+    matches equal those at R's (sorted, within ``tol``): P differs from R only by a different pick
+    among (near-)tied entries -- P(top-k) saturates at 1.0, where the reference's own argsort order
+    is implementation defined (quirk A.10(v))."""
+    import torch
+    a, b = ds[P > 0], ds[R > 0]
+    return a.numel() == b.numel() and bool((torch.sort(a).values - torch.sort(b).values).abs().max() <= tol
+                                          if a.numel() else True)
+
+
 def parity_vs_oracle(pairs, ref, sd, dev, dtypes):
     """The GPU forward (each compute mode) on the CPU baseline's own sample, against the oracle's
     outputs for it: max|d| per output and perm_mat agreement (SURVEY §8(d) parity gate: fp32 gated
@@ -112,6 +123,8 @@ def parity_vs_oracle(pairs, ref, sd, dev, dtypes):
         d["perm_entries_agree"] = float((P == R).float().mean())
         d["perm_matches_kept"] = float((P * R).sum() / R.sum().clamp(min=1))
         d["perm_pairs_identical"] = float(np.mean([torch.equal(P[b], R[b]) for b in range(P.shape[0])]))
+        d["perm_pairs_tie_equivalent"] = float(np.mean([tie_equivalent(P[b], R[b], ref["ds_mat"][b])
+                                                        for b in range(P.shape[0])]))
         out[dt] = d
     out["pairs"] = len(pairs)
     return out

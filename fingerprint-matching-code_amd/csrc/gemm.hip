@@ -117,6 +117,45 @@ extern "C" int fpm_cast_bf16(const float* x, void* y, long n, void* stream) {
     return fpm::check_launch("fpm_cast_bf16");
 }
 
+// Global weights of each pair, normalize_over_channels(cat(w1[b], w2[b])) (ngm.py:65-67, 262-268):
+// one 256-thread workgroup per pair; the sum of squares is reduced in a fixed order (per-thread
+// strided partials, then a fixed LDS tree), so a pair's result does not depend on how many pairs
+// share the launch -- a shard or a pipeline chunk computed alone reproduces its slice exactly.
+namespace {
+__global__ __launch_bounds__(256) void global_weights_kernel(const float* __restrict__ w1, long ld1,
+                                                             const float* __restrict__ w2, long ld2, int D1, int D2,
+                                                             float* __restrict__ out, long ldo) {
+    __shared__ float red[256];
+    const int b = blockIdx.x, t = threadIdx.x;
+    const float* a = w1 + (long)b * ld1;
+    const float* c = w2 + (long)b * ld2;
+    float acc = 0.f;
+    for (int i = t; i < D1 + D2; i += 256) {
+        const float v = i < D1 ? a[i] : c[i - D1];
+        acc = fmaf(v, v, acc);
+    }
+    red[t] = acc;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if (t < h) red[t] += red[t + h];
+        __syncthreads();
+    }
+    const float nrm = sqrtf(red[0]);
+    float* o = out + (long)b * ldo;
+    for (int i = t; i < D1 + D2; i += 256) o[i] = (i < D1 ? a[i] : c[i - D1]) / nrm;
+}
+}  // namespace
+
+extern "C" int fpm_global_weights(const float* w1, long ld1, const float* w2, long ld2, int B, int D1, int D2,
+                                  float* out, long ldo, void* stream) {
+    FPM_CHECK_ARG(B >= 0 && D1 >= 0 && D2 >= 0 && ld1 >= D1 && ld2 >= D2 && ldo >= D1 + D2,
+                  "global_weights: bad sizes");
+    if (B == 0) return 0;
+    hipLaunchKernelGGL(global_weights_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, w1, ld1, w2, ld2, D1, D2,
+                       out, ldo);
+    return fpm::check_launch("fpm_global_weights");
+}
+
 // Device -> pinned-host copy on a few workgroups.  The runtime's blit copy for this direction
 // launches one 512-thread workgroup per CU for the whole (PCIe-bound) transfer; the transfer needs
 // only enough 16-B stores in flight, so a handful of workgroups keep the CUs for the compute

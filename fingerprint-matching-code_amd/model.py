@@ -332,8 +332,7 @@ class Net(nn.Module):
         """Global weights w = L2norm(cat(w1, w2)) and vertex-affinity coefficients c = tanh(A w + a)
         for every pair of ``bt`` (ngm.py:262-268, affinity_layer.py:13); one launch per forward."""
         wp = self.packed(bt.device)
-        gw = torch.cat([bt.w[0], bt.w[1]], dim=1)
-        gw = (gw / torch.norm(gw, dim=1, keepdim=True)).contiguous()
+        gw = ops.global_weights(bt.w[0], bt.w[1])
         coef = torch.empty(bt.B, C.NODE_FEATURE_DIM, device=bt.device, dtype=torch.float32)
         ops.gemm(gw, wp["aff_w"], bt.B, C.NODE_FEATURE_DIM, C.GLOBAL_STATE_DIM, C.GLOBAL_STATE_DIM,
                  C.GLOBAL_STATE_DIM, epi=ops.EPI_TANH, bias=wp["aff_b"], out_f=coef)

@@ -118,6 +118,22 @@ def gemm(A, B, M, N, K, lda, ldb, batch=1, sA=0, sB=0, a_rows=None, epi=EPI_STOR
               _stream(A))
 
 
+def global_weights(w1, w2, out=None):
+    """normalize_over_channels(cat(w1, w2)) per pair (ngm.py:262-268) -> (B, D1 + D2) fp32."""
+    _dev(w1, w2)
+    if w1.dtype != torch.float32 or w2.dtype != torch.float32 or w1.stride(1) != 1 or w2.stride(1) != 1:
+        raise _lib.FpmError("global_weights: float32 rows with unit stride expected")
+    B, D1 = w1.shape
+    D2 = w2.shape[1]
+    _shape(w2, (B, D2), "global_weights w2")
+    if out is None:
+        out = torch.empty(B, D1 + D2, device=w1.device, dtype=torch.float32)
+    _shape(out, (B, D1 + D2), "global_weights out")
+    _lib.call("fpm_global_weights", _p(w1), w1.stride(0), _p(w2), w2.stride(0), B, D1, D2, _p(out), out.stride(0),
+              _stream(w1))
+    return out
+
+
 def cast_bf16(x, out=None):
     _dev(x)
     if out is None:

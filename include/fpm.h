@@ -61,6 +61,12 @@ int fpm_topk_select(const float* ds, long d_sb, long d_ld, const int* assign, lo
 int fpm_greedy_perm(const long* top_idx, long t_sb, int T, const float* k, int B, int n1max, int n2max, float* x,
                     long x_sb, long x_ld, void* stream);
 
+/* ---- global weights ---------------------------------------------------------------------------
+ * Replaces normalize_over_channels(cat(global_src, global_tgt)) (src/model/ngm.py:65-67, 262-268):
+ * out[b] = cat(w1[b], w2[b]) / ||cat(w1[b], w2[b])||_2, reduced in a fixed per-pair order. */
+int fpm_global_weights(const float* w1, long ld1, const float* w2, long ld2, int B, int D1, int D2, float* out,
+                       long ldo, void* stream);
+
 /* ---- generic MFMA GEMM with fused epilogue ----------------------------------------------------
  * C[b][r][n] = epi(sum_k A[b][row(r)][k] * B[b][n][k] (+ bias[n])), row(r) = a_rows ? a_rows[r] : r.
  * epi: 0 store, 1 relu, 2 tanh, 3 affinity (softplus(v) - 0.5 inside [:n2[b], :n1[b]], else 0).

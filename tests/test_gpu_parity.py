@@ -217,6 +217,11 @@ def fidelity_stats(res, ref):
     d["perm_entries_agree"] = float((P == R).float().mean())
     d["perm_matches_kept"] = float((P * R).sum() / R.sum().clamp(min=1))
     d["perm_pairs_identical"] = float(np.mean([torch.equal(P[b], R[b]) for b in range(P.shape[0])]))
+    # same count and the oracle's ds_mat values at the picks equal: differs only among (near-)ties
+    d["perm_pairs_tie_equivalent"] = float(np.mean([
+        int((P[b] > 0).sum()) == int((R[b] > 0).sum()) and
+        bool(((torch.sort(ref["ds_mat"][b][P[b] > 0]).values - torch.sort(ref["ds_mat"][b][R[b] > 0]).values).abs()
+              .max() <= 1e-5) if int((R[b] > 0).sum()) else True) for b in range(P.shape[0])]))
     return d
 
 
@@ -591,3 +596,14 @@ def test_copy_async_to_pinned():
     ops.copy_async(h, x, 8)
     torch.cuda.synchronize()
     assert torch.equal(h, x.cpu())
+
+
+def test_global_weights_kernel():
+    """normalize_over_channels(cat(w1, w2)) (ngm.py:65-67, 262-268): within 1e-6 of the oracle, and a
+    pair's row does not depend on how many pairs share the launch (shards / chunks computed alone)."""
+    g = torch.Generator().manual_seed(31)
+    w1, w2 = torch.rand(7, 512, generator=g), torch.rand(7, 512, generator=g) * 3
+    full = ops.global_weights(w1.to(DEV), w2.to(DEV))
+    assert (full.cpu() - O.global_weights(w1, w2)).abs().max() < 1e-6
+    part = ops.global_weights(w1[2:5].to(DEV), w2[2:5].to(DEV))
+    assert torch.equal(part, full[2:5])
