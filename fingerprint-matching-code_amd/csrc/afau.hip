@@ -40,7 +40,9 @@ struct AfSmem {
     float traw[256], tsort[256];
 };
 
-template <typename T, int TJ>
+// SPLIT (T = bf16): each output row is [hi | lo | hi] (3 x 256 bf16, hi = bf16(o), lo = bf16(o - hi)),
+// the split operand of the near-fp32 combine product (weights packed [W_hi | W_hi | W_lo]).
+template <typename T, int TJ, bool SPLIT = false>
 __global__ __launch_bounds__(256) void afau_row_attn_kernel(const float* __restrict__ cost, long c_sb, long c_ld,
                                                             int n1max, int n2max, const int* __restrict__ n2,
                                                             const float* __restrict__ Wv, int emb,
@@ -186,7 +188,18 @@ __global__ __launch_bounds__(256) void afau_row_attn_kernel(const float* __restr
                 sum = fmaf(ms.y, sc, sum);
                 o = fmaf(S.part[buf][w][tid], sc, o);
             }
-            if (ii < n1max) out[((long)b * n1max + ii) * 256 + h * 16 + d] = fpm::from_f<T>(o / sum);
+            if (ii < n1max) {
+                const float v = o / sum;
+                if constexpr (SPLIT) {
+                    T* orow = out + ((long)b * n1max + ii) * 768 + h * 16 + d;
+                    const bf16_t hi = fpm::f2bf(v);
+                    orow[0] = hi;
+                    orow[256] = fpm::f2bf(v - fpm::bf2f(hi));
+                    orow[512] = hi;
+                } else {
+                    out[((long)b * n1max + ii) * 256 + h * 16 + d] = fpm::from_f<T>(v);
+                }
+            }
         }
     }
 }
@@ -321,11 +334,12 @@ extern "C" int fpm_crossset_attn_fwd(int dtype, const float* cost, long c_sb, lo
     // fp32 (parity) mode scores with the 16-term sum (the reference's operation order); the LUT is
     // the bf16 throughput mode's (env FPM_AFAU_LUT / fpm_set_tuning("afau_lut") override)
     const int lut = afau_lut_flag() != 2 ? afau_lut_flag() : (dtype != 0);
-#define FPM_ATT(TT, TJ_)                                                                                         \
-    hipLaunchKernelGGL((afau_row_attn_kernel<TT, TJ_>), grid, dim3(256), 0, st, cost, c_sb, c_ld, n1max, n2max, n2, \
-                       Wv, emb, mix1w, mix1b, mix2w, mix2b, (TT*)out, lut)
-    if (dtype == 0) { if (n2max <= 256) FPM_ATT(float, 16); else FPM_ATT(float, 40); }
-    else { if (n2max <= 256) FPM_ATT(bf16_t, 16); else FPM_ATT(bf16_t, 40); }
+#define FPM_ATT(TT, TJ_, SP_)                                                                                    \
+    hipLaunchKernelGGL((afau_row_attn_kernel<TT, TJ_, SP_>), grid, dim3(256), 0, st, cost, c_sb, c_ld, n1max, n2max, \
+                       n2, Wv, emb, mix1w, mix1b, mix2w, mix2b, (TT*)out, lut)
+    if (dtype == 0) { if (n2max <= 256) FPM_ATT(float, 16, false); else FPM_ATT(float, 40, false); }
+    else if (dtype == 1) { if (n2max <= 256) FPM_ATT(bf16_t, 16, false); else FPM_ATT(bf16_t, 40, false); }
+    else { if (n2max <= 256) FPM_ATT(bf16_t, 16, true); else FPM_ATT(bf16_t, 40, true); }
 #undef FPM_ATT
     return fpm::check_launch("fpm_crossset_attn_fwd");
 }

@@ -156,6 +156,36 @@ extern "C" int fpm_global_weights(const float* w1, long ld1, const float* w2, lo
     return fpm::check_launch("fpm_global_weights");
 }
 
+// Split-bf16 operand rows for near-fp32 GEMMs on the bf16 MFMA path: x = hi + lo with hi = bf16(x)
+// and lo = bf16(x - hi); dst row = [hi | lo | hi] (each segment Kp wide, zero in [K, Kp)), to be
+// multiplied by weights packed as [B_hi | B_hi | B_lo] along K, which sums hi*B_hi + lo*B_hi +
+// hi*B_lo (the dropped lo*B_lo term is ~2^-16 of the product) with fp32 accumulation.
+namespace {
+__global__ __launch_bounds__(256) void split_bf16x3_kernel(const float* __restrict__ src, long lds, int K, int Kp,
+                                                           bf16_t* __restrict__ dst, long ldd) {
+    const long r = blockIdx.x;
+    const float* a = src + r * lds;
+    bf16_t* o = dst + r * ldd;
+    for (int k = threadIdx.x; k < Kp; k += 256) {
+        const float v = k < K ? a[k] : 0.f;
+        const bf16_t hi = fpm::f2bf(v);
+        const bf16_t lo = fpm::f2bf(v - fpm::bf2f(hi));
+        o[k] = hi;
+        o[Kp + k] = lo;
+        o[2 * Kp + k] = hi;
+    }
+}
+}  // namespace
+
+extern "C" int fpm_split_bf16x3(const float* src, long lds, long rows, int K, int Kp, void* dst, long ldd,
+                                void* stream) {
+    FPM_CHECK_ARG(rows >= 0 && K > 0 && Kp >= K && lds >= K && ldd >= 3L * Kp, "split_bf16x3: bad sizes");
+    if (rows == 0) return 0;
+    hipLaunchKernelGGL(split_bf16x3_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, src, lds, K, Kp,
+                       (bf16_t*)dst, ldd);
+    return fpm::check_launch("fpm_split_bf16x3");
+}
+
 // Device -> pinned-host copy on a few workgroups.  The runtime's blit copy for this direction
 // launches one 512-thread workgroup per CU for the whole (PCIe-bound) transfer; the transfer needs
 // only enough 16-B stores in flight, so a handful of workgroups keep the CUs for the compute

@@ -93,6 +93,14 @@ class Net(nn.Module):
         if dtype not in ("f32", "bf16"):
             raise ValueError("dtype must be 'f32' or 'bf16'")
         self.dtype_mode = dtype
+        # AFA-U operands in the bf16 mode (FPM_AFAU_DTYPE): "bf16s" (default) keeps the attention
+        # output as split bf16 hi + lo terms for the multi-head combine product and runs the FFN on
+        # bf16; "bf16" rounds the attention output to bf16 (k_prob 8e-3 from the fp32 oracle at C3
+        # vs 8e-4, perm_mat tie-equivalent on 1-2 of 8 vs 7 of 8 pairs, 1 % faster); "bf16x3" /
+        # "f32" every AFA-U product near-fp32 / fp32 (15-19 % slower end to end).
+        self.afau_mode = "f32" if dtype == "f32" else os.environ.get("FPM_AFAU_DTYPE", "bf16s")
+        if self.afau_mode not in ("f32", "bf16", "bf16s", "bf16x3"):
+            raise ValueError("FPM_AFAU_DTYPE must be f32, bf16, bf16s or bf16x3")
         # Hungarian pool: 2 threads per CPU of the process's share (FPM_LSA_THREADS overrides).  Measured
         # on the 16-CPU box share: 16 / 32 / 48 threads -> 29-44 / 17-22 / 17-18 ms per 1024 pairs
         # (the pairs of a chunk differ in cost; idle stragglers at each chunk's join dominate at 1x)
@@ -130,7 +138,7 @@ class Net(nn.Module):
         return dict(self.state_dict())
 
     def _key(self, device):
-        return (str(device), self.dtype_mode, tuple(p._version for p in self.parameters()),
+        return (str(device), self.dtype_mode, self.afau_mode, tuple(p._version for p in self.parameters()),
                 tuple(b._version for b in self.buffers()))
 
     def packed(self, device):
@@ -162,6 +170,7 @@ class Net(nn.Module):
             d["gnn%d" % l] = torch.cat([t.reshape(-1).float() for t in parts]).to(device).contiguous()
         d["cls_w"] = g("classifier.weight").reshape(-1).contiguous()
         d["cls_b"] = g("classifier.bias")
+        op = torch.bfloat16 if self.afau_mode == "bf16" else torch.float32
         for blk in ("row", "col"):
             pre = "encoder_k.layers.0.%s_encoding_block" % blk
             d[blk + "_Wv"] = g(pre + ".Wv.weight")                                  # (256, 600)
@@ -169,14 +178,27 @@ class Net(nn.Module):
             d[blk + "_mix1b"] = g(pre + ".mixed_score_MHA.mix1_bias")
             d[blk + "_mix2w"] = g(pre + ".mixed_score_MHA.mix2_weight")
             d[blk + "_mix2b"] = g(pre + ".mixed_score_MHA.mix2_bias")
-            d[blk + "_Wc"] = sd[pre + ".multi_head_combine.weight"].to(device).contiguous().to(op)   # (600, 256)
-            d[blk + "_bc"] = g(pre + ".multi_head_combine.bias")
+            Wc = sd[pre + ".multi_head_combine.weight"].to(device)                                   # (600, 256)
             W1 = sd[pre + ".feed_forward.W1.weight"].to(device)                                      # (256, 600)
-            if op == torch.bfloat16:      # K padded with zeros to the 256-row kernel's BK multiple
-                W1 = F.pad(W1, (0, C.AFAU_EMB_PAD - C.AFAU_EMB))
-            d[blk + "_W1"] = W1.contiguous().to(op)
+            W2 = sd[pre + ".feed_forward.W2.weight"].to(device)                                      # (600, 256)
+            if self.afau_mode == "bf16s":
+                # the combine product on split operands ([W_hi | W_hi | W_lo]); FFN plain bf16
+                d[blk + "_Wc"] = ops.split_weights_bf16x3(Wc, C.AFAU_HEADS * C.AFAU_QKV)
+                d[blk + "_W1"] = F.pad(W1, (0, C.AFAU_EMB_PAD - C.AFAU_EMB)).contiguous().to(torch.bfloat16)
+                d[blk + "_W2"] = W2.contiguous().to(torch.bfloat16)
+            elif self.afau_mode == "bf16x3":
+                # [W_hi | W_hi | W_lo] along K for the split-bf16 operands (ops.split_bf16x3)
+                d[blk + "_Wc"] = ops.split_weights_bf16x3(Wc, C.AFAU_HEADS * C.AFAU_QKV)
+                d[blk + "_W1"] = ops.split_weights_bf16x3(W1, C.AFAU_EMB_PAD)
+                d[blk + "_W2"] = ops.split_weights_bf16x3(W2, C.AFAU_FF)
+            else:
+                if op == torch.bfloat16:      # K padded with zeros to the 256-row kernel's BK multiple
+                    W1 = F.pad(W1, (0, C.AFAU_EMB_PAD - C.AFAU_EMB))
+                d[blk + "_Wc"] = Wc.contiguous().to(op)
+                d[blk + "_W1"] = W1.contiguous().to(op)
+                d[blk + "_W2"] = W2.contiguous().to(op)
+            d[blk + "_bc"] = g(pre + ".multi_head_combine.bias")
             d[blk + "_b1"] = g(pre + ".feed_forward.W1.bias")
-            d[blk + "_W2"] = sd[pre + ".feed_forward.W2.weight"].to(device).contiguous().to(op)      # (600, 256)
             d[blk + "_b2"] = g(pre + ".feed_forward.W2.bias")
             for k in (1, 2):
                 d["%s_n%dw" % (blk, k)] = g(pre + ".add_n_normalization_%d.norm.weight" % k)
@@ -245,15 +267,27 @@ class Net(nn.Module):
         """AFA-U k regression (ngm.py:386-412) -> ks (B,)."""
         dev = ss.device
         B, n1max, n2max = bt.B, bt.n1max, bt.n2max
-        op = torch.bfloat16 if self.dtype_mode == "bf16" else torch.float32
+        # f32 / bf16x3: fp32 activations; bf16 / bf16s: bf16 FFN operands
+        op = torch.bfloat16 if self.afau_mode in ("bf16", "bf16s") else torch.float32
         E, HD, FF = C.AFAU_EMB, C.AFAU_HEADS * C.AFAU_QKV, C.AFAU_FF
         if max(n1max, n2max) > self.univ_size:
             raise AssertionError("UNIV_SIZE cap: n1max/n2max must be <= %d (ngm.py:387-389)" % self.univ_size)
-        att = torch.empty(B * n1max, HD, device=dev, dtype=op)
+        x3 = self.afau_mode == "bf16x3"          # near-fp32 products on bf16 MFMA (split operands)
+        split = self.afau_mode == "bf16s"        # the combine product alone on split operands
+        att = torch.empty(B * n1max, 3 * HD if split else HD, device=dev,
+                          dtype=torch.bfloat16 if split else op)
         ops.crossset_attn(ss, bt.n2, wp["row_Wv"], wp["row_mix1w"], wp["row_mix1b"], wp["row_mix2w"],
-                          wp["row_mix2b"], att)
+                          wp["row_mix2b"], att, split=split)
         mh = torch.empty(B * n1max, E, device=dev, dtype=torch.float32)
-        ops.gemm(att, wp["row_Wc"], B * n1max, E, HD, HD, HD, bias=wp["row_bc"], out_f=mh, ldc=E)
+        # diagnostic: FPM_AFAU_X3_MASK selects which of (combine, W1, W2) use the three split terms;
+        # the others multiply the hi parts only (plain bf16 products)
+        mask = int(os.environ.get("FPM_AFAU_X3_MASK", "7"))
+        kx = lambda bit, kp: 3 * kp if mask & bit else kp
+        if x3:
+            att = ops.split_bf16x3(att, HD)
+        # bf16s: hi*W_hi + lo*W_hi (2 terms; the W_lo term changed nothing measurable, +0.7 % time)
+        kc = int(os.environ.get("FPM_AFAU_SPLIT_TERMS", "2")) * HD if split else (kx(1, HD) if x3 else HD)
+        ops.gemm(att, wp["row_Wc"], B * n1max, E, kc, att.shape[1], att.shape[1], bias=wp["row_bc"], out_f=mh, ldc=E)
         gmax = {}
         # The column block sees a = one-hot rows and b = zero rows, so k = v = 0 and its attention
         # output is exactly the combine bias (afau.py:99-142): its result depends on n2 (and the
@@ -276,12 +310,21 @@ class Net(nn.Module):
             else:
                 ops.instnorm(None, Bu, P_, E, wp["col_n1w"], wp["col_n1b"], nvalid=n2u_d, onehot_bias=wp["col_bc"],
                              out_f=o1f, out_t=None if op == torch.float32 else o1t, ldt=KE)
-            hbuf = torch.empty(rows, FF, device=dev, dtype=op)
-            ops.gemm(o1t, wp[blk + "_W1"], rows, FF, KE, KE, KE, epi=ops.EPI_RELU, bias=wp[blk + "_b1"],
-                     out_t=hbuf if op != torch.float32 else None, out_f=hbuf if op == torch.float32 else None,
-                     ldc=FF)
             ff = torch.empty(rows, E, device=dev, dtype=torch.float32)
-            ops.gemm(hbuf, wp[blk + "_W2"], rows, E, FF, FF, FF, bias=wp[blk + "_b2"], out_f=ff, ldc=E)
+            if x3:
+                o13 = ops.split_bf16x3(o1f, C.AFAU_EMB_PAD)
+                hf = torch.empty(rows, FF, device=dev, dtype=torch.float32)
+                ops.gemm(o13, wp[blk + "_W1"], rows, FF, kx(2, C.AFAU_EMB_PAD), o13.shape[1], o13.shape[1],
+                         epi=ops.EPI_RELU, bias=wp[blk + "_b1"], out_f=hf, ldc=FF)
+                h3 = ops.split_bf16x3(hf, FF)
+                ops.gemm(h3, wp[blk + "_W2"], rows, E, kx(4, FF), h3.shape[1], h3.shape[1], bias=wp[blk + "_b2"],
+                         out_f=ff, ldc=E)
+            else:
+                hbuf = torch.empty(rows, FF, device=dev, dtype=op)
+                ops.gemm(o1t, wp[blk + "_W1"], rows, FF, KE, KE, KE, epi=ops.EPI_RELU, bias=wp[blk + "_b1"],
+                         out_t=hbuf if op != torch.float32 else None, out_f=hbuf if op == torch.float32 else None,
+                         ldc=FF)
+                ops.gemm(hbuf, wp[blk + "_W2"], rows, E, FF, FF, FF, bias=wp[blk + "_b2"], out_f=ff, ldc=E)
             gm = torch.empty(nb_, E, device=dev, dtype=torch.float32)
             ops.instnorm(o1f, nb_, P_, E, wp[blk + "_n2w"], wp[blk + "_n2b"], in2=ff, gmax=gm)
             if blk == "col" and Bu != B:

@@ -134,6 +134,28 @@ def global_weights(w1, w2, out=None):
     return out
 
 
+def split_bf16x3(x, Kp, out=None):
+    """(rows, K) fp32 rows -> (rows, 3 * Kp) bf16 [hi | lo | hi] split operands (fpm_split_bf16x3)."""
+    _dev(x)
+    if x.dtype != torch.float32 or x.dim() != 2 or x.stride(1) != 1:
+        raise _lib.FpmError("split_bf16x3: (rows, K) float32 rows with unit stride expected")
+    rows, K = x.shape
+    if out is None:
+        out = torch.empty(rows, 3 * Kp, device=x.device, dtype=torch.bfloat16)
+    _shape(out, (rows, 3 * Kp), "split_bf16x3 out")
+    _lib.call("fpm_split_bf16x3", _p(x), x.stride(0), rows, K, int(Kp), _p(out), out.stride(0), _stream(x))
+    return out
+
+
+def split_weights_bf16x3(W, Kp):
+    """(N, K) fp32 weights -> (N, 3 * Kp) bf16 [W_hi | W_hi | W_lo] (parameter packing, host side)."""
+    N, K = W.shape
+    Wp = torch.nn.functional.pad(W.float(), (0, Kp - K))
+    hi = Wp.to(torch.bfloat16)
+    lo = (Wp - hi.float()).to(torch.bfloat16)
+    return torch.cat([hi, hi, lo], dim=1).contiguous()
+
+
 def cast_bf16(x, out=None):
     _dev(x)
     if out is None:
@@ -219,10 +241,14 @@ def node_classifier(X, B, n1max, n2max, w, b, out, vpart=None):
     _lib.call("fpm_node_classifier", _p(X), B, n1max, n2max, _p(w), _p(b), _p(vpart), _p(out), _stream(X))
 
 
-def crossset_attn(cost, n2, Wv, mix1w, mix1b, mix2w, mix2b, out):
+def crossset_attn(cost, n2, Wv, mix1w, mix1b, mix2w, mix2b, out, split=False):
+    """``split``: out is (B * n1max, 768) bf16 [hi | lo | hi] rows (near-fp32 operand)."""
     _dev(cost, n2, Wv, out)
     B, n1max, n2max = cost.shape
-    _lib.call("fpm_crossset_attn_fwd", _code(out), _p(cost), cost.stride(0), cost.stride(1), B, n1max, n2max,
+    _shape(out, (B * n1max, 768 if split else 256), "crossset_attn out")
+    if split and out.dtype != torch.bfloat16:
+        raise _lib.FpmError("crossset_attn: split rows are bf16")
+    _lib.call("fpm_crossset_attn_fwd", 2 if split else _code(out), _p(cost), cost.stride(0), cost.stride(1), B, n1max, n2max,
               _p(n2), _p(Wv), Wv.shape[1], _p(mix1w), _p(mix1b), _p(mix2w), _p(mix2b), _p(out), _stream(cost))
 
 

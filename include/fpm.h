@@ -67,6 +67,12 @@ int fpm_greedy_perm(const long* top_idx, long t_sb, int T, const float* k, int B
 int fpm_global_weights(const float* w1, long ld1, const float* w2, long ld2, int B, int D1, int D2, float* out,
                        long ldo, void* stream);
 
+/* ---- split-bf16 operands ------------------------------------------------------------------------
+ * dst[r] = [hi | lo | hi] (bf16, each Kp wide, zero-padded from K), hi = bf16(src[r]),
+ * lo = bf16(src[r] - hi): the A operand of a near-fp32 product on the bf16 MFMA path (weights
+ * packed [B_hi | B_hi | B_lo]); used for the AFA-U projections (afau.py:99-103, 188-199). */
+int fpm_split_bf16x3(const float* src, long lds, long rows, int K, int Kp, void* dst, long ldd, void* stream);
+
 /* ---- generic MFMA GEMM with fused epilogue ----------------------------------------------------
  * C[b][r][n] = epi(sum_k A[b][row(r)][k] * B[b][n][k] (+ bias[n])), row(r) = a_rows ? a_rows[r] : r.
  * epi: 0 store, 1 relu, 2 tanh, 3 affinity (softplus(v) - 0.5 inside [:n2[b], :n1[b]], else 0).
@@ -146,7 +152,10 @@ int fpm_gnn_param_count(int C);
 int fpm_node_classifier(const float* X, int B, int n1max, int n2max, const float* w, const float* bias,
                         const float* vpart, float* s, void* stream);
 
-/* ---- AFA-U k regressor (ngm.py:386-412, src/model/afau.py) ------------------------------------ */
+/* ---- AFA-U k regressor (ngm.py:386-412, src/model/afau.py) ------------------------------------
+ * crossset_attn: the row block's multi-head cross-set attention (afau.py:99-142) -> out rows of
+ * 256 = 16 heads x 16; dtype 0 = fp32, 1 = bf16, 2 = split bf16 rows [hi | lo | hi] (768 wide, the
+ * A operand of the near-fp32 combine product, see fpm_split_bf16x3). */
 int fpm_crossset_attn_fwd(int dtype, const float* cost, long c_sb, long c_ld, int B, int n1max, int n2max,
                           const int* n2, const float* Wv, int emb, const float* mix1w, const float* mix1b,
                           const float* mix2w, const float* mix2b, void* out, void* stream);

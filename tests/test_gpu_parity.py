@@ -607,3 +607,41 @@ def test_global_weights_kernel():
     assert (full.cpu() - O.global_weights(w1, w2)).abs().max() < 1e-6
     part = ops.global_weights(w1[2:5].to(DEV), w2[2:5].to(DEV))
     assert torch.equal(part, full[2:5])
+
+
+def test_split_bf16x3_operands():
+    """[hi | lo | hi] split rows: hi = bf16(x), hi + lo within 2^-16 of x, zero K padding; packed
+    [W_hi | W_hi | W_lo] weights give a product within 1e-5 (relative) of the fp32 one."""
+    g = torch.Generator().manual_seed(32)
+    x = torch.randn(37, 600, generator=g)
+    s3 = ops.split_bf16x3(x.to(DEV), 640).cpu()
+    hi, lo, hi2 = s3[:, :640].float(), s3[:, 640:1280].float(), s3[:, 1280:].float()
+    assert torch.equal(hi[:, :600], x.to(torch.bfloat16).float()) and torch.equal(hi, hi2)
+    assert (hi[:, 600:] == 0).all() and (lo[:, 600:] == 0).all()
+    assert ((hi + lo)[:, :600] - x).abs().max() <= x.abs().max() * 2.0 ** -16
+    W = torch.randn(256, 600, generator=g) * 0.05
+    W3 = ops.split_weights_bf16x3(W.to(DEV), 640)
+    out = torch.empty(37, 256, device=DEV)
+    ops.gemm(s3.to(DEV), W3, 37, 256, 1920, 1920, 1920, out_f=out)
+    ref = x.double() @ W.double().t()
+    assert ((out.cpu().double() - ref).abs().max() / ref.abs().max()) < 1e-5
+
+
+def test_crossset_attn_split_rows(sd):
+    """The attention kernel's split store (dtype 2): hi equals the bf16 store bit for bit (same
+    arithmetic), hi + lo is the unrounded value (within 2^-16)."""
+    net = fpm.Net(regression=True, dtype="bf16", backbone=False)
+    net.load_state_dict(sd)
+    wp = net.packed(DEV)
+    g = torch.Generator().manual_seed(33)
+    B, n = 3, 64
+    ss = (torch.rand(B, n, n, generator=g) ** 4).to(DEV)
+    n2 = _i32([64, 50, 61])
+    args = [wp[k] for k in ("row_Wv", "row_mix1w", "row_mix1b", "row_mix2w", "row_mix2b")]
+    a16 = torch.empty(B * n, 256, device=DEV, dtype=torch.bfloat16)
+    ops.crossset_attn(ss, n2, *args, a16)
+    a3 = torch.empty(B * n, 768, device=DEV, dtype=torch.bfloat16)
+    ops.crossset_attn(ss, n2, *args, a3, split=True)
+    assert torch.equal(a3[:, :256], a16) and torch.equal(a3[:, 512:], a16)
+    full = a3[:, :256].float() + a3[:, 256:512].float()
+    assert (full - a16.float()).abs().max() <= full.abs().max() * 2.0 ** -8
