@@ -234,12 +234,22 @@ def _record(name, d):
     print(name, d)
 
 
+def _bf16_gate(d):
+    """Bounds for the bf16 throughput mode against the fp32 oracle (reported, with
+    these gates).  Measured on the box (round 2): Kp <= 1.3e-5, ss <= 1.3e-6, ds_mat
+    <= 3.3e-6, k_prob <= 7.8e-4, cls_prob <= 2.7e-5, perm_mat tie-equivalent on 7-8 of 8 pairs.
+    The gates leave ~5-10x room; a pair's perm_mat may differ from the oracle's only by picks
+    among (near-)tied soft top-k entries or by a k* that moved across a rounding boundary."""
+    assert d["Kp"] < 1e-4 and d["ss"] < 1e-5 and d["ds_mat"] < 5e-5, d
+    assert d["k_prob"] < 5e-3 and d["cls_prob"] < 2e-4, d
+    assert d["perm_matches_kept"] >= 0.97 and d["perm_pairs_tie_equivalent"] >= 0.5, d
+
+
 def test_forward_bf16_fidelity_n128(sd):
     """bf16 MFMA mode vs the fp32 oracle at n=128 (C2 size)."""
     d = _fidelity(synth.make_batch(6, 2, 128), sd)
     _record("bf16_fidelity_n128", d)
-    assert d["Kp"] < 0.05 and d["k_prob"] < 0.05, d
-    assert d["perm_matches_kept"] >= 0.5, d
+    _bf16_gate(d)
 
 
 def test_forward_bf16_fidelity_c3(sd):
@@ -247,8 +257,7 @@ def test_forward_bf16_fidelity_c3(sd):
     fp32 oracle, max|d| on ss / ds_mat / k_prob / cls_prob and perm_mat agreement, recorded and bounded."""
     d = _fidelity(synth.make_batch(61, 4, 256), sd)
     _record("bf16_fidelity_c3", d)
-    assert d["Kp"] < 0.05 and d["k_prob"] < 0.05 and d["cls_prob"] < 0.05, d
-    assert d["perm_matches_kept"] >= 0.5, d
+    _bf16_gate(d)
 
 
 @pytest.mark.slow
@@ -256,8 +265,7 @@ def test_forward_bf16_fidelity_c5(sd):
     """The same gate at C5's graph size (n=512, B=1)."""
     d = _fidelity(synth.make_batch(62, 1, 512), sd)
     _record("bf16_fidelity_c5", d)
-    assert d["Kp"] < 0.05 and d["k_prob"] < 0.05 and d["cls_prob"] < 0.05, d
-    assert d["perm_matches_kept"] >= 0.5, d
+    _bf16_gate(d)
 
 
 def test_forward_data_dict_surface(sd):

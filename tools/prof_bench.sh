@@ -1,7 +1,11 @@
 #!/bin/bash
-# rocprofv3 kernel-trace + stats of the default bench command (the round's committed profile)
+# rocprofv3 kernel-trace + stats of the default bench command (the round's committed profile):
+#   bash tools/prof_bench.sh <tag>   -> gpurun_out/prof_<tag>/ (+ .json / .err)
+# The run does warmup 1 + 2 x 5 timed steps + 1 isolated forward = 12 forwards of 1024 pairs
+# (tools/roofline_table.py --forwards 12); no CPU baseline / parity / f32 line inside the trace.
 set -o pipefail
 export TMPDIR=/tmp
+TAG=${1:-bench}
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bench -o run --output-format csv -- \
-  python bench.py --steps 5 --warmup 1 --cpu-pairs 8 > gpurun_out/prof_bench.json 2> gpurun_out/prof_bench.err
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- \
+  python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-f32-line > gpurun_out/prof_$TAG.json 2> gpurun_out/prof_$TAG.err
