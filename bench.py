@@ -240,8 +240,12 @@ def main():
 
     if world > 1:
         dist.init_process_group("gloo")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one GPU per rank; with fewer visible GPUs than ranks (a rehearsal of the N-rank path on a
+    # smaller box) ranks share devices round-robin and say so in the JSON
+    ndev = torch.cuda.device_count()
+    shared_devices = ndev < world
+    torch.cuda.set_device(local % ndev)
+    dev = torch.device("cuda", local % ndev)
     sd = params.init_params(args.seed)
     net = fpm.Net(regression=True, backbone=False, dtype=args.dtype, lsa_threads=args.lsa_threads or None)
     net.load_state_dict(sd)
@@ -406,6 +410,7 @@ def main():
             "parity_vs_oracle": parity,
             "f32_line": f32_line,
             "strong_scaling": strong,
+            "ranks_share_devices": shared_devices,
             "input_gen_s": t_gen,
             "graph_build": graph_build,
         }

@@ -5,6 +5,10 @@
 #include <cstdlib>
 #include <cstring>
 
+namespace fpm {
+int& gemm_aff_big_flag();
+}
+
 extern "C" int fpm_gemm(int dtype, const void* A, long lda, long sA, const int* a_rows, const void* B, long ldb,
                         long sB, int M, int N, int K, int batch, int epi, const float* bias, float* Cf, void* Ct,
                         long ldc, long sC, const int* n1, const int* n2, void* stream) {
@@ -27,7 +31,7 @@ extern "C" int fpm_gemm(int dtype, const void* A, long lda, long sA, const int* 
     hipStream_t st = (hipStream_t)stream;
     // bf16 with a large M: the 256-row LDS-DMA tiles (gemm_big.h)
     const int mt = (M + G2_BM - 1) / G2_BM;
-    const bool epi_ok = epi == EPI_STORE || epi == EPI_RELU || (epi == EPI_AFFINITY && Cf && !Ct);
+    const bool epi_ok = epi == EPI_STORE || epi == EPI_RELU || (epi == EPI_AFFINITY && Cf && !Ct && gemm_aff_big_flag());
     const bool big = dtype == 1 && M >= G2_BM && K % G2_BK == 0 && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
                      !(Cf && Ct) && (Cf ? ldc % 4 == 0 : ldc % 8 == 0) && epi_ok &&
                      (long)mt * ((N + 127) / 128) * batch >= 128;
@@ -62,6 +66,16 @@ extern "C" int fpm_gemm(int dtype, const void* A, long lda, long sA, const int* 
 }
 
 namespace fpm {
+// the vertex-affinity epilogue on the 256-row LDS-DMA tiles (1) or the 128x128 tiles (0);
+// env FPM_GEMM_AFF_BIG or fpm_set_tuning("gemm_aff_big", v)
+int& gemm_aff_big_flag() {
+    static int on = [] {
+        const char* e = getenv("FPM_GEMM_AFF_BIG");
+        return e ? atoi(e) : 1;
+    }();
+    return on;
+}
+
 int& gemm_phase_flag() {
     static int on = [] {
         const char* e = getenv("FPM_GEMM_PHASE");
@@ -75,6 +89,8 @@ int& gnn_packed_flag();
 int& gnn_unroll_flag();
 int& gnn_group_flag();
 int& gnn_group1_flag();
+int& gnn_wide_flag();
+int& gnn_il_flag();
 int& combine_npb_flag();
 int& afau_lut_flag();
 int& sinkhorn_fast_flag();
@@ -83,10 +99,13 @@ int& soft_topk_fast_flag();
 extern "C" int fpm_set_tuning(const char* key, int value) {
     int* f = nullptr;
     if (key && !strcmp(key, "gemm_phase")) f = &fpm::gemm_phase_flag();
+    else if (key && !strcmp(key, "gemm_aff_big")) f = &fpm::gemm_aff_big_flag();
     else if (key && !strcmp(key, "gnn_packed")) f = &gnn_packed_flag();
     else if (key && !strcmp(key, "gnn_unroll")) f = &gnn_unroll_flag();
     else if (key && !strcmp(key, "gnn_group")) f = &gnn_group_flag();
     else if (key && !strcmp(key, "gnn_group1")) f = &gnn_group1_flag();
+    else if (key && !strcmp(key, "gnn_wide")) f = &gnn_wide_flag();
+    else if (key && !strcmp(key, "gnn_il")) f = &gnn_il_flag();
     else if (key && !strcmp(key, "combine_npb")) f = &combine_npb_flag();
     else if (key && !strcmp(key, "afau_lut")) f = &afau_lut_flag();
     else if (key && !strcmp(key, "sinkhorn_fast")) f = &sinkhorn_fast_flag();

@@ -45,7 +45,11 @@ __device__ __forceinline__ void pk_fma_bcast(f2_t& acc, f2_t w, f2_t v, bool hi)
     else asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1]" : "+v"(acc) : "s"(w), "v"(v));
 }
 
-template <int C, bool PACKED, int U = 1, int G = 1>
+// WIDE (C = 17, n1max % 4 == 0): phase 1 with 16-B loads -- each thread sums one quad of graph-1
+// positions (4 consecutive i) for a group of <= 5 channels, so a graph-2 neighbour row costs
+// 17 / 4 times fewer vector-memory instructions; the per-position sums (same order, same
+// values) land in the same LDS layout, so phase 2 and the outputs are bit-identical.
+template <int C, bool PACKED, int U = 1, int G = 1, bool WIDE = false, bool IL = false>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(PACKED ? 5 : 6, 8))) void gnn_layer_kernel(const float* __restrict__ X, int n1max, int n2max,
                                                          const int* __restrict__ ptr1, const int* __restrict__ nbr1,
                                                          const int* __restrict__ ptr2, const int* __restrict__ nbr2,
@@ -84,7 +88,48 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(PACKED ? 5
     __syncthreads();
     const int nn2 = active ? nnb2_[sub] : 0;
     const int beg2 = active ? beg2_[sub] : 0;
-    if (i < n1max && active) {
+    if constexpr (WIDE) {
+        static_assert(C == 17, "WIDE phase 1 is the 17-channel layer's");
+        constexpr int CPG = 5;                               // ceil(17 / 4); ng >= 4 channel groups
+        const int nq = n1max >> 2;
+        const int ng = subw / nq;
+        const int q = i % nq, g = i / nq;
+        const int c0 = g * ((C + ng - 1) / ng);
+        const int cn = min(C - c0, (C + ng - 1) / ng);
+        if (active && g < ng && cn > 0) {
+            float4 acc[CPG];
+#pragma unroll
+            for (int cc = 0; cc < CPG; ++cc) acc[cc] = make_float4(0.f, 0.f, 0.f, 0.f);
+            const float* base = Xb + (long)c0 * N + 4 * q;
+            auto add_row = [&](int nb) {
+                const float* row = base + (long)nb * n1max;
+                float4 v[CPG];
+#pragma unroll
+                for (int cc = 0; cc < CPG; ++cc)
+                    if (cc < cn) v[cc] = *(const float4*)(row + (long)cc * N);
+#pragma unroll
+                for (int cc = 0; cc < CPG; ++cc)
+                    if (cc < cn) {
+                        acc[cc].x += v[cc].x;
+                        acc[cc].y += v[cc].y;
+                        acc[cc].z += v[cc].z;
+                        acc[cc].w += v[cc].w;
+                    }
+            };
+            const int nl = nn2 < 64 ? nn2 : 64;
+            for (int k = 0; k < nl; ++k) add_row(nb2[k]);
+            for (int k = 64; k < nn2; ++k) add_row(nbr2[beg2 + k]);
+            float* Tq = Tg + 4 * q * TS + c0;
+#pragma unroll
+            for (int cc = 0; cc < CPG; ++cc)
+                if (cc < cn) {
+                    Tq[cc] = acc[cc].x;
+                    Tq[TS + cc] = acc[cc].y;
+                    Tq[2 * TS + cc] = acc[cc].z;
+                    Tq[3 * TS + cc] = acc[cc].w;
+                }
+        }
+    } else if (i < n1max && active) {
         // neighbour-outer, channel-inner: C independent loads in flight per neighbour row
         float acc[C];
 #pragma unroll
@@ -203,6 +248,60 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(PACKED ? 5
         a2[k] = (f2_t){agg[2 * k], 2 * k + 1 < C ? agg[2 * k + 1] : 0.f};
     }
     const f2_t* W2p = (const f2_t*)W;                     // pair view (all block offsets even)
+    if constexpr (IL) {
+        // input-channel-outer order: a weight row W[c][0..15] is contiguous, so the scalar loads
+        // merge into wide s_load_dwordx8/x16 (the per-(c, pair) order issued one s_load_dwordx2
+        // per FMA: ~470 scalar-memory instructions per wave).  Every accumulator keeps its fma
+        // chain order, so the outputs are bit-identical to the loop above.
+        f2_t h[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) h[m] = W2p[(P::b1 >> 1) + m];
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int m = 0; m < 8; ++m) pk_fma_bcast(h[m], W2p[((P::W1 + c * 16) >> 1) + m], x2[c >> 1], c & 1);
+#pragma unroll
+        for (int m = 0; m < 8; ++m) h[m] = (f2_t){fmaxf(h[m].x, 0.f), fmaxf(h[m].y, 0.f)};
+        float z = 0.f, vp = 0.f;
+        float* Xob = Xo + (long)b * 17 * N + p;
+        constexpr int OPB = 4;                            // output pairs per block (register budget)
+#pragma unroll
+        for (int ob = 0; ob < 8; ob += OPB) {
+            f2_t l[OPB], r[OPB], t[OPB];
+#pragma unroll
+            for (int k = 0; k < OPB; ++k) l[k] = r[k] = t[k] = (f2_t){0.f, 0.f};
+#pragma unroll
+            for (int c = 0; c < C; ++c)
+#pragma unroll
+                for (int k = 0; k < OPB; ++k) {
+                    pk_fma_bcast(l[k], W2p[((P::Wl + c * 16) >> 1) + ob + k], a2[c >> 1], c & 1);
+                    pk_fma_bcast(r[k], W2p[((P::Wr + c * 16) >> 1) + ob + k], x2[c >> 1], c & 1);
+                }
+#pragma unroll
+            for (int m = 0; m < 16; ++m)
+#pragma unroll
+                for (int k = 0; k < OPB; ++k)
+                    pk_fma_bcast(t[k], W2p[((P::W2 + m * 16) >> 1) + ob + k], h[m >> 1], m & 1);
+#pragma unroll
+            for (int k = 0; k < OPB; ++k) {
+                const int op = ob + k, o = 2 * op;
+                const f2_t tb = t[k] + W2p[(P::b2 >> 1) + op];
+                const f2_t x1 = ((l[k] + W2p[(P::bl >> 1) + op]) + r[k]) + (f2_t){fmaxf(tb.x, 0.f), fmaxf(tb.y, 0.f)};
+                if (vpart) {
+                    vp = fmaf(cls_w[o], x1.x, vp);
+                    vp = fmaf(cls_w[o + 1], x1.y, vp);
+                } else {
+                    Xob[(long)o * N] = x1.x;
+                    Xob[(long)(o + 1) * N] = x1.y;
+                }
+                z = fmaf(W[P::wc + o], x1.x, z);
+                z = fmaf(W[P::wc + o + 1], x1.y, z);
+            }
+        }
+        if (vpart) vpart[(long)b * N + p] = vp;
+        zbuf[(long)b * N + p] = z + W[P::bc];
+        return;
+    }
     f2_t h[8];
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
@@ -294,6 +393,26 @@ int& gnn_group1_flag() {
     return u;
 }
 
+// 16-B phase-1 loads for the 17-channel layer (bit-identical); env FPM_GNN_WIDE or
+// fpm_set_tuning("gnn_wide", v)
+int& gnn_wide_flag() {
+    static int u = [] {
+        const char* e = getenv("FPM_GNN_WIDE");
+        return e ? atoi(e) : 1;
+    }();
+    return u;
+}
+
+// input-channel-outer MLP order (wide scalar weight loads, bit-identical); env FPM_GNN_IL or
+// fpm_set_tuning("gnn_il", v)
+int& gnn_il_flag() {
+    static int u = [] {
+        const char* e = getenv("FPM_GNN_IL");
+        return e ? atoi(e) : 1;
+    }();
+    return u;
+}
+
 // graph-2 neighbour rows loaded U at a time (1, 2 or 3; bit-identical); env FPM_GNN_UNROLL or
 // fpm_set_tuning("gnn_unroll", v)
 int& gnn_unroll_flag() {
@@ -320,29 +439,41 @@ extern "C" int fpm_kron_gnn_layer_fwd(const float* X, int C, int B, int n1max, i
     const int un = gnn_unroll_flag();
     // default 2 (21% faster at n = 256, 13% at n = 100; slower as a 1024-thread workgroup at n = 512)
     const int grp = gnn_group_flag() * threads <= 512 ? gnn_group_flag() : 1;
-#define FPM_GNN(C_, P_, U_, G_)                                                                                  \
+    const bool wide = gnn_wide_flag() != 0 && (n1max & 3) == 0;
+    const bool il = gnn_il_flag() != 0;
+#define FPM_GNN_WI(C_, P_, U_, G_, W_, I_)                                                                       \
     do {                                                                                                         \
         const size_t sh_ = sh * G_;                                                                              \
         if (sh_ > 65536)                                                                                         \
-            (void)hipFuncSetAttribute((const void*)gnn_layer_kernel<C_, P_, U_, G_>,                             \
+            (void)hipFuncSetAttribute((const void*)gnn_layer_kernel<C_, P_, U_, G_, W_, I_>,                     \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh_);                     \
         const dim3 g_(pair_grid((n2max + G_ - 1) / G_, B));                                                      \
         const dim3 t_(threads * G_);                                                                             \
-        hipLaunchKernelGGL((gnn_layer_kernel<C_, P_, U_, G_>), g_, t_, sh_, st, X, n1max, n2max, ptr1,           \
+        hipLaunchKernelGGL((gnn_layer_kernel<C_, P_, U_, G_, W_, I_>), g_, t_, sh_, st, X, n1max, n2max, ptr1,   \
                            nbr1, ptr2, nbr2, n1, n2, params, Xout, zbuf, vpart, cls_w, B);                       \
     } while (0)
+#define FPM_GNN_W(C_, P_, U_, G_, W_)                                                                            \
+    do {                                                                                                         \
+        if (il) FPM_GNN_WI(C_, P_, U_, G_, W_, true);                                                            \
+        else FPM_GNN_WI(C_, P_, U_, G_, W_, false);                                                              \
+    } while (0)
+#define FPM_GNN(C_, P_, U_, G_) FPM_GNN_W(C_, P_, U_, G_, false)
     if (C == 1) {
         if (!packed) FPM_GNN(1, false, 1, 1);
         else if (grp == 2 && gnn_group1_flag()) FPM_GNN(1, true, 1, 2);
         else FPM_GNN(1, true, 1, 1);
     }
     else if (!packed) FPM_GNN(17, false, 1, 1);
+    else if (wide && grp == 2) FPM_GNN_W(17, true, 1, 2, true);
+    else if (wide) FPM_GNN_W(17, true, 1, 1, true);
     else if (grp == 2) FPM_GNN(17, true, 1, 2);
     else if (grp == 4) FPM_GNN(17, true, 1, 4);
     else if (un == 2) FPM_GNN(17, true, 2, 1);
     else if (un == 3) FPM_GNN(17, true, 3, 1);
     else FPM_GNN(17, true, 1, 1);
 #undef FPM_GNN
+#undef FPM_GNN_W
+#undef FPM_GNN_WI
     return fpm::check_launch("fpm_kron_gnn_layer_fwd");
 }
 

@@ -584,7 +584,7 @@ def test_gnn_kernel_variants_bit_identical(sd):
     net.load_state_dict(sd)
     bt = DeviceBatch.from_pairs(pairs, DEV)
     outs = []
-    for key, val in (("gnn_group", 1), ("gnn_group", 2), ("gnn_unroll", 3), ("combine_npb", 16)):
+    for key, val in (("gnn_group", 1), ("gnn_group", 2), ("gnn_unroll", 3), ("combine_npb", 16), ("gnn_wide", 0), ("gnn_il", 0)):
         prev = ops.set_tuning(key, val)
         try:
             r = net.run(bt, chunks=1)
