@@ -40,9 +40,15 @@ SIGNATURES = {
     "fpm_kron_gnn_layer_fwd": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P]),
     "fpm_gnn_param_count": (I, [I]),
     "fpm_node_classifier": (I, [P, I, I, I, P, P, P, P, P]),
-    "fpm_crossset_attn_fwd": (I, [I, P, L, L, I, I, I, P, P, I, P, P, P, P, P, P]),
+    "fpm_crossset_attn_fwd": (I, [I, P, L, L, I, I, I, P, P, I, P, P, P, P, P, P, P]),
     "fpm_instnorm": (I, [I, P, P, I, I, I, P, P, P, P, F, P, P, I, P, P]),
     "fpm_afau_head": (I, [P, P, I, I, P, P, P, P, P, P, P, P, P, P]),
+    "fpm_afau_head_bwd": (I, [P, P, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P]),
+    "fpm_instnorm_bwd": (I, [P, P, I, I, I, P, P, P, P, F, P, P, P, I, P, P, P]),
+    "fpm_afau_attn_bwd": (I, [P, L, L, I, I, I, P, P, I, P, P, P, P, P, P, P, P, P, P]),
+    "fpm_rows_sum": (I, [P, I, L, P, I, P, I, P]),
+    "fpm_transpose": (I, [P, L, I, L, P, L, P]),
+    "fpm_elementwise": (I, [P, P, L, I, P]),
     "fpm_match_cls_ws_floats": (L, [I, I, I]),
     "fpm_match_cls_fwd": (I, [I, P, P, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),
     "fpm_lsa_batch_host": (I, [P, L, L, P, P, I, I, P, I]),

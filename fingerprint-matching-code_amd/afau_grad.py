@@ -1,0 +1,232 @@
+"""AFA-U k regressor: fp32 HIP forward that keeps its intermediates, and the hand-written HIP
+backward (``csrc/afau_bwd.hip``) that turns d(ks) into the regressor's parameter gradients.
+
+Reference: ``src/model/afau.py:54-300`` (Encoder / EncoderLayer / EncodingBlock /
+CrossSet_MultiHeadAttention / AddAndInstanceNormalization / FeedForward) and ``ngm.py:386-412``
+(R0 = 0 rows, C0 = one-hot columns, max pool over positions, final_row / final_col heads,
+ks = sigmoid(mean)), trained through ``ks_loss`` (``training_loop.py:23-70``; ``ss`` is detached,
+ngm.py:398).  With R0 = 0 the row block's query, its keys' contribution and the dot-product input
+of the mixed score vanish, so ``Wq``, ``Wk`` and ``mix1_weight[:, 0]`` get exactly zero gradient;
+the col block reads zero rows (v = 0), so its attention parameters get zero gradient and its
+combine bias is cancelled by the instance norm.  The products (FFN, combine and their weight
+gradients) run on ``fpm_gemm`` in fp32.
+"""
+import math
+
+import torch
+
+from . import _lib
+from . import config as C
+from . import ops
+
+E, HD, FF, H = C.AFAU_EMB, C.AFAU_HEADS * C.AFAU_QKV, C.AFAU_FF, C.AFAU_HEADS
+PRE = "encoder_k.layers.0."
+
+
+def _gemm(A, W, M, N, K, bias=None, epi=ops.EPI_STORE):
+    """C (M x N) fp32 = epi(A (M x K) W^T (+ bias)), W (N x K) row-major."""
+    out = torch.empty(M, N, device=A.device, dtype=torch.float32)
+    ops.gemm(A, W, M, N, K, A.stride(0), W.stride(0), epi=epi, bias=bias, out_f=out, ldc=N)
+    return out
+
+
+def rows_sum(x, key=None, nkeys=1):
+    """Sum over the leading dim in order (fpm_rows_sum); with ``key``: out[u] = sum of x[b] with
+    key[b] == u.  Long sums run in two levels (chunks of ~64 rows, then the chunk sums)."""
+    x = x.contiguous()
+    B = x.shape[0]
+    K = x[0].numel() if B else 0
+    if key is None and B > 256:
+        S = (B + 63) // 64
+        part = torch.empty(S, *x.shape[1:], device=x.device, dtype=torch.float32)
+        _lib.call("fpm_rows_sum", ops._p(x), B, K, None, S, ops._p(part), 0, ops._stream(x))
+        return rows_sum(part)
+    shape = ((nkeys,) if key is not None else ()) + tuple(x.shape[1:])
+    out = torch.empty(shape, device=x.device, dtype=torch.float32)
+    _lib.call("fpm_rows_sum", ops._p(x), B, K, ops._p(key), nkeys if key is not None else 1, ops._p(out), 0,
+              ops._stream(x))
+    return out
+
+
+def transpose(x, ldo):
+    """(R, C) -> (C, ldo) with zero columns beyond R (fpm_transpose)."""
+    R, Cc = x.shape
+    out = torch.empty(Cc, ldo, device=x.device, dtype=torch.float32)
+    _lib.call("fpm_transpose", ops._p(x), R, Cc, x.stride(0), ops._p(out), ldo, ops._stream(x))
+    return out
+
+
+def wgrad(dY, X, split_k=512):
+    """dY^T X (N1 x N2) for row-major dY (R x N1), X (R x N2): transposed operands, K = rows split into
+    slices of <= split_k (a batched fpm_gemm), partial products summed in order."""
+    R, N1 = dY.shape
+    N2 = X.shape[1]
+    S = max(1, math.ceil(R / split_k))
+    Ks = ((math.ceil(R / S) + 3) // 4) * 4
+    Rp = S * Ks
+    T1, T2 = transpose(dY, Rp), transpose(X, Rp)
+    part = torch.empty(S, N1, N2, device=dY.device, dtype=torch.float32)
+    ops.gemm(T1, T2, N1, N2, Ks, Rp, Rp, batch=S, sA=Ks, sB=Ks, out_f=part, ldc=N2, sC=N1 * N2)
+    return rows_sum(part)
+
+
+def _ew(x, ref, mode):
+    _lib.call("fpm_elementwise", ops._p(x), ops._p(ref), x.numel(), int(mode), ops._stream(x))
+    return x
+
+
+def _instnorm_bwd(x1, x2, B, P, nvalid=None, onehot_bias=None, w=None, b=None, dy=None, gseed=None, want_dx=True):
+    dev = w.device
+    dx = torch.empty(B * P, E, device=dev, dtype=torch.float32) if want_dx else None
+    dwp = torch.empty(B, E, device=dev, dtype=torch.float32)
+    dbp = torch.empty(B, E, device=dev, dtype=torch.float32)
+    _lib.call("fpm_instnorm_bwd", ops._p(x1), ops._p(x2), B, P, E, ops._p(nvalid), ops._p(onehot_bias), ops._p(w),
+              ops._p(b), float(C.IN_EPS), ops._p(dy), ops._p(gseed), ops._p(dx), 0, ops._p(dwp), ops._p(dbp),
+              ops._stream(w))
+    return dx, rows_sum(dwp), rows_sum(dbp)
+
+
+class AfauSaved:
+    """What the backward reads: per block the instance-norm inputs, the FFN hidden rows, the max-pool
+    results; for the row block also the attention output and its softmax statistics."""
+
+
+def forward(P, ss, bt):
+    """ks (B,) by the fp32 HIP forward (the same kernels as Net._afau), keeping the intermediates.
+    ``P(name)`` returns a parameter (reference state_dict names) on the device."""
+    dev = ss.device
+    B, n1max, n2max = bt.B, bt.n1max, bt.n2max
+    if max(n1max, n2max) > C.UNIV_SIZE:
+        raise AssertionError("UNIV_SIZE cap: n1max/n2max must be <= %d (ngm.py:387-389)" % C.UNIV_SIZE)
+    g = lambda blk, k: P(PRE + blk + "_encoding_block." + k).detach().contiguous()
+    sv = AfauSaved()
+    sv.B, sv.n1max, sv.n2max = B, n1max, n2max
+    ssc = ss.detach().contiguous()
+    sv.ss = ssc
+    R = B * n1max
+    sv.stats = torch.empty(R, 16, 2, device=dev, dtype=torch.float32)
+    sv.att = torch.empty(R, HD, device=dev, dtype=torch.float32)
+    ops.crossset_attn(ssc, bt.n2, g("row", "Wv.weight"), g("row", "mixed_score_MHA.mix1_weight"),
+                      g("row", "mixed_score_MHA.mix1_bias"), g("row", "mixed_score_MHA.mix2_weight"),
+                      g("row", "mixed_score_MHA.mix2_bias"), sv.att, stats=sv.stats)
+    sv.mh = _gemm(sv.att, g("row", "multi_head_combine.weight"), R, E, HD, bias=g("row", "multi_head_combine.bias"))
+    n2h = bt.n_host[1].to(torch.int64)
+    n2u, inv = torch.unique(n2h, return_inverse=True)
+    sv.Bu = int(n2u.numel())
+    sv.n2u = n2u.to(device=dev, dtype=torch.int32)
+    sv.inv = inv.to(device=dev, dtype=torch.int32)
+    sv.n2 = bt.n2
+    sv.blk = {}
+    for blk, nb, Pn in (("row", B, n1max), ("col", sv.Bu, n2max)):
+        rows = nb * Pn
+        o1 = torch.empty(rows, E, device=dev, dtype=torch.float32)
+        if blk == "row":
+            ops.instnorm(sv.mh, nb, Pn, E, g(blk, "add_n_normalization_1.norm.weight"),
+                         g(blk, "add_n_normalization_1.norm.bias"), out_f=o1)
+        else:
+            ops.instnorm(None, nb, Pn, E, g(blk, "add_n_normalization_1.norm.weight"),
+                         g(blk, "add_n_normalization_1.norm.bias"), nvalid=sv.n2u,
+                         onehot_bias=g(blk, "multi_head_combine.bias"), out_f=o1)
+        h = _gemm(o1, g(blk, "feed_forward.W1.weight"), rows, FF, E, bias=g(blk, "feed_forward.W1.bias"),
+                  epi=ops.EPI_RELU)
+        ff = _gemm(h, g(blk, "feed_forward.W2.weight"), rows, E, FF, bias=g(blk, "feed_forward.W2.bias"))
+        gm = torch.empty(nb, E, device=dev, dtype=torch.float32)
+        ops.instnorm(o1, nb, Pn, E, g(blk, "add_n_normalization_2.norm.weight"),
+                     g(blk, "add_n_normalization_2.norm.bias"), in2=ff, gmax=gm)
+        sv.blk[blk] = dict(o1=o1, h=h, ff=ff, gm=gm, nb=nb, P=Pn)
+    sv.gr = sv.blk["row"]["gm"]
+    sv.gc = sv.blk["col"]["gm"].index_select(0, sv.inv.long()).contiguous()
+    ks = torch.empty(B, device=dev, dtype=torch.float32)
+    hp = lambda k: P(k).detach().contiguous()
+    ops.afau_head(sv.gr, sv.gc, B, E, hp("final_row.0.weight"), hp("final_row.0.bias"), hp("final_row.2.weight"),
+                  hp("final_row.2.bias"), hp("final_col.0.weight"), hp("final_col.0.bias"), hp("final_col.2.weight"),
+                  hp("final_col.2.bias"), ks)
+    return ks, sv
+
+
+def backward(P, sv, dks, names):
+    """Parameter gradients of the regressor for d(ks) -> list aligned with ``names``."""
+    dev = dks.device
+    B = sv.B
+    g = lambda blk, k: P(PRE + blk + "_encoding_block." + k).detach().contiguous()
+    hp = lambda k: P(k).detach().contiguous()
+    grads = {}
+    # heads
+    dgr = torch.empty(B, E, device=dev, dtype=torch.float32)
+    dgc = torch.empty(B, E, device=dev, dtype=torch.float32)
+    PS = 8 * E + 17
+    part = torch.empty(B, 2 * PS, device=dev, dtype=torch.float32)
+    _lib.call("fpm_afau_head_bwd", ops._p(sv.gr), ops._p(sv.gc), B, E, ops._p(hp("final_row.0.weight")),
+              ops._p(hp("final_row.0.bias")), ops._p(hp("final_row.2.weight")), ops._p(hp("final_row.2.bias")),
+              ops._p(hp("final_col.0.weight")), ops._p(hp("final_col.0.bias")), ops._p(hp("final_col.2.weight")),
+              ops._p(hp("final_col.2.bias")), ops._p(dks.contiguous()), ops._p(dgr), ops._p(dgc), ops._p(part),
+              ops._stream(dks))
+    hs = rows_sum(part)
+    for q, head in enumerate(("final_row", "final_col")):
+        o = q * PS
+        grads[head + ".0.weight"] = hs[o:o + 8 * E].view(8, E)
+        grads[head + ".0.bias"] = hs[o + 8 * E:o + 8 * E + 8]
+        grads[head + ".2.weight"] = hs[o + 8 * E + 8:o + 8 * E + 16].view(1, 8)
+        grads[head + ".2.bias"] = hs[o + 8 * E + 16:o + 8 * E + 17]
+    dgcu = rows_sum(dgc, key=sv.inv, nkeys=sv.Bu)
+    for blk, seed in (("row", dgr), ("col", dgcu)):
+        st = sv.blk[blk]
+        nb, Pn = st["nb"], st["P"]
+        rows = nb * Pn
+        pre = PRE + blk + "_encoding_block."
+        # output instance norm, fed by the max pool
+        dx2, gw, gb = _instnorm_bwd(st["o1"], st["ff"], nb, Pn, w=g(blk, "add_n_normalization_2.norm.weight"),
+                                    b=g(blk, "add_n_normalization_2.norm.bias"), gseed=seed)
+        grads[pre + "add_n_normalization_2.norm.weight"] = gw
+        grads[pre + "add_n_normalization_2.norm.bias"] = gb
+        # feed-forward: ff = W2 relu(W1 o1 + b1) + b2
+        W1, W2 = g(blk, "feed_forward.W1.weight"), g(blk, "feed_forward.W2.weight")
+        dpre = _gemm(dx2, W2.t().contiguous(), rows, FF, E)
+        _ew(dpre, st["h"], 0)
+        grads[pre + "feed_forward.W2.weight"] = wgrad(dx2, st["h"])
+        grads[pre + "feed_forward.W2.bias"] = rows_sum(dx2)
+        grads[pre + "feed_forward.W1.weight"] = wgrad(dpre, st["o1"])
+        grads[pre + "feed_forward.W1.bias"] = rows_sum(dpre)
+        do1 = _gemm(dpre, W1.t().contiguous(), rows, E, FF)
+        _ew(do1, dx2, 1)
+        # first instance norm: row input = combine(att); col input = one-hot + combine bias
+        if blk == "row":
+            dmh, gw, gb = _instnorm_bwd(sv.mh, None, nb, Pn, w=g(blk, "add_n_normalization_1.norm.weight"),
+                                        b=g(blk, "add_n_normalization_1.norm.bias"), dy=do1)
+        else:
+            _, gw, gb = _instnorm_bwd(None, None, nb, Pn, nvalid=sv.n2u, onehot_bias=g(blk, "multi_head_combine.bias"),
+                                      w=g(blk, "add_n_normalization_1.norm.weight"),
+                                      b=g(blk, "add_n_normalization_1.norm.bias"), dy=do1, want_dx=False)
+        grads[pre + "add_n_normalization_1.norm.weight"] = gw
+        grads[pre + "add_n_normalization_1.norm.bias"] = gb
+        if blk == "col":
+            continue
+        Wc = g(blk, "multi_head_combine.weight")
+        grads[pre + "multi_head_combine.weight"] = wgrad(dmh, sv.att)
+        grads[pre + "multi_head_combine.bias"] = rows_sum(dmh)
+        datt = _gemm(dmh, Wc.t().contiguous(), rows, HD, E)
+        n2max = sv.n2max
+        dwvp = torch.empty(B, HD, n2max, device=dev, dtype=torch.float32)
+        mixp = torch.empty(B, H, 49, device=dev, dtype=torch.float32)
+        Wv = g(blk, "Wv.weight")
+        _lib.call("fpm_afau_attn_bwd", ops._p(sv.ss), sv.ss.stride(0), sv.ss.stride(1), B, sv.n1max, n2max,
+                  ops._p(sv.n2), ops._p(Wv), Wv.shape[1], ops._p(g(blk, "mixed_score_MHA.mix1_weight")),
+                  ops._p(g(blk, "mixed_score_MHA.mix1_bias")), ops._p(g(blk, "mixed_score_MHA.mix2_weight")),
+                  ops._p(g(blk, "mixed_score_MHA.mix2_bias")), ops._p(sv.att), ops._p(datt), ops._p(sv.stats),
+                  ops._p(dwvp), ops._p(mixp), ops._stream(dks))
+        dwv = torch.zeros(HD, Wv.shape[1], device=dev, dtype=torch.float32)
+        dwv[:, :n2max] = rows_sum(dwvp)
+        grads[pre + "Wv.weight"] = dwv
+        mix = rows_sum(mixp)                                   # (H, 49)
+        m1 = torch.zeros(H, 2, C.AFAU_MS_HIDDEN, device=dev, dtype=torch.float32)
+        m1[:, 1] = mix[:, 16:32]                               # row 0 multiplies the (zero) dot product
+        grads[pre + "mixed_score_MHA.mix1_weight"] = m1
+        grads[pre + "mixed_score_MHA.mix1_bias"] = mix[:, 32:48].contiguous()
+        grads[pre + "mixed_score_MHA.mix2_weight"] = mix[:, 0:16].reshape(H, C.AFAU_MS_HIDDEN, 1).contiguous()
+        grads[pre + "mixed_score_MHA.mix2_bias"] = mix[:, 48:49].contiguous()
+    out = []
+    for k in names:
+        v = grads.get(k)
+        p = P(k)
+        out.append(torch.zeros_like(p) if v is None else v.reshape(p.shape).to(p.dtype))
+    return out

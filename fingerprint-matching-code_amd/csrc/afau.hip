@@ -50,7 +50,7 @@ __global__ __launch_bounds__(256) void afau_row_attn_kernel(const float* __restr
                                                             const float* __restrict__ mix1b,
                                                             const float* __restrict__ mix2w,
                                                             const float* __restrict__ mix2b, T* __restrict__ out,
-                                                            int use_lut) {
+                                                            int use_lut, float2* __restrict__ stats) {
     typedef float f32x4_t __attribute__((ext_vector_type(4)));
     __shared__ AfSmem S;
     const int b = blockIdx.x, i0 = blockIdx.y * 16, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -188,6 +188,7 @@ __global__ __launch_bounds__(256) void afau_row_attn_kernel(const float* __restr
                 sum = fmaf(ms.y, sc, sum);
                 o = fmaf(S.part[buf][w][tid], sc, o);
             }
+            if (stats && d == 0 && ii < n1max) stats[((long)b * n1max + ii) * 16 + h] = make_float2(M, sum);
             if (ii < n1max) {
                 const float v = o / sum;
                 if constexpr (SPLIT) {
@@ -325,7 +326,7 @@ int& afau_lut_flag() {
 
 extern "C" int fpm_crossset_attn_fwd(int dtype, const float* cost, long c_sb, long c_ld, int B, int n1max, int n2max,
                                      const int* n2, const float* Wv, int emb, const float* mix1w, const float* mix1b,
-                                     const float* mix2w, const float* mix2b, void* out, void* stream) {
+                                     const float* mix2w, const float* mix2b, void* out, float* stats, void* stream) {
     FPM_CHECK_ARG(n2max <= emb, "crossset_attn: n2max > embedding dim");
     if (B == 0) return 0;
     dim3 grid(B, (n1max + 15) / 16);
@@ -336,7 +337,7 @@ extern "C" int fpm_crossset_attn_fwd(int dtype, const float* cost, long c_sb, lo
     const int lut = afau_lut_flag() != 2 ? afau_lut_flag() : (dtype != 0);
 #define FPM_ATT(TT, TJ_, SP_)                                                                                    \
     hipLaunchKernelGGL((afau_row_attn_kernel<TT, TJ_, SP_>), grid, dim3(256), 0, st, cost, c_sb, c_ld, n1max, n2max, \
-                       n2, Wv, emb, mix1w, mix1b, mix2w, mix2b, (TT*)out, lut)
+                       n2, Wv, emb, mix1w, mix1b, mix2w, mix2b, (TT*)out, lut, (float2*)stats)
     if (dtype == 0) { if (n2max <= 256) FPM_ATT(float, 16, false); else FPM_ATT(float, 40, false); }
     else if (dtype == 1) { if (n2max <= 256) FPM_ATT(bf16_t, 16, false); else FPM_ATT(bf16_t, 40, false); }
     else { if (n2max <= 256) FPM_ATT(bf16_t, 16, true); else FPM_ATT(bf16_t, 40, true); }

@@ -248,8 +248,10 @@ def crossset_attn(cost, n2, Wv, mix1w, mix1b, mix2w, mix2b, out, split=False):
     _shape(out, (B * n1max, 768 if split else 256), "crossset_attn out")
     if split and out.dtype != torch.bfloat16:
         raise _lib.FpmError("crossset_attn: split rows are bf16")
+    _shape(stats, (B * n1max, 16, 2), "crossset_attn stats")
     _lib.call("fpm_crossset_attn_fwd", 2 if split else _code(out), _p(cost), cost.stride(0), cost.stride(1), B, n1max, n2max,
-              _p(n2), _p(Wv), Wv.shape[1], _p(mix1w), _p(mix1b), _p(mix2w), _p(mix2b), _p(out), _stream(cost))
+              _p(n2), _p(Wv), Wv.shape[1], _p(mix1w), _p(mix1b), _p(mix2w), _p(mix2b), _p(out), _p(stats),
+              _stream(cost))
 
 
 def instnorm(in1, B, P, Cn, w, b, in2=None, nvalid=None, onehot_bias=None, out_f=None, out_t=None, gmax=None,

@@ -13,18 +13,23 @@ same HIP forward kernels as inference and has a hand-written backward:
   * ``GnnLayerFn``     PYGNNLayer: Sinkhorn backward (``fpm_sinkhorn_log_bwd``), node MLP algebra,
     and the Kronecker aggregation's transpose (``fpm_kron_agg`` over the out-edge CSRs);
   * ``NodeClsFn`` / ``SinkhornFn`` / ``SoftTopkFn`` (``fpm_soft_topk_bwd``, incl. the anchors);
-  * ``AfauFn``         AFA-U: HIP forward, backward by replaying ``afau_torch`` under autograd
-    (``ks`` reads ``ss.detach()``, ngm.py:398, so only the regressor's parameters get gradients).
+  * ``AfauFn``         AFA-U: fp32 HIP forward keeping its intermediates, hand-written HIP backward
+    (``fpm.afau_grad``: head, max pool, instance norms, FFN / combine products and the cross-set
+    attention with its mixed-score MLP; ``ks`` reads ``ss.detach()``, ngm.py:398, so only the
+    regressor's parameters get gradients).
 
 The MatchClassifier runs as torch conv / batch-norm (MIOpen) in train mode (batch statistics,
 running buffers updated), like the reference module.  The Hungarian + greedy selection carry no
 gradient (``perm_mat`` is a constant mask of ``s``, ngm.py:444-453).  Gradients reach every
 parameter of the matcher and the node / global feature rows; the backbone is not trained here.
 """
+import os
+
 import torch
 import torch.nn.functional as F
 
 from . import _lib
+from . import afau_grad
 from . import afau_torch
 from . import config as C
 from . import ops
@@ -323,17 +328,30 @@ class SoftTopkFn(torch.autograd.Function):
 
 
 class AfauFn(torch.autograd.Function):
-    """ks from the HIP AFA-U forward; gradients by replaying ``afau_torch`` under autograd."""
+    """ks from the fp32 HIP AFA-U forward with its intermediates kept; gradients from the
+    hand-written HIP backward (``fpm.afau_grad``, ``csrc/afau_bwd.hip``).  ``FPM_AFAU_BWD=replay``
+    selects the earlier device replay of ``afau_torch`` under autograd (kept as a cross-check)."""
 
     @staticmethod
     def forward(ctx, ss, net, bt, *params):
-        ks = net._afau(net.packed(ss.device), ss.detach().contiguous(), bt)
         ctx.net, ctx.bt = net, bt
-        ctx.save_for_backward(ss, *params)
+        ctx.replay = os.environ.get("FPM_AFAU_BWD", "hip") == "replay"
+        if ctx.replay:
+            ks = net._afau(net.packed(ss.device), ss.detach().contiguous(), bt)
+            ctx.save_for_backward(ss, *params)
+            return ks
+        pd = dict(zip(net._afau_names, params))
+        ks, ctx.sv = afau_grad.forward(lambda k: pd[k], ss, bt)
+        ctx.save_for_backward(*params)
         return ks
 
     @staticmethod
     def backward(ctx, gks):
+        if not ctx.replay:
+            params = ctx.saved_tensors
+            pd = dict(zip(ctx.net._afau_names, params))
+            grads = afau_grad.backward(lambda k: pd[k], ctx.sv, gks.contiguous().float(), ctx.net._afau_names)
+            return (None, None, None) + tuple(grads)
         ss, *params = ctx.saved_tensors
         net, bt = ctx.net, ctx.bt
         names = net._afau_names

@@ -155,16 +155,45 @@ int fpm_node_classifier(const float* X, int B, int n1max, int n2max, const float
 /* ---- AFA-U k regressor (ngm.py:386-412, src/model/afau.py) ------------------------------------
  * crossset_attn: the row block's multi-head cross-set attention (afau.py:99-142) -> out rows of
  * 256 = 16 heads x 16; dtype 0 = fp32, 1 = bf16, 2 = split bf16 rows [hi | lo | hi] (768 wide, the
- * A operand of the near-fp32 combine product, see fpm_split_bf16x3). */
+ * A operand of the near-fp32 combine product, see fpm_split_bf16x3).  stats (optional, training):
+ * per (pair, row, head) the softmax's (max score, sum of exp(score - max)), float2[B][n1max][16]. */
 int fpm_crossset_attn_fwd(int dtype, const float* cost, long c_sb, long c_ld, int B, int n1max, int n2max,
                           const int* n2, const float* Wv, int emb, const float* mix1w, const float* mix1b,
-                          const float* mix2w, const float* mix2b, void* out, void* stream);
+                          const float* mix2w, const float* mix2b, void* out, float* stats, void* stream);
 int fpm_instnorm(int dtype, const float* in1, const float* in2, int B, int P, int Cn, const int* nvalid,
                  const float* onehot_bias, const float* w, const float* bias, float eps, float* out_f, void* out_t,
                  int ldt, float* gmax, void* stream);
 int fpm_afau_head(const float* gr, const float* gc, int B, int E, const float* r0w, const float* r0b,
                   const float* r2w, const float* r2b, const float* c0w, const float* c0b, const float* c2w,
                   const float* c2b, float* ks, void* stream);
+
+/* ---- AFA-U backward (training, src/model/afau.py:54-300 through ks_loss, training_loop.py:60) ---
+ * fpm_afau_head_bwd: ks = sigmoid((final_row(gr) + final_col(gc)) / 2) -> dgr, dgc (B x E) and
+ *   per-pair parameter partials part[b] = 2 x [dW0 (8 x E) | db0 (8) | dw2 (8) | db2] (row, col).
+ * fpm_instnorm_bwd: InstanceNorm1d over positions (afau.py:154-176), input in1 (+ in2) or the col
+ *   block's one-hot + bias; seed dy (dense) or gseed (max-pool gradient routed to the argmax);
+ *   dx (optional, accumulate) and per-pair dw / db partials (B x Cn).
+ * fpm_afau_attn_bwd: the row block's cross-set attention (afau.py:231-300 with R0 = 0) given the
+ *   forward's output and softmax stats: per-pair dWv partials (B x 256 x n2max) and mixed-score
+ *   partials (B x 16 x 49 = [dW2 | dW1 row 1 | db1 | db2]).
+ * fpm_rows_sum: out[u][k] (+)= sum_b in[b][k] in order over the b with key[b] == u, or (key NULL)
+ *   over the u-th of nkeys contiguous row chunks (deterministic).
+ * fpm_transpose: out[c][r] = in[r][c], rows [R, ldo) of out zero.
+ * fpm_elementwise: mode 0 x *= (ref > 0) (ReLU backward), mode 1 x += ref. */
+int fpm_afau_head_bwd(const float* gr, const float* gc, int B, int E, const float* r0w, const float* r0b,
+                      const float* r2w, const float* r2b, const float* c0w, const float* c0b, const float* c2w,
+                      const float* c2b, const float* dks, float* dgr, float* dgc, float* part, void* stream);
+int fpm_instnorm_bwd(const float* in1, const float* in2, int B, int P, int Cn, const int* nvalid,
+                     const float* onehot_bias, const float* w, const float* bias, float eps, const float* dy,
+                     const float* gseed, float* dx, int accumulate, float* dw_part, float* db_part, void* stream);
+int fpm_afau_attn_bwd(const float* cost, long c_sb, long c_ld, int B, int n1max, int n2max, const int* n2,
+                      const float* Wv, int emb, const float* mix1w, const float* mix1b, const float* mix2w,
+                      const float* mix2b, const float* att_out, const float* datt, const float* stats,
+                      float* dwv_part, float* mix_part, void* stream);
+int fpm_rows_sum(const float* in, int B, long K, const int* key, int nkeys, float* out, int accumulate,
+                 void* stream);
+int fpm_transpose(const float* in, long R, int C, long ldi, float* out, long ldo, void* stream);
+int fpm_elementwise(float* x, const float* ref, long n, int mode, void* stream);
 
 /* ---- MatchClassifier (ngm.py:75-106, applied at :451-455) -------------------------------------
  * dtype 0: conv2 on fp32 matrix cores (exact fp32 products, parity mode); 1: conv2 operands in

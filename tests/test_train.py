@@ -346,3 +346,47 @@ def test_train_step_bf16_finite(sd):
     for k, p in net.named_parameters():
         if p.grad is not None:
             assert torch.isfinite(p.grad).all(), k
+
+
+@pytest.mark.parametrize("n1s,n2s", [((40, 40, 40, 40), (40, 40, 40, 40)), ((37, 40, 25, 40), (40, 31, 40, 31))])
+def test_afau_hip_backward_vs_replay(sd, n1s, n2s):
+    """The hand-written AFA-U backward (fpm.afau_grad / csrc/afau_bwd.hip) against autograd through
+    the device statement of the regressor (fpm.afau_torch, pinned to the oracle in float64 by
+    tests/test_train_cpu.py) at the same ss and d(ks): every regressor parameter, relative to its
+    group's gradient scale.  Zero-gradient parameters (Wq, Wk, the dot-product row of mix1, the col
+    block's attention, combine biases in front of an instance norm) are exactly 0 here."""
+    import os
+    from fpm import afau_torch, afau_grad
+    g = torch.Generator().manual_seed(sum(n1s) + sum(n2s))
+    B, n1max, n2max = len(n1s), max(n1s), max(n2s)
+    ss = torch.zeros(B, n1max, n2max)
+    for b in range(B):
+        ss[b, :n1s[b], :n2s[b]] = torch.softmax(torch.randn(n1s[b], n2s[b], generator=g) * 3, dim=1)
+    pairs = synth.make_batch(5, B, list(n1s), n2=list(n2s))
+    bt = DeviceBatch.from_pairs(pairs, DEV)
+    names = [k for k in sd if k.startswith(afau_torch.AFAU_PARAM_PREFIXES) and sd[k].is_floating_point()]
+    prm = {k: sd[k].to(DEV).float() for k in names}
+    ssd = ss.to(DEV)
+    ks, sv = afau_grad.forward(lambda k: prm[k], ssd, bt)
+    dks = torch.randn(B, generator=g).to(DEV)
+    grads = dict(zip(names, afau_grad.backward(lambda k: prm[k], sv, dks, names)))
+    leaves = {k: v.clone().requires_grad_(True) for k, v in prm.items()}
+    ks_ref = afau_torch.afau_ks(ssd, torch.tensor(n1s, device=DEV), torch.tensor(n2s, device=DEV),
+                                lambda k: leaves[k])
+    assert (ks - ks_ref).abs().max() < 1e-5
+    (ks_ref * dks).sum().backward()
+    scale = {}
+    for k in names:
+        grp = k.split(".")[0] + ("." + k.split(".")[3] if k.startswith("encoder_k") else "")
+        if leaves[k].grad is not None:
+            scale[grp] = max(scale.get(grp, 0.0), float(leaves[k].grad.abs().max()))
+    for k in names:
+        grp = k.split(".")[0] + ("." + k.split(".")[3] if k.startswith("encoder_k") else "")
+        ref = leaves[k].grad
+        got = grads[k].cpu()
+        if ref is None or k.endswith(("Wq.weight", "Wk.weight")):
+            assert float(got.abs().max()) == 0.0, k
+            continue
+        tol = 2e-3 * max(scale[grp], 1e-12)
+        err = float((got - ref.cpu()).abs().max())
+        assert err <= tol or k.endswith("multi_head_combine.bias"), (k, err, tol)

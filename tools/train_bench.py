@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--cpu-pairs", type=int, default=2)
+    ap.add_argument("--no-regression", action="store_true", help="Net(regression=False): no AFA-U")
     args = ap.parse_args()
     import torch
     import fpm
@@ -40,7 +41,7 @@ def main():
     gt = torch.zeros(B, n, n, device=dev)
     gt[:, torch.arange(n), torch.arange(n)] = 1.0
     label = (torch.arange(B, device=dev) % 2).float()
-    net = fpm.Net(regression=True, backbone=False, dtype=args.dtype)
+    net = fpm.Net(regression=not args.no_regression, backbone=False, dtype=args.dtype)
     net.load_state_dict(sd)
     net.to(dev).train()
     opt = torch.optim.AdamW([p for p in net.parameters() if p.requires_grad], lr=1e-4, weight_decay=1e-4)
