@@ -272,52 +272,79 @@ __global__ __launch_bounds__(256) void afau_attn_bwd_kernel(const float* __restr
             dwv[u][d] = 0.f;
         }
     }
-    float gw2[16], gw1[16], gb1[16], gb2 = 0.f;
+    // gb1 is a bias-like sum: sum_j ds_ij = 0 in every row (softmax), so sum over the active entries
+    // = -(sum over the inactive ones); both are accumulated and the one over fewer entries is used
+    // (a unit active on all of [0, 1] then gets its exact gradient 0 instead of cancellation noise).
+    // mix2_bias shifts every score of a head: its gradient is exactly 0 (gb2 is not accumulated).
+    float gw2[16], gw1[16], gb1[16], gb1n[16];
+    int nact[16];
 #pragma unroll
-    for (int m = 0; m < 16; ++m) gw2[m] = gw1[m] = gb1[m] = 0.f;
+    for (int m = 0; m < 16; ++m) {
+        gw2[m] = gw1[m] = gb1[m] = gb1n[m] = 0.f;
+        nact[m] = 0;
+    }
+    int ntot = 0;
     const float* Cb = cost + (long)b * c_sb;
+    __shared__ float dred[2][4];
     for (int i = 0; i < n1max; ++i) {
         const long row = (long)b * n1max + i;
         float da[16];
-        float dot = 0.f;
 #pragma unroll
-        for (int d = 0; d < 16; ++d) {
-            da[d] = datt[row * 256 + h * 16 + d];
-            dot = fmaf(da[d], att_out[row * 256 + h * 16 + d], dot);
-        }
+        for (int d = 0; d < 16; ++d) da[d] = datt[row * 256 + h * 16 + d];
         const float2 st = stats[row * 16 + h];
         const float invS = 1.f / st.y;
+        float cj[TJ], att[TJ], dA[TJ];
+        float part = 0.f;
+#pragma unroll
+        for (int u = 0; u < TJ; ++u) {
+            const int j = tid + 256 * u;
+            cj[u] = 0.f;
+            att[u] = 0.f;
+            dA[u] = 0.f;
+            if (j >= n2max) continue;
+            const float c = Cb[(long)i * c_ld + j];
+            float sc = 0.f;
+#pragma unroll
+            for (int m = 0; m < 16; ++m) sc += fmaxf(c * w1[m] + b1[m], 0.f) * w2[m];
+            sc += b2;
+            cj[u] = c;
+            att[u] = expf(sc - st.x) * invS;
+            float a = 0.f;
+#pragma unroll
+            for (int d = 0; d < 16; ++d) a = fmaf(da[d], vj[u][d], a);
+            dA[u] = a;
+            part = fmaf(att[u], a, part);
+        }
+        // the softmax backward's row term sum_j att dA, reduced exactly over the row (not taken
+        // as datt . out from the forward: the bias-like parameters' true gradient is a sum with
+        // heavy cancellation, which a 1-ulp mismatch between the two would bias)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+        if (lane == 0) dred[i & 1][wv] = part;
+        __syncthreads();
+        const float dot = ((dred[i & 1][0] + dred[i & 1][1]) + dred[i & 1][2]) + dred[i & 1][3];
 #pragma unroll
         for (int u = 0; u < TJ; ++u) {
             const int j = tid + 256 * u;
             if (j >= n2max) continue;
-            const float c = Cb[(long)i * c_ld + j];
-            float pre[16];
-            float sc = 0.f;
+            const float c = cj[u];
+#pragma unroll
+            for (int d = 0; d < 16; ++d) dwv[u][d] = fmaf(att[u], da[d], dwv[u][d]);
+            const float ds = att[u] * (dA[u] - dot);
+            ++ntot;
 #pragma unroll
             for (int m = 0; m < 16; ++m) {
-                pre[m] = c * w1[m] + b1[m];
-                sc += fmaxf(pre[m], 0.f) * w2[m];
-            }
-            sc += b2;
-            const float att = expf(sc - st.x) * invS;
-            float dA = 0.f;
-#pragma unroll
-            for (int d = 0; d < 16; ++d) {
-                dA = fmaf(da[d], vj[u][d], dA);
-                dwv[u][d] = fmaf(att, da[d], dwv[u][d]);
-            }
-            const float ds = att * (dA - dot);
-#pragma unroll
-            for (int m = 0; m < 16; ++m) {
-                if (pre[m] > 0.f) {
-                    gw2[m] = fmaf(ds, pre[m], gw2[m]);
+                const float pre = c * w1[m] + b1[m];
+                if (pre > 0.f) {
+                    gw2[m] = fmaf(ds, pre, gw2[m]);
                     const float t = ds * w2[m];
                     gw1[m] = fmaf(t, c, gw1[m]);
                     gb1[m] += t;
+                    ++nact[m];
+                } else {
+                    gb1n[m] = fmaf(ds, w2[m], gb1n[m]);
                 }
             }
-            gb2 += ds;
         }
     }
 #pragma unroll
@@ -333,19 +360,39 @@ __global__ __launch_bounds__(256) void afau_attn_bwd_kernel(const float* __restr
         for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
         return x;
     };
+    auto isum = [&](int x) {
+        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+        return x;
+    };
+    __shared__ float redn[16][4];
+    __shared__ int cnt[17][4];
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
-        const float a = wsum(gw2[m]), e = wsum(gw1[m]), f = wsum(gb1[m]);
+        const float a = wsum(gw2[m]), e = wsum(gw1[m]), f = wsum(gb1[m]), fn = wsum(gb1n[m]);
+        const int na = isum(nact[m]);
         if (lane == 0) {
             red[m][wv] = a;
             red[16 + m][wv] = e;
             red[32 + m][wv] = f;
+            redn[m][wv] = fn;
+            cnt[m][wv] = na;
         }
     }
-    const float g2s = wsum(gb2);
-    if (lane == 0) red[48][wv] = g2s;
+    const int nt = isum(ntot);
+    if (lane == 0) cnt[16][wv] = nt;
     __syncthreads();
-    if (tid < 49) mix_part[((long)b * 16 + h) * 49 + tid] = red[tid][0] + red[tid][1] + red[tid][2] + red[tid][3];
+    float* mp = mix_part + ((long)b * 16 + h) * 49;
+    if (tid < 48) {
+        float v = red[tid][0] + red[tid][1] + red[tid][2] + red[tid][3];
+        if (tid >= 32) {
+            const int m = tid - 32;
+            const int na = cnt[m][0] + cnt[m][1] + cnt[m][2] + cnt[m][3];
+            const int nn = cnt[16][0] + cnt[16][1] + cnt[16][2] + cnt[16][3] - na;
+            if (nn < na) v = -(redn[m][0] + redn[m][1] + redn[m][2] + redn[m][3]);
+        }
+        mp[tid] = v;
+    }
+    if (tid == 48) mp[48] = 0.f;
 }
 
 // out[u][k] (+)= sum of in[b][k] over b in order: with key, the b with key[b] == u; without, the

@@ -241,8 +241,9 @@ def node_classifier(X, B, n1max, n2max, w, b, out, vpart=None):
     _lib.call("fpm_node_classifier", _p(X), B, n1max, n2max, _p(w), _p(b), _p(vpart), _p(out), _stream(X))
 
 
-def crossset_attn(cost, n2, Wv, mix1w, mix1b, mix2w, mix2b, out, split=False):
-    """``split``: out is (B * n1max, 768) bf16 [hi | lo | hi] rows (near-fp32 operand)."""
+def crossset_attn(cost, n2, Wv, mix1w, mix1b, mix2w, mix2b, out, split=False, stats=None):
+    """``split``: out is (B * n1max, 768) bf16 [hi | lo | hi] rows (near-fp32 operand); ``stats``:
+    optional (B * n1max, 16, 2) fp32 softmax (max, sum) per row and head (training)."""
     _dev(cost, n2, Wv, out)
     B, n1max, n2max = cost.shape
     _shape(out, (B * n1max, 768 if split else 256), "crossset_attn out")
