@@ -498,7 +498,7 @@ extern "C" int fpm_rows_sum(const float* in, int B, long K, const int* key, int 
     FPM_CHECK_ARG(B >= 0 && K >= 0 && nkeys > 0, "rows_sum: bad sizes");
     if (K == 0) return 0;
     dim3 grid((unsigned)((K + 255) / 256), nkeys);
-    hipLaunchKernelGGL(rows_sum_kernel, grid, dim3(256), 0, (hipStream_t)stream, in, B, K, key, key ? nkeys : 1, out,
+    hipLaunchKernelGGL(rows_sum_kernel, grid, dim3(256), 0, (hipStream_t)stream, in, B, K, key, nkeys, out,
                        accumulate);
     return fpm::check_launch("fpm_rows_sum");
 }

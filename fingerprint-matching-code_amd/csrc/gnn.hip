@@ -398,7 +398,7 @@ int& gnn_group1_flag() {
 int& gnn_wide_flag() {
     static int u = [] {
         const char* e = getenv("FPM_GNN_WIDE");
-        return e ? atoi(e) : 1;
+        return e ? atoi(e) : 0;
     }();
     return u;
 }
@@ -408,7 +408,7 @@ int& gnn_wide_flag() {
 int& gnn_il_flag() {
     static int u = [] {
         const char* e = getenv("FPM_GNN_IL");
-        return e ? atoi(e) : 1;
+        return e ? atoi(e) : 0;
     }();
     return u;
 }
