@@ -404,3 +404,59 @@ extern "C" int fpm_soft_topk_bwd(const float* ss, long sb, long ld, const int* n
                        tau, dds, db, dld, dss, n1max, n2max, (float2*)ws, status);
     return fpm::check_launch("fpm_soft_topk_bwd");
 }
+
+// ---- small-weight gradient reductions of the GNN layers (gnn.py:207-226 parameters) ---------
+// out[o][c] = sum_{b, p} U[b][o][p] V[b][c][p] (and, with ones, out[o][C] = sum U[b][o][p]):
+// the (O x K)(K x C) products with K = B * N (millions of positions) and O, C <= 17.  One
+// workgroup per (pair, slice of <= 4096 positions) stages 256-position tiles of U and V in LDS
+// (rows padded to 257 floats: conflict-free column reads) and thread q = o * (C + ones) + c keeps
+// one accumulator; per-workgroup partials part[b * S + s][q] are summed in order by fpm_rows_sum.
+namespace {
+constexpr int OS_T = 256, OS_L = 4096, OS_MAXC = 17;
+__global__ __launch_bounds__(512) void outer_sum_kernel(const float* __restrict__ U, long sUb, long sUo, int O,
+                                                        const float* __restrict__ V, long sVb, long sVc, int Cc,
+                                                        int ones, long N, int S, float* __restrict__ part) {
+    __shared__ float Ut[OS_MAXC][OS_T + 1], Vt[OS_MAXC][OS_T + 1];
+    const int b = blockIdx.x / S, s = blockIdx.x % S, t = threadIdx.x;
+    const int C1 = Cc + ones, nq = O * C1;
+    const int o = t / C1, c = t - o * C1;
+    const long p0 = (long)s * OS_L, p1 = min(N, p0 + OS_L);
+    float acc = 0.f;
+    for (long q0 = p0; q0 < p1; q0 += OS_T) {
+        const int len = (int)min((long)OS_T, p1 - q0);
+        for (int k = t; k < O * OS_T; k += 512) {
+            const int r = k / OS_T, p = k - r * OS_T;
+            Ut[r][p] = p < len ? U[b * sUb + r * sUo + q0 + p] : 0.f;
+        }
+        for (int k = t; k < Cc * OS_T; k += 512) {
+            const int r = k / OS_T, p = k - r * OS_T;
+            Vt[r][p] = p < len ? V[b * sVb + r * sVc + q0 + p] : 0.f;
+        }
+        __syncthreads();
+        if (t < nq) {
+            if (c < Cc) {
+#pragma unroll 8
+                for (int p = 0; p < OS_T; ++p) acc = fmaf(Ut[o][p], Vt[c][p], acc);
+            } else {
+#pragma unroll 8
+                for (int p = 0; p < OS_T; ++p) acc += Ut[o][p];
+            }
+        }
+        __syncthreads();
+    }
+    if (t < nq) part[(long)blockIdx.x * nq + t] = acc;
+}
+}  // namespace
+
+extern "C" long fpm_outer_sum_parts(int B, long N) { return (long)B * ((N + OS_L - 1) / OS_L); }
+
+extern "C" int fpm_outer_sum(const float* U, long sUb, long sUo, int O, const float* V, long sVb, long sVc, int Cc,
+                             int ones, int B, long N, float* part, void* stream) {
+    FPM_CHECK_ARG(O > 0 && O <= OS_MAXC && Cc >= 0 && Cc <= OS_MAXC && O * (Cc + (ones != 0)) <= 512 && N > 0,
+                  "outer_sum: 0 < O, C <= 17 required");
+    if (B == 0) return 0;
+    const int S = (int)((N + OS_L - 1) / OS_L);
+    hipLaunchKernelGGL(outer_sum_kernel, dim3((unsigned)(B * S)), dim3(512), 0, (hipStream_t)stream, U, sUb, sUo, O, V,
+                       sVb, sVc, Cc, ones != 0, N, S, part);
+    return fpm::check_launch("fpm_outer_sum");
+}

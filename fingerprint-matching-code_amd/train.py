@@ -168,11 +168,28 @@ class AffinityFn(torch.autograd.Function):
         return dx1.reshape(B * n1max, D), dx2.reshape(B * n2max, D), dcoef, None, None
 
 
-def _outer_sum(U, V):
-    """sum_{b,p} U[b,:,p] (x) V[b,:,p] -> (O, C) for channel-major U (B, O, N), V (B, C, N).
-    A single (O x K) (K x C) product with K = B*N (millions) and O, C <= 17 gets one workgroup
-    from the library; splitting K into 1024-long slices gives B*N/1024 small products in one
-    batched GEMM, then a sum over the slices."""
+def _outer_sum(U, V, ones=False):
+    """sum_{b,p} U[b,:,p] (x) V[b,:,p] -> (O, C) for channel-major U (B, O, N), V (B, C, N) with unit
+    position stride (fpm_outer_sum: per-workgroup partials over 4096-position slices, summed in
+    order).  ``ones``: also sum_{b,p} U[b,:,p] (the bias gradient) -> ((O, C), (O,))."""
+    B, O, N = U.shape
+    Cc = V.shape[1] if V is not None else 0
+    if U.stride(2) != 1 or (V is not None and V.stride(2) != 1):
+        raise _lib.FpmError("outer_sum: unit position stride required")
+    rows = int(_lib.load().fpm_outer_sum_parts(B, N))
+    C1 = Cc + (1 if ones else 0)
+    part = torch.empty(rows, O * C1, device=U.device, dtype=torch.float32)
+    _lib.call("fpm_outer_sum", ops._p(U), U.stride(0), U.stride(1), O, ops._p(V), V.stride(0) if V is not None else 0,
+              V.stride(1) if V is not None else 0, Cc, int(ones), B, N, ops._p(part), ops._stream(U))
+    tot = afau_grad.rows_sum(part).view(O, C1)
+    if ones:
+        return tot[:, :Cc], tot[:, Cc]
+    return tot
+
+
+def _outer_sum_torch(U, V):
+    """The earlier library form of _outer_sum (batched GEMM over 1024-long slices, then a sum);
+    kept for the A/B check in tests."""
     B, O, N = U.shape
     Cc = V.shape[1]
     q = N
@@ -238,14 +255,10 @@ class GnnLayerFn(torch.autograd.Function):
         ops.gnn_layer_bwd_point(Xc, Cin, B, n1max, n2max, gXn, dz, _gnn_pack(Wl, bl, Wr, W1, b1, W2, b2, wc, bc), dX,
                                 dagg, V)
         dx1, dh1, dm, h1 = V[:, 0:16], V[:, 16:32], V[:, 32:48], V[:, 48:64]
-        dwc = _outer_sum(dz[:, None], x1)
-        dbc = dz.sum().reshape(1)
-        dW2 = _outer_sum(dm, h1)
-        db2 = dm.sum((0, 2))
-        dW1 = _outer_sum(dh1, Xf)
-        db1 = dh1.sum((0, 2))
-        dWl = _outer_sum(dx1, agg)
-        dbl = dx1.sum((0, 2))
+        dwc, dbc = _outer_sum(dz[:, None], x1, ones=True)
+        dW2, db2 = _outer_sum(dm, h1, ones=True)
+        dW1, db1 = _outer_sum(dh1, Xf, ones=True)
+        dWl, dbl = _outer_sum(dx1, agg, ones=True)
         dWr = _outer_sum(dx1, Xf)
         dXa = torch.empty(B, Cin, n2max, n1max, device=Xc.device, dtype=torch.float32)
         ops.kron_agg(dagg.view(B, Cin, n2max, n1max), Cin, B, n1max, n2max, g.s0.out_csr(), g.s1.out_csr(),
@@ -272,8 +285,7 @@ class NodeClsFn(torch.autograd.Function):
         gT = gs.transpose(1, 2)                                    # (B, n2max, n1max)
         dX = w.reshape(-1)[None, :, None, None] * gT[:, None]
         B = X.shape[0]
-        dw = _outer_sum(gT.reshape(B, 1, -1), X.reshape(B, X.shape[1], -1))
-        db = gs.sum().reshape(1)
+        dw, db = _outer_sum(gT.reshape(B, 1, -1).contiguous(), X.reshape(B, X.shape[1], -1), ones=True)
         return dX, dw, db, None
 
 

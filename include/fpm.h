@@ -195,6 +195,14 @@ int fpm_rows_sum(const float* in, int B, long K, const int* key, int nkeys, floa
 int fpm_transpose(const float* in, long R, int C, long ldi, float* out, long ldo, void* stream);
 int fpm_elementwise(float* x, const float* ref, long n, int mode, void* stream);
 
+/* ---- GNN weight-gradient reductions (training, gnn.py:207-226 parameters) --------------------
+ * part[w][o * (C + ones) + c] over fpm_outer_sum_parts(B, N) rows w: per-workgroup partial sums of
+ * U[b][o][p] V[b][c][p] (and of U[b][o][p] alone in column C when ones != 0); strides in elements;
+ * O, C <= 17.  The caller sums the rows (fpm_rows_sum). */
+long fpm_outer_sum_parts(int B, long N);
+int fpm_outer_sum(const float* U, long sUb, long sUo, int O, const float* V, long sVb, long sVc, int Cc, int ones,
+                  int B, long N, float* part, void* stream);
+
 /* ---- MatchClassifier (ngm.py:75-106, applied at :451-455) -------------------------------------
  * dtype 0: conv2 on fp32 matrix cores (exact fp32 products, parity mode); 1: conv2 operands in
  * bf16 (fp32 accumulation, the bf16 throughput mode). */

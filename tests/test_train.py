@@ -396,3 +396,18 @@ def test_afau_hip_backward_vs_replay(sd, n1s, n2s):
         tol = 2e-3 * max(scale[grp], 1e-12)
         err = float((got - ref.cpu()).abs().max())
         assert err <= tol or k.endswith("multi_head_combine.bias"), (k, err, tol)
+
+
+def test_outer_sum_kernel():
+    """fpm_outer_sum (GNN weight / bias gradient reductions) against the float64 sums, incl. strided
+    channel views and a ragged slice count."""
+    from fpm.train import _outer_sum
+    g = torch.Generator().manual_seed(44)
+    for B, O, Cc, N in ((3, 16, 17, 10000), (2, 1, 16, 65536), (4, 16, 1, 333)):
+        U = torch.randn(B, O + 1, N, generator=g)[:, 1:]          # strided channel view
+        V = torch.randn(B, Cc, N, generator=g)
+        w, bsum = _outer_sum(U.to(DEV), V.to(DEV), ones=True)
+        ref = torch.einsum("bon,bcn->oc", U.double(), V.double())
+        assert (w.cpu().double() - ref).abs().max() < 1e-4 * ref.abs().max()
+        assert (bsum.cpu().double() - U.double().sum((0, 2))).abs().max() < 1e-4 * max(1.0, float(U.abs().sum()) / N)
+        assert torch.equal(_outer_sum(U.to(DEV), V.to(DEV)), w)
