@@ -92,6 +92,14 @@ class DeviceBatch:
             out.pair_range = self.pair_range
         return out
 
+    def max_graph_edges(self, side):
+        """Largest edge count of one graph on ``side`` (host edge offsets; 0 when unknown): lets the
+        spline plan use its per-graph kernels."""
+        if self.edge_off is None:
+            return 0
+        off = torch.as_tensor(self.edge_off[side])
+        return int((off[1:] - off[:-1]).max()) if off.numel() > 1 else 0
+
     @property
     def n1(self):
         return self.n[0]

@@ -326,6 +326,240 @@ __global__ void plan_expand_kernel(const int* __restrict__ src, const int* __res
     basis4[p] = *(const float4*)(basis_e + 4 * (long)e);
 }
 
+// ---- per-graph plan (graphs of <= 4096 directed edges and <= 1024 nodes) ---------------------
+// The same plan as the global kernels above, built one workgroup per graph with LDS instead of
+// device-wide atomics: a graph's edges are a contiguous range (every batch builder groups them by
+// graph, so src is non-decreasing across graph boundaries and the range is found by binary
+// search), its nodes are [g nmax, (g + 1) nmax), and its dst CSR occupies exactly its edge range.
+// Output fields and orders are identical (cell rows in node order, in-edges by ascending source
+// then edge id), so everything downstream is bit-identical to the global path.
+constexpr int PG_MAXE = 4096, PG_MAXN = 1024, PG_THREADS = 512;
+
+__device__ __forceinline__ long pg_lower_bound(const int* __restrict__ a, long n, int v) {
+    long lo = 0, hi = n;
+    while (lo < hi) {
+        const long mid = (lo + hi) >> 1;
+        if (a[mid] < v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// K1: edge basis / group, node cell masks, per-graph cell counts, dst CSR (sorted in LDS)
+__global__ __launch_bounds__(PG_THREADS) void plan_graph_kernel(const int* __restrict__ src,
+                                                                const int* __restrict__ dst,
+                                                                const float* __restrict__ pseudo, long E, int nmax,
+                                                                int ngraphs, int* __restrict__ mask,
+                                                                float* __restrict__ basis_e, int* __restrict__ grp_e,
+                                                                int* __restrict__ cellcnt, int* __restrict__ dst_ptr,
+                                                                int* __restrict__ csr_e, int* __restrict__ nbr_local,
+                                                                int* __restrict__ eoff) {
+    __shared__ unsigned key[PG_MAXE];
+    __shared__ int maskL[PG_MAXN], cnt[PG_MAXN];
+    __shared__ long range[2];
+    __shared__ int ccount[NCELL];
+    const int g = blockIdx.x, tid = threadIdx.x;
+    const int base = g * nmax;
+    if (tid == 0) range[0] = pg_lower_bound(src, E, base);
+    if (tid == 1) range[1] = pg_lower_bound(src, E, base + nmax);
+    for (int u = tid; u < nmax; u += PG_THREADS) {
+        maskL[u] = 0;
+        cnt[u] = 0;
+    }
+    if (tid < NCELL) ccount[tid] = 0;
+    __syncthreads();
+    const long e0 = range[0];
+    const int ne = (int)(range[1] - e0);
+    if (tid == 0) eoff[g] = (int)e0;
+    if (tid == 0 && g == ngraphs - 1) eoff[ngraphs] = (int)E;
+    int npow = 1;
+    while (npow < ne) npow <<= 1;
+    for (int t = tid; t < npow; t += PG_THREADS) {
+        if (t >= ne) {
+            key[t] = 0xffffffffu;
+            continue;
+        }
+        const long e = e0 + t;
+        int f[2];
+        float fr[2];
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+            const float v = pseudo[2 * e + d] * 4.0f;
+            const float fl = floorf(v);
+            f[d] = (int)fl;
+            fr[d] = v - fl;
+        }
+        float b4[4];
+        int bits = 0;
+        const int gg = f[0] + 5 * f[1];
+#pragma unroll
+        for (int sidx = 0; sidx < 4; ++sidx) {
+            float bb = 1.0f;
+            bb = bb * ((sidx & 1) ? fr[0] : 1.0f - fr[0]);
+            bb = bb * ((sidx >> 1) ? fr[1] : 1.0f - fr[1]);
+            b4[sidx] = bb;
+            bits |= 1 << fpm::spline_cell(gg, sidx);
+        }
+        grp_e[e] = gg;
+        *(float4*)(basis_e + 4 * e) = make_float4(b4[0], b4[1], b4[2], b4[3]);
+        const int su = src[e] - base, du = dst[e] - base;
+        atomicOr(&maskL[su], bits);
+        atomicAdd(&cnt[du], 1);
+        key[t] = ((unsigned)du << 22) | ((unsigned)su << 12) | (unsigned)t;
+    }
+    __syncthreads();
+    // bitonic sort of (dst, src, edge) keys, ascending
+    for (int size = 2; size <= npow; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int t = tid; t < npow / 2; t += PG_THREADS) {
+                const int lo = 2 * t - (t & (stride - 1)), hi = lo + stride;
+                const bool up = (lo & size) == 0;
+                const unsigned a = key[lo], b = key[hi];
+                if ((a > b) == up) {
+                    key[lo] = b;
+                    key[hi] = a;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int t = tid; t < ne; t += PG_THREADS) {
+        const unsigned k = key[t];
+        csr_e[e0 + t] = (int)(e0 + (k & 0xfffu));
+        nbr_local[e0 + t] = (int)((k >> 12) & 0x3ffu);
+    }
+    // masks (root bit added by the readers, as in the global path) and per-cell node counts
+    for (int u = tid; u < nmax; u += PG_THREADS) {
+        const int m = maskL[u];
+        mask[base + u] = m;
+        const int mr = m | (1 << 25);
+        for (int k = 0; k < NCELL; ++k)
+            if ((mr >> k) & 1) atomicAdd(&ccount[k], 1);
+    }
+    // dst pointers: exclusive scan of the in-degrees (one wave, nmax <= 1024)
+    if (tid < 64) {
+        int carry = 0;
+        for (int u0 = 0; u0 < nmax; u0 += 64) {
+            const int u = u0 + tid;
+            const int v = u < nmax ? cnt[u] : 0;
+            int incl = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int y = __shfl_up(incl, o);
+                if (tid >= o) incl += y;
+            }
+            if (u < nmax) dst_ptr[base + u] = (int)e0 + carry + incl - v;
+            carry += __shfl(incl, 63);
+        }
+        if (tid == 0 && g == ngraphs - 1) dst_ptr[(long)ngraphs * nmax] = (int)E;
+    }
+    __syncthreads();
+    if (tid < NCELL) cellcnt[g * NCELL + tid] = ccount[tid];
+}
+
+// K2: one block -- per-cell exclusive scan over graphs (in place), cell offsets, tile tables
+__global__ __launch_bounds__(1024) void plan_graph_scan_kernel(int* cellcnt, int ngraphs, int* cell_off,
+                                                               int* tile_info, int max_tiles, int* tile_info2,
+                                                               int max_tiles2) {
+    __shared__ int cell_tot[NCELL], tile_off[NCELL + 1], coff[NCELL + 1];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    for (int k = wv; k < NCELL; k += 16) {
+        int carry = 0;
+        for (int t0 = 0; t0 < ngraphs; t0 += 64) {
+            const int i = t0 + lane;
+            const int v = i < ngraphs ? cellcnt[i * NCELL + k] : 0;
+            int incl = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int y = __shfl_up(incl, o);
+                if (lane >= o) incl += y;
+            }
+            if (i < ngraphs) cellcnt[i * NCELL + k] = carry + incl - v;
+            carry += __shfl(incl, 63);
+        }
+        if (lane == 0) cell_tot[k] = carry;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int off = 0;
+        for (int k = 0; k < NCELL; ++k) {
+            cell_off[k] = off;
+            coff[k] = off;
+            off += cell_tot[k];
+        }
+        cell_off[NCELL] = off;
+        coff[NCELL] = off;
+    }
+    __syncthreads();
+    build_tile_table(coff, cell_tot, tile_off, fpm::GBM, tile_info, max_tiles);
+    build_tile_table(coff, cell_tot, tile_off, fpm::G2_BM, tile_info2, max_tiles2);
+}
+
+// K3: rowid / arows (ranks of the graph's nodes per cell, in node order), then the CSR slots'
+// 4 product rows and basis weights
+__global__ __launch_bounds__(PG_THREADS) void plan_graph_rank_kernel(const int* __restrict__ src, const int* mask,
+                                                                     int nmax, const int* __restrict__ gbase,
+                                                                     const int* __restrict__ cell_off,
+                                                                     const int* __restrict__ eoff,
+                                                                     const int* __restrict__ csr_e,
+                                                                     const int* __restrict__ grp_e,
+                                                                     const float* __restrict__ basis_e, int* rowid,
+                                                                     int* __restrict__ arows, int4* __restrict__ rows4,
+                                                                     float4* __restrict__ basis4) {
+    __shared__ int wc[PG_THREADS / 64][NCELL];
+    __shared__ int run[NCELL];
+    const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const long base = (long)g * nmax;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    if (tid < NCELL) run[tid] = cell_off[tid] + gbase[g * NCELL + tid];
+    __syncthreads();
+    for (int u0 = 0; u0 < nmax; u0 += PG_THREADS) {
+        const int u = u0 + tid;
+        const int m = u < nmax ? (mask[base + u] | (1 << 25)) : 0;
+        int myrank[NCELL];
+#pragma unroll
+        for (int k = 0; k < NCELL; ++k) {
+            const unsigned long long b = __ballot((m >> k) & 1);
+            if (lane == 0) wc[wave][k] = __popcll(b);
+            myrank[k] = __popcll(b & lt);
+        }
+        __syncthreads();
+        if (u < nmax) {
+#pragma unroll
+            for (int k = 0; k < NCELL; ++k) {
+                int r = -1;
+                if ((m >> k) & 1) {
+                    int pre = run[k];
+                    for (int w = 0; w < wave; ++w) pre += wc[w][k];
+                    r = pre + myrank[k];
+                    arows[r] = (int)(base + u);
+                }
+                rowid[(base + u) * NCELL + k] = r;
+            }
+        }
+        __syncthreads();
+        if (tid < NCELL) {
+            int add = 0;
+            for (int w = 0; w < PG_THREADS / 64; ++w) add += wc[w][tid];
+            run[tid] += add;
+        }
+        __syncthreads();
+    }
+    const int e0 = eoff[g], e1 = eoff[g + 1];
+    for (int p = e0 + tid; p < e1; p += PG_THREADS) {
+        const int e = csr_e[p];
+        const int gg = grp_e[e];
+        const long sn = src[e];
+        int4 r;
+        r.x = rowid[sn * NCELL + fpm::spline_cell(gg, 0)];
+        r.y = rowid[sn * NCELL + fpm::spline_cell(gg, 1)];
+        r.z = rowid[sn * NCELL + fpm::spline_cell(gg, 2)];
+        r.w = rowid[sn * NCELL + fpm::spline_cell(gg, 3)];
+        rows4[p] = r;
+        basis4[p] = *(const float4*)(basis_e + 4 * (long)e);
+    }
+}
+
 // out[v] = max_{in-edges e} sum_s basis[e,s] * Y[row(src_e, cell_s)] + Y[root row v] + bias
 //   mode 0: relu(.) ; mode 1: xres[v] + 0.1 * (.)   (+ optional per-pair column scale on out_t)
 // One wave per node, 12 channels per lane (3 x 4 contiguous).
@@ -562,6 +796,48 @@ extern "C" int fpm_spline_plan(const int* src, const int* dst, const float* pseu
                        (const int*)(w + L.grp_e), (const float*)(w + L.basis_e), (const int*)(w + L.rowid),
                        (int4*)(w + L.rows4), (float4*)(w + L.basis4));
     return fpm::check_launch("fpm_spline_plan");
+}
+
+// Per-graph plan when every graph has <= 4096 edges and nmax <= 1024 (max_graph_edges: the
+// caller's bound, e.g. from the batch's host edge offsets); otherwise the global kernels.  The
+// scratch fields blk_cnt (per-graph cell counts / bases) and dslot (graph edge offsets) are reused.
+// per-graph plan kernels (1, default) or the global ones (0); bit-identical.  Env FPM_PLAN_GRAPH or
+// fpm_set_tuning("plan_graph", v)
+int& plan_graph_flag() {
+    static int v = [] {
+        const char* e = getenv("FPM_PLAN_GRAPH");
+        return e ? atoi(e) : 1;
+    }();
+    return v;
+}
+
+extern "C" int fpm_spline_plan_graphs(const int* src, const int* dst, const float* pseudo, long E, long num_nodes,
+                                      int nmax, long max_graph_edges, void* ws, long ws_bytes, void* stream) {
+    const long ngraphs = nmax > 0 ? num_nodes / nmax : 0;
+    // the per-graph path keeps its per-graph cell counts in the indeg scratch (num_nodes ints) and
+    // the graph edge offsets in the dslot scratch (E ints)
+    const bool fits = max_graph_edges > 0 && max_graph_edges <= PG_MAXE && nmax <= PG_MAXN && nmax >= NCELL &&
+                      ngraphs > 0 && ngraphs * nmax == num_nodes && ngraphs + 1 <= E;
+    if (!fits || plan_graph_flag() == 0)
+        return fpm_spline_plan(src, dst, pseudo, E, num_nodes, nmax, ws, ws_bytes, stream);
+    PlanLayout L = plan_layout(E, num_nodes);
+    FPM_CHECK_ARG(ws_bytes >= L.total, "spline_plan: workspace too small");
+    FPM_CHECK_ARG(num_nodes * NCELL < (1L << 31) && L.max_rows < (1L << 31), "spline_plan: batch too large");
+    char* w = (char*)ws;
+    hipStream_t st = (hipStream_t)stream;
+    int* gcnt = (int*)(w + L.indeg);
+    int* eoff = (int*)(w + L.dslot);
+    hipLaunchKernelGGL(plan_graph_kernel, dim3((unsigned)ngraphs), dim3(PG_THREADS), 0, st, src, dst, pseudo, E, nmax,
+                       (int)ngraphs, (int*)(w + L.mask), (float*)(w + L.basis_e), (int*)(w + L.grp_e), gcnt,
+                       (int*)(w + L.dst_ptr), (int*)(w + L.csr_e), (int*)(w + L.nbr_local), eoff);
+    hipLaunchKernelGGL(plan_graph_scan_kernel, dim3(1), dim3(1024), 0, st, gcnt, (int)ngraphs, (int*)(w + L.cell_off),
+                       (int*)(w + L.tile_info), (int)L.max_tiles, (int*)(w + L.tile_info2), (int)L.max_tiles2);
+    hipLaunchKernelGGL(plan_graph_rank_kernel, dim3((unsigned)ngraphs), dim3(PG_THREADS), 0, st, src,
+                       (const int*)(w + L.mask), nmax, (const int*)gcnt, (const int*)(w + L.cell_off),
+                       (const int*)eoff, (const int*)(w + L.csr_e), (const int*)(w + L.grp_e),
+                       (const float*)(w + L.basis_e), (int*)(w + L.rowid), (int*)(w + L.arows), (int4*)(w + L.rows4),
+                       (float4*)(w + L.basis4));
+    return fpm::check_launch("fpm_spline_plan_graphs");
 }
 
 // Pointers into the plan for the GNN layer (dst CSR with local neighbour indices).

@@ -227,7 +227,8 @@ class Net(nn.Module):
         op = torch.bfloat16 if self.dtype_mode == "bf16" else torch.float32
         nn_ = bt.B * bt.nmax[side]
         E = bt.E[side]
-        plan = ops.spline_plan(bt.src[side], bt.dst[side], bt.pseudo[side], nn_, bt.nmax[side])
+        plan = ops.spline_plan(bt.src[side], bt.dst[side], bt.pseudo[side], nn_, bt.nmax[side],
+                               bt.max_graph_edges(side))
         if side == 0 and bt.shared0 and bt.B > 1:
             return (plan,) + self._spline_shared(wp, bt, cscale)
         x0 = bt.x[side]
@@ -249,7 +250,7 @@ class Net(nn.Module):
         nm = bt.nmax[0]
         e0 = int(bt.edge_off[0][1])
         src, dst, ps = bt.src[0][:e0], bt.dst[0][:e0], bt.pseudo[0][:e0]
-        plan = ops.spline_plan(src, dst, ps, nm, nm)
+        plan = ops.spline_plan(src, dst, ps, nm, nm, e0)
         x0 = bt.x[0][:nm]
         nv = bt.n[0][:1]
         x_op = ops.cast_bf16(x0) if op == torch.bfloat16 else x0

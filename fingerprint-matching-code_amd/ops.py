@@ -164,12 +164,15 @@ def cast_bf16(x, out=None):
     return out
 
 
-def spline_plan(src, dst, pseudo, num_nodes, nmax):
+def spline_plan(src, dst, pseudo, num_nodes, nmax, max_graph_edges=0):
+    """``max_graph_edges``: the largest per-graph edge count (host-known, e.g. from the batch's edge
+    offsets) -> the per-graph plan kernels when it allows; 0 -> the global plan kernels."""
     _dev(src, dst, pseudo)
     E = src.numel()
     nbytes = _lib.load().fpm_spline_plan_bytes(E, num_nodes)
     ws = torch.empty(nbytes, device=src.device, dtype=torch.uint8)
-    _lib.call("fpm_spline_plan", _p(src), _p(dst), _p(pseudo), E, num_nodes, nmax, _p(ws), nbytes, _stream(src))
+    _lib.call("fpm_spline_plan_graphs", _p(src), _p(dst), _p(pseudo), E, num_nodes, nmax, int(max_graph_edges), _p(ws),
+              nbytes, _stream(src))
     return ws
 
 

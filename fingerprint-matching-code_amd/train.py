@@ -49,7 +49,8 @@ class _Side:
         self.num_nodes = bt.B * self.nmax
         self.E = bt.E[side]
         self.nvalid = bt.n[side]
-        self.plan = ops.spline_plan(bt.src[side], bt.dst[side], bt.pseudo[side], self.num_nodes, self.nmax)
+        self.plan = ops.spline_plan(bt.src[side], bt.dst[side], bt.pseudo[side], self.num_nodes, self.nmax,
+                                    bt.max_graph_edges(side))
         self.csr = ops.plan_csr(self.plan, self.E, self.num_nodes)
         self._rplan = None
 
@@ -57,7 +58,7 @@ class _Side:
         if self._rplan is None:
             bt = self.bt
             self._rplan = ops.spline_plan(bt.dst[self.side], bt.src[self.side], bt.pseudo[self.side],
-                                          self.num_nodes, self.nmax)
+                                          self.num_nodes, self.nmax, bt.max_graph_edges(self.side))
         return ops.plan_csr(self._rplan, self.E, self.num_nodes)
 
 

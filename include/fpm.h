@@ -115,6 +115,12 @@ long fpm_spline_plan_bytes(long E, long num_nodes);
 long fpm_spline_y_bytes(int dtype, long E, long num_nodes);
 int fpm_spline_plan(const int* src, const int* dst, const float* pseudo, long E, long num_nodes, int nmax, void* ws,
                     long ws_bytes, void* stream);
+/* the same plan built one workgroup per graph (LDS sort / counts instead of device-wide atomics)
+ * when every graph has <= max_graph_edges <= 4096 edges and 26 <= nmax <= 1024; otherwise (or
+ * max_graph_edges <= 0) it is fpm_spline_plan.  Graphs' edges must be contiguous ranges in graph
+ * order (every batch builder emits them so).  Bit-identical plan. */
+int fpm_spline_plan_graphs(const int* src, const int* dst, const float* pseudo, long E, long num_nodes, int nmax,
+                           long max_graph_edges, void* ws, long ws_bytes, void* stream);
 int fpm_spline_plan_csr(void* ws, long E, long num_nodes, int** dst_ptr, int** nbr_local);
 int fpm_spline_conv_fwd(int dtype, const void* x_op, const void* plan_ws, long E, long num_nodes, int nmax,
                         const int* nvalid, const void* W, const float* bias, void* y_ws, long y_ws_bytes, int mode,

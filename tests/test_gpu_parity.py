@@ -584,7 +584,8 @@ def test_gnn_kernel_variants_bit_identical(sd):
     net.load_state_dict(sd)
     bt = DeviceBatch.from_pairs(pairs, DEV)
     outs = []
-    for key, val in (("gnn_group", 1), ("gnn_group", 2), ("gnn_unroll", 3), ("combine_npb", 16), ("gnn_wide", 0), ("gnn_il", 0)):
+    for key, val in (("gnn_group", 1), ("gnn_group", 2), ("gnn_unroll", 3), ("combine_npb", 16), ("gnn_wide", 1), ("gnn_il", 1),
+                     ("plan_graph", 0)):
         prev = ops.set_tuning(key, val)
         try:
             r = net.run(bt, chunks=1)
@@ -653,3 +654,41 @@ def test_crossset_attn_split_rows(sd):
     assert torch.equal(a3[:, :256], a16) and torch.equal(a3[:, 512:], a16)
     full = a3[:, :256].float() + a3[:, 256:512].float()
     assert (full - a16.float()).abs().max() <= full.abs().max() * 2.0 ** -8
+
+
+@pytest.mark.parametrize("n,n2", [(256, [256, 256]), (40, [40, 31, 26]), (512, [512])])
+def test_plan_per_graph_equals_global(n, n2):
+    """The per-graph spline plan (one workgroup per graph, LDS sort) and the global plan give the
+    same CSR, product rows and GEMM tile tables: SplineConv outputs and the GNN CSR bit-identical."""
+    pairs = synth.make_batch(50 + n, len(n2), n, n2=n2)
+    bt = DeviceBatch.from_pairs(pairs, DEV)
+    for side in range(2):
+        nn_ = bt.B * bt.nmax[side]
+        me = bt.max_graph_edges(side)
+        assert me > 0
+        p1 = ops.spline_plan(bt.src[side], bt.dst[side], bt.pseudo[side], nn_, bt.nmax[side], me)
+        p0 = ops.spline_plan(bt.src[side], bt.dst[side], bt.pseudo[side], nn_, bt.nmax[side], 0)
+        E = bt.E[side]
+        c1, c0 = ops.plan_csr(p1, E, nn_), ops.plan_csr(p0, E, nn_)
+        base1, base0 = p1.data_ptr(), p0.data_ptr()
+        ptr1 = p1[c1[0] - base1:c1[0] - base1 + 4 * (nn_ + 1)].view(torch.int32)
+        ptr0 = p0[c0[0] - base0:c0[0] - base0 + 4 * (nn_ + 1)].view(torch.int32)
+        nb1 = p1[c1[1] - base1:c1[1] - base1 + 4 * E].view(torch.int32)
+        nb0 = p0[c0[1] - base0:c0[1] - base0 + 4 * E].view(torch.int32)
+        assert torch.equal(ptr1, ptr0) and torch.equal(nb1, nb0)
+        a1, o1 = ops.spline_plan_rows(p1, E, nn_)
+        a0, o0 = ops.spline_plan_rows(p0, E, nn_)
+        assert torch.equal(o1, o0)
+        tot = int(o0[26].item())
+        assert torch.equal(a1[:tot], a0[:tot])
+    net = fpm.Net(regression=True, dtype="f32", backbone=False)
+    outs = []
+    for v in (1, 0):
+        prev = ops.set_tuning("plan_graph", v)
+        try:
+            outs.append(net.run_gpu_stage(bt, keep_feats=True))
+            torch.cuda.synchronize()
+        finally:
+            ops.set_tuning("plan_graph", prev)
+    for k in ("feat0", "feat1", "s", "ss"):
+        assert torch.equal(outs[0][k], outs[1][k]), k
