@@ -36,16 +36,35 @@ __device__ __forceinline__ void lse_combine(float& m, float& s, float mo, float 
     m = mn;
 }
 
-// Reduce (max, then sum of exp) over the 32 lanes sharing tr (xor 1..16 stays inside a half-wave).
+// Reductions over the 32 lanes sharing tr, on the VALU: DPP quad_perm xor 1 / xor 2, then the
+// half-row / row mirrors (after the quad steps every lane of a quad holds the same value, so a
+// mirror pairs whole quads / half-rows like an xor 4 / xor 8), then v_permlane16_swap for xor 16.
+// Every lane of the 32 ends with the bit-identical result (each step adds the same two operands).
+// (ds_bpermute shuffles, one LDS round trip per level, left these kernels latency-bound.)
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
 __device__ __forceinline__ float lane32_max(float v) {
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-    return v;
+    v = fmaxf(v, dppf<0xB1>(v));
+    v = fmaxf(v, dppf<0x4E>(v));
+    v = fmaxf(v, dppf<0x141>(v));
+    v = fmaxf(v, dppf<0x140>(v));
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
+    return fmaxf(__int_as_float(r[0]), __int_as_float(r[1]));
 }
 __device__ __forceinline__ float lane32_sum(float v) {
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+    v += dppf<0xB1>(v);
+    v += dppf<0x4E>(v);
+    v += dppf<0x141>(v);
+    v += dppf<0x140>(v);
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
+    return __int_as_float(r[0]) + __int_as_float(r[1]);
+}
+// value of lane ^ 32 (v_permlane32_swap: the two wave halves exchange)
+__device__ __forceinline__ float xor32(float v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
+    return __int_as_float((threadIdx.x & 32) ? r[0] : r[1]);
 }
 
 template <int ER, int EC>
@@ -75,8 +94,8 @@ __global__ __launch_bounds__(1024) void sinkhorn_reg_kernel(SinkArgs a) {
     const bool u_on_R = (a.contig_j != 0) == (!transposed);
 
     const float* in = a.in + (long)b * a.in_sb;
-    const long spr = a.contig_j ? a.in_si : a.in_sj;
-    const long spc = a.contig_j ? a.in_sj : a.in_si;
+    const int ispr = (int)(a.contig_j ? a.in_si : a.in_sj);
+    const int ispc = (int)(a.contig_j ? a.in_sj : a.in_si);
 
     float M[ER][EC];
     float pR[ER], pC[EC];
@@ -88,7 +107,9 @@ __global__ __launch_bounds__(1024) void sinkhorn_reg_kernel(SinkArgs a) {
         for (int f = 0; f < EC; ++f) {
             const int pc = tc + 32 * f;
             float v = -INFINITY;
-            if (pr < limPR && pc < limPC) v = (in[pr * spr + pc * spc] / a.tau) * fpm::LOG2E_F;
+            // 32-bit in-pair offsets (a pair's block is < 2^31 elements): 64-bit address math for
+            // the 64 loads held the register tile hostage (spills in the step loop)
+            if (pr < limPR && pc < limPC) v = (in[pr * ispr + pc * ispc] / a.tau) * fpm::LOG2E_F;
             M[e][f] = v;
         }
     }
@@ -105,20 +126,39 @@ __global__ __launch_bounds__(1024) void sinkhorn_reg_kernel(SinkArgs a) {
     auto ok_s = [](float x) { return x >= 0x1p-30f && x <= 0x1p30f; };
     // potR[e] = lse_f(M - pC) (+ dummy term)
     auto update_R = [&](bool add_dummy, bool fast) {
+        if (fast) {
+            bool bad = false;
+            // all ER rows' sums first, then their reductions: ER independent DPP chains in flight.
+            // M - (pC + sh), not (M - pC) - sh: the latter is CSE'd with the max-shifted path's
+            // M - pC, which then stays live as a second 64-value tile (VGPR spills)
+            float s[ER];
+#pragma unroll
+            for (int e = 0; e < ER; ++e) {
+                const float sh = pR[e];
+                float t = 0.f;
+#pragma unroll
+                for (int f = 0; f < EC; ++f) t += fpm::fast_exp2(M[e][f] - (pC[f] + sh));
+                s[e] = t;
+            }
+#pragma unroll
+            for (int e = 0; e < ER; ++e) s[e] = lane32_sum(s[e]);
+#pragma unroll
+            for (int e = 0; e < ER; ++e) {
+                float t = s[e];
+                if (add_dummy) t += (float)nd * fpm::fast_exp2(DUMMY - ud - pR[e]);
+                s[e] = t;
+                bad |= !ok_s(t);
+            }
+            // any row of the wave out of range: the whole wave redoes the step max-shifted (rare;
+            // keeps one path live at a time -- per-row fallbacks spilled the register tile)
+            if (__ballot(bad) == 0ull) {
+#pragma unroll
+                for (int e = 0; e < ER; ++e) pR[e] += fpm::fast_log2(s[e]);
+                return;
+            }
+        }
 #pragma unroll
         for (int e = 0; e < ER; ++e) {
-            if (fast) {
-                const float sh = pR[e];
-                float s = 0.f;
-#pragma unroll
-                for (int f = 0; f < EC; ++f) s += fpm::fast_exp2(M[e][f] - pC[f] - sh);
-                s = lane32_sum(s);
-                if (add_dummy) s += (float)nd * fpm::fast_exp2(DUMMY - ud - sh);
-                if (ok_s(s)) {
-                    pR[e] = sh + fpm::fast_log2(s);
-                    continue;
-                }
-            }
             float m = -INFINITY;
 #pragma unroll
             for (int f = 0; f < EC; ++f) m = fmaxf(m, M[e][f] - pC[f]);
@@ -128,7 +168,7 @@ __global__ __launch_bounds__(1024) void sinkhorn_reg_kernel(SinkArgs a) {
             float s = 0.f;
             if (m != -INFINITY) {
 #pragma unroll
-                for (int f = 0; f < EC; ++f) s += fpm::fast_exp2(M[e][f] - pC[f] - m);
+                for (int f = 0; f < EC; ++f) s += fpm::fast_exp2(M[e][f] - (pC[f] + m));
             }
             s = lane32_sum(s);
             if (add_dummy && m != -INFINITY) s += (float)nd * fpm::fast_exp2(dv - m);
@@ -138,12 +178,17 @@ __global__ __launch_bounds__(1024) void sinkhorn_reg_kernel(SinkArgs a) {
     // potC[f] = lse_e(M - pR) (+ dummy term): across the 32 thread-rows via LDS
     auto update_C = [&](bool add_dummy, bool fast) {
         if (fast) {
+            float cs[EC];
 #pragma unroll
             for (int f = 0; f < EC; ++f) {
                 float s = 0.f;
 #pragma unroll
-                for (int e = 0; e < ER; ++e) s += fpm::fast_exp2(M[e][f] - pR[e] - pC[f]);
-                s += __shfl_xor(s, 32);
+                for (int e = 0; e < ER; ++e) s += fpm::fast_exp2(M[e][f] - (pR[e] + pC[f]));
+                cs[f] = s;
+            }
+#pragma unroll
+            for (int f = 0; f < EC; ++f) {
+                const float s = cs[f] + xor32(cs[f]);
                 if ((tid & 63) < 32) red_s[wv][tc + 32 * f] = s;
                 if (tr == 0) fin[tc + 32 * f] = pC[f];            // the old potentials (shifts)
             }
@@ -174,9 +219,9 @@ __global__ __launch_bounds__(1024) void sinkhorn_reg_kernel(SinkArgs a) {
             float s = 0.f;
             if (m != -INFINITY) {
 #pragma unroll
-                for (int e = 0; e < ER; ++e) s += fpm::fast_exp2(M[e][f] - pR[e] - m);
+                for (int e = 0; e < ER; ++e) s += fpm::fast_exp2(M[e][f] - (pR[e] + m));
             }
-            float mo = __shfl_xor(m, 32), so = __shfl_xor(s, 32);
+            float mo = xor32(m), so = xor32(s);
             lse_combine(m, s, mo, so);
             if ((tid & 63) < 32) {
                 red_m[wv][tc + 32 * f] = m;
@@ -220,7 +265,7 @@ __global__ __launch_bounds__(1024) void sinkhorn_reg_kernel(SinkArgs a) {
                 for (int e = 0; e < ER; ++e)
                     if (tr + 32 * e < limPR) s += fpm::fast_exp2(DUMMY - pR[e] - m);
             }
-            float mo = __shfl_xor(m, 32), so = __shfl_xor(s, 32);
+            float mo = xor32(m), so = xor32(s);
             lse_combine(m, s, mo, so);
             if ((tid & 63) == 0) { blk_m[wv] = m; blk_s[wv] = s; }
             __syncthreads();
@@ -245,8 +290,8 @@ __global__ __launch_bounds__(1024) void sinkhorn_reg_kernel(SinkArgs a) {
     (void)lognd;
 
     float* out = a.out + (long)b * a.out_sb;
-    const long opr = a.contig_j ? a.out_si : a.out_sj;
-    const long opc = a.contig_j ? a.out_sj : a.out_si;
+    const int opr = (int)(a.contig_j ? a.out_si : a.out_sj);
+    const int opc = (int)(a.contig_j ? a.out_sj : a.out_si);
 #pragma unroll
     for (int e = 0; e < ER; ++e) {
         const int pr = tr + 32 * e;
@@ -509,7 +554,12 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
 
 }  // namespace
 
-// shifted single-pass lse steps (env FPM_SINKHORN_FAST / fpm_set_tuning("sinkhorn_fast"))
+// Sinkhorn step form (env FPM_SINKHORN_FAST / fpm_set_tuning("sinkhorn_fast")): 0 max-shifted log
+// domain, 1 (default) shifted single-pass lse after the first step; 2 = 1 with scalar loads in the
+// streaming kernel.  (A scaling form -- K = exp2(M - pR - pC) absorbed once, later steps as FMA
+// row/column rescales with a log-domain fallback when a line sum leaves [2^-40, 2^40] -- was
+// measured 2.8x slower at n = 256, tau = 0.01: small temperatures move the potentials by tens of
+// log2 units per step, so the guard tripped on most steps; removed.)
 int& sinkhorn_fast_flag() {
     static int v = [] {
         const char* e = getenv("FPM_SINKHORN_FAST");
@@ -536,14 +586,13 @@ extern "C" int fpm_sinkhorn_log_fwd(const float* s, long s_sb, long s_si, long s
     FPM_CHECK_ARG(s_sj == 1 || s_si == 1, "sinkhorn: one of the input's row/column strides must be 1");
     int nmax = n1max > n2max ? n1max : n2max;
     hipStream_t st = (hipStream_t)stream;
-    if (nmax <= 32)
-        hipLaunchKernelGGL((sinkhorn_reg_kernel<1, 1>), dim3(B), dim3(1024), 0, st, a);
-    else if (nmax <= 64)
-        hipLaunchKernelGGL((sinkhorn_reg_kernel<2, 2>), dim3(B), dim3(1024), 0, st, a);
-    else if (nmax <= 128)
-        hipLaunchKernelGGL((sinkhorn_reg_kernel<4, 4>), dim3(B), dim3(1024), 0, st, a);
-    else if (nmax <= 256)
-        hipLaunchKernelGGL((sinkhorn_reg_kernel<8, 8>), dim3(B), dim3(1024), 0, st, a);
+    void (*k)(SinkArgs) = nullptr;
+    if (nmax <= 32) k = sinkhorn_reg_kernel<1, 1>;
+    else if (nmax <= 64) k = sinkhorn_reg_kernel<2, 2>;
+    else if (nmax <= 128) k = sinkhorn_reg_kernel<4, 4>;
+    else if (nmax <= 256) k = sinkhorn_reg_kernel<8, 8>;
+    if (k)
+        hipLaunchKernelGGL(k, dim3(B), dim3(1024), 0, st, a);
     else
         hipLaunchKernelGGL(sinkhorn_stream_kernel, dim3(B), dim3(1024), 0, st, a);
     return fpm::check_launch("fpm_sinkhorn_log_fwd");

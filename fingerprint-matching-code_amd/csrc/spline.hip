@@ -355,10 +355,10 @@ __global__ __launch_bounds__(PG_THREADS) void plan_graph_kernel(const int* __res
                                                                 int* __restrict__ csr_e, int* __restrict__ nbr_local,
                                                                 int* __restrict__ eoff) {
     __shared__ unsigned key[PG_MAXE];
-    __shared__ int maskL[PG_MAXN], cnt[PG_MAXN];
+    __shared__ int maskL[PG_MAXN], cnt[PG_MAXN], pos[PG_MAXN + 1];
     __shared__ long range[2];
     __shared__ int ccount[NCELL];
-    const int g = blockIdx.x, tid = threadIdx.x;
+    const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const int base = g * nmax;
     if (tid == 0) range[0] = pg_lower_bound(src, E, base);
     if (tid == 1) range[1] = pg_lower_bound(src, E, base + nmax);
@@ -372,13 +372,7 @@ __global__ __launch_bounds__(PG_THREADS) void plan_graph_kernel(const int* __res
     const int ne = (int)(range[1] - e0);
     if (tid == 0) eoff[g] = (int)e0;
     if (tid == 0 && g == ngraphs - 1) eoff[ngraphs] = (int)E;
-    int npow = 1;
-    while (npow < ne) npow <<= 1;
-    for (int t = tid; t < npow; t += PG_THREADS) {
-        if (t >= ne) {
-            key[t] = 0xffffffffu;
-            continue;
-        }
+    for (int t = tid; t < ne; t += PG_THREADS) {
         const long e = e0 + t;
         int f[2];
         float fr[2];
@@ -402,41 +396,13 @@ __global__ __launch_bounds__(PG_THREADS) void plan_graph_kernel(const int* __res
         }
         grp_e[e] = gg;
         *(float4*)(basis_e + 4 * e) = make_float4(b4[0], b4[1], b4[2], b4[3]);
-        const int su = src[e] - base, du = dst[e] - base;
+        const int su = src[e] - base;
         atomicOr(&maskL[su], bits);
-        atomicAdd(&cnt[du], 1);
-        key[t] = ((unsigned)du << 22) | ((unsigned)su << 12) | (unsigned)t;
+        atomicAdd(&cnt[dst[e] - base], 1);
     }
     __syncthreads();
-    // bitonic sort of (dst, src, edge) keys, ascending
-    for (int size = 2; size <= npow; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int t = tid; t < npow / 2; t += PG_THREADS) {
-                const int lo = 2 * t - (t & (stride - 1)), hi = lo + stride;
-                const bool up = (lo & size) == 0;
-                const unsigned a = key[lo], b = key[hi];
-                if ((a > b) == up) {
-                    key[lo] = b;
-                    key[hi] = a;
-                }
-            }
-            __syncthreads();
-        }
-    }
-    for (int t = tid; t < ne; t += PG_THREADS) {
-        const unsigned k = key[t];
-        csr_e[e0 + t] = (int)(e0 + (k & 0xfffu));
-        nbr_local[e0 + t] = (int)((k >> 12) & 0x3ffu);
-    }
-    // masks (root bit added by the readers, as in the global path) and per-cell node counts
-    for (int u = tid; u < nmax; u += PG_THREADS) {
-        const int m = maskL[u];
-        mask[base + u] = m;
-        const int mr = m | (1 << 25);
-        for (int k = 0; k < NCELL; ++k)
-            if ((mr >> k) & 1) atomicAdd(&ccount[k], 1);
-    }
-    // dst pointers: exclusive scan of the in-degrees (one wave, nmax <= 1024)
+    // dst pointers: exclusive scan of the in-degrees (one wave, nmax <= 1024), kept in LDS as the
+    // counting-sort cursors
     if (tid < 64) {
         int carry = 0;
         for (int u0 = 0; u0 < nmax; u0 += 64) {
@@ -448,12 +414,54 @@ __global__ __launch_bounds__(PG_THREADS) void plan_graph_kernel(const int* __res
                 const int y = __shfl_up(incl, o);
                 if (tid >= o) incl += y;
             }
-            if (u < nmax) dst_ptr[base + u] = (int)e0 + carry + incl - v;
+            if (u < nmax) {
+                dst_ptr[base + u] = (int)e0 + carry + incl - v;
+                pos[u] = carry + incl - v;
+            }
             carry += __shfl(incl, 63);
         }
+        if (tid == 0) pos[nmax] = carry;
         if (tid == 0 && g == ngraphs - 1) dst_ptr[(long)ngraphs * nmax] = (int)E;
     }
     __syncthreads();
+    // counting sort by destination: (src, edge) keys scattered into each destination's segment
+    for (int t = tid; t < ne; t += PG_THREADS) {
+        const long e = e0 + t;
+        const int slot = atomicAdd(&pos[dst[e] - base], 1);
+        key[slot] = ((unsigned)(src[e] - base) << 12) | (unsigned)t;
+    }
+    // masks (root bit added by the readers, as in the global path) and per-cell node counts
+    // (wave ballots, one LDS atomic per wave and cell)
+    for (int u0 = 0; u0 < nmax; u0 += PG_THREADS) {
+        const int u = u0 + tid;
+        const int m = u < nmax ? maskL[u] : 0;
+        if (u < nmax) mask[base + u] = m;
+        const int mr = u < nmax ? (m | (1 << 25)) : 0;
+#pragma unroll
+        for (int k = 0; k < NCELL; ++k) {
+            const unsigned long long bk = __ballot((mr >> k) & 1);
+            if (lane == 0 && bk) atomicAdd(&ccount[k], __popcll(bk));
+        }
+    }
+    __syncthreads();
+    // each destination's in-edges ascending by (local source, edge): insertion sort of ~6 keys
+    for (int u = tid; u < nmax; u += PG_THREADS) {
+        const int end = pos[u], beg = end - cnt[u];
+        for (int a = beg + 1; a < end; ++a) {
+            const unsigned k = key[a];
+            int b = a - 1;
+            while (b >= beg && key[b] > k) {
+                key[b + 1] = key[b];
+                --b;
+            }
+            key[b + 1] = k;
+        }
+        for (int a = beg; a < end; ++a) {
+            const unsigned k = key[a];
+            csr_e[e0 + a] = (int)(e0 + (k & 0xfffu));
+            nbr_local[e0 + a] = (int)(k >> 12);
+        }
+    }
     if (tid < NCELL) cellcnt[g * NCELL + tid] = ccount[tid];
 }
 
@@ -563,7 +571,10 @@ __global__ __launch_bounds__(PG_THREADS) void plan_graph_rank_kernel(const int* 
 // out[v] = max_{in-edges e} sum_s basis[e,s] * Y[row(src_e, cell_s)] + Y[root row v] + bias
 //   mode 0: relu(.) ; mode 1: xres[v] + 0.1 * (.)   (+ optional per-pair column scale on out_t)
 // One wave per node, 12 channels per lane (3 x 4 contiguous).
-template <typename T, int NPB = 4>
+// PF: the node's in-edge row ids / basis weights are loaded once into lanes (one per edge) and
+// read back with v_readlane, and two in-edges' 8 product rows are loaded together (24 loads in
+// flight per lane instead of 12 behind a scalar rows4 load); same fma / max order, bit-identical.
+template <typename T, int NPB = 4, bool PF = false>
 __global__ __launch_bounds__(64 * NPB) void combine_kernel(const T* __restrict__ Y, const int* __restrict__ cell_off,
                                                       const float* __restrict__ bias,
                                                       const int* __restrict__ dst_ptr, const int4* __restrict__ rows4,
@@ -588,6 +599,82 @@ __global__ __launch_bounds__(64 * NPB) void combine_kernel(const T* __restrict__
     for (int t = 0; t < 3; ++t)
 #pragma unroll
         for (int j = 0; j < 4; ++j) m[t][j] = beg < end ? -INFINITY : 0.f;   // torch_scatter: empty -> 0
+    if constexpr (PF) {
+        const int deg = end - beg;
+        int4 rl = make_int4(0, 0, 0, 0);
+        float4 bl = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (lane < deg) {
+            rl = rows4[beg + lane];
+            bl = basis4[beg + lane];
+        }
+        auto rd = [](int v, int k) { return __builtin_amdgcn_readlane(v, k); };
+        auto rdf = [](float v, int k) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k)); };
+        // edge k of the node: product-row pointers and basis weights (wave-uniform)
+        auto edge = [&](int k, const T* (&y)[4], float (&bs)[4]) {
+            int4 r;
+            float4 b4;
+            if (k < 64) {
+                r = make_int4(rd(rl.x, k), rd(rl.y, k), rd(rl.z, k), rd(rl.w, k));
+                b4 = make_float4(rdf(bl.x, k), rdf(bl.y, k), rdf(bl.z, k), rdf(bl.w, k));
+            } else {
+                r = rows4[beg + k];
+                b4 = basis4[beg + k];
+            }
+            y[0] = Y + (long)r.x * 768; y[1] = Y + (long)r.y * 768;
+            y[2] = Y + (long)r.z * 768; y[3] = Y + (long)r.w * 768;
+            bs[0] = b4.x; bs[1] = b4.y; bs[2] = b4.z; bs[3] = b4.w;
+        };
+        int k = 0;
+        for (; k + 2 <= deg; k += 2) {
+            const T* ya[4];
+            const T* yb[4];
+            float ba[4], bb[4];
+            edge(k, ya, ba);
+            edge(k + 1, yb, bb);
+            float a[3][4][4], c[3][4][4];
+#pragma unroll
+            for (int t = 0; t < 3; ++t)
+#pragma unroll
+                for (int s4 = 0; s4 < 4; ++s4) {
+                    fpm::load4(ya[s4] + 4 * lane + 256 * t, a[t][s4]);
+                    fpm::load4(yb[s4] + 4 * lane + 256 * t, c[t][s4]);
+                }
+#pragma unroll
+            for (int t = 0; t < 3; ++t)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    float msg = ba[0] * a[t][0][j];
+                    msg = fmaf(ba[1], a[t][1][j], msg);
+                    msg = fmaf(ba[2], a[t][2][j], msg);
+                    msg = fmaf(ba[3], a[t][3][j], msg);
+                    m[t][j] = fmaxf(m[t][j], msg);
+                    float msg2 = bb[0] * c[t][0][j];
+                    msg2 = fmaf(bb[1], c[t][1][j], msg2);
+                    msg2 = fmaf(bb[2], c[t][2][j], msg2);
+                    msg2 = fmaf(bb[3], c[t][3][j], msg2);
+                    m[t][j] = fmaxf(m[t][j], msg2);
+                }
+        }
+        if (k < deg) {
+            const T* ya[4];
+            float ba[4];
+            edge(k, ya, ba);
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                float a[4][4];
+#pragma unroll
+                for (int s4 = 0; s4 < 4; ++s4) fpm::load4(ya[s4] + 4 * lane + 256 * t, a[s4]);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    float msg = ba[0] * a[0][j];
+                    msg = fmaf(ba[1], a[1][j], msg);
+                    msg = fmaf(ba[2], a[2][j], msg);
+                    msg = fmaf(ba[3], a[3][j], msg);
+                    m[t][j] = fmaxf(m[t][j], msg);
+                }
+            }
+        }
+    } else
     for (int e = beg; e < end; ++e) {
         const int4 r = rows4[e];
         const float4 bs = basis4[e];
@@ -756,6 +843,17 @@ int& combine_npb_flag() {
     return u;
 }
 
+// combine in-edge prefetch + 2-edge loads (1) or the per-edge loop (0, default); bit-identical,
+// measured neutral at C3 (26.3 K vs 26.3 K pairs/s, interleaved A/B).  Env FPM_COMBINE_PF or
+// fpm_set_tuning("combine_pf", v)
+int& combine_pf_flag() {
+    static int u = [] {
+        const char* e = getenv("FPM_COMBINE_PF");
+        return e ? atoi(e) : 0;
+    }();
+    return u;
+}
+
 extern "C" long fpm_spline_plan_bytes(long E, long num_nodes) {
     return plan_layout(E, num_nodes).total;
 }
@@ -900,17 +998,20 @@ extern "C" int fpm_spline_conv_fwd(int dtype, const void* x_op, const void* plan
     {
         const long graphs = (num_nodes + nmax - 1) / nmax;
         const int npb = combine_npb_flag();
-#define FPM_COMB(T_, N_)                                                                                         \
-    hipLaunchKernelGGL((combine_kernel<T_, N_>), dim3((unsigned)(((graphs + 7) / 8) * 8 * ((nmax + N_ - 1) / N_))), \
+        const bool pf = combine_pf_flag() != 0;
+#define FPM_COMB1(T_, N_, P_)                                                                                    \
+    hipLaunchKernelGGL((combine_kernel<T_, N_, P_>), dim3((unsigned)(((graphs + 7) / 8) * 8 * ((nmax + N_ - 1) / N_))), \
                        dim3(64 * N_), 0, st, (const T_*)y_ws, (const int*)(w + L.cell_off), bias,                \
                        (const int*)(w + L.dst_ptr), (const int4*)(w + L.rows4), (const float4*)(w + L.basis4),   \
                        num_nodes, nmax, nvalid, mode, xres, cscale, out_f, (T_*)out_t)
+#define FPM_COMB(T_, N_) do { if (pf) FPM_COMB1(T_, N_, true); else FPM_COMB1(T_, N_, false); } while (0)
         if (dtype == 0) {
             if (npb == 16) FPM_COMB(float, 16); else if (npb == 8) FPM_COMB(float, 8); else FPM_COMB(float, 4);
         } else {
             if (npb == 16) FPM_COMB(bf16_t, 16); else if (npb == 8) FPM_COMB(bf16_t, 8); else FPM_COMB(bf16_t, 4);
         }
 #undef FPM_COMB
+#undef FPM_COMB1
     }
     return check_launch("fpm_spline_conv_fwd");
 }

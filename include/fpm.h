@@ -98,6 +98,7 @@ int fpm_copy_async(const void* src, void* dst, long bytes, int nblocks, void* st
  *   "combine_npb" (FPM_COMBINE_NPB, default 4): destination nodes per SplineConv combine workgroup
  * Switches whose variants round differently (results within fp32 rounding, not bit-identical):
  *   "sinkhorn_fast" (FPM_SINKHORN_FAST, default 1): shifted single-pass lse after the first step
+ *       (0 = max-shifted lse every step; 2 = 1 with scalar loads in the n > 256 streaming kernel)
  *   "topk_fast" (FPM_TOPK_FAST, default 1): shifted single-pass early soft top-k column steps
  *   "afau_lut" (FPM_AFAU_LUT, default 2 = by dtype): AFA-U score lookup table (1) or 16-term sum (0) */
 int fpm_set_tuning(const char* key, int value);

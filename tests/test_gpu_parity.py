@@ -54,6 +54,39 @@ def test_sinkhorn_vs_oracle(n1s, n2s, iters, tau):
     assert (o2.cpu().double() - ref).abs().max() < 1e-4
 
 
+@pytest.mark.parametrize("form", [0, 1])
+@pytest.mark.parametrize("n1s,n2s,iters,tau,scale", [
+    ((256, 200, 131), (256, 256, 240), 20, 0.001, 0.1),    # small tau: shifted sums out of range -> max-shifted
+                                                            # (|S / tau| <= ~430 log2 units: fp32 conditioning ~3e-5)
+    ((240, 256), (256, 97), 20, 0.05, -2.0),                # one column + one row far below the rest:
+                                                            # their lines underflow against the shifts
+    ((64, 50), (64, 64), 1, 0.05, 0.3),                     # a single (log-domain) step
+    ((128, 128, 77), (128, 60, 128), 21, 0.02, 1.0),        # odd step count, dummy rows, transposed pair
+])
+def test_sinkhorn_forms_vs_oracle(form, n1s, n2s, iters, tau, scale):
+    """Both Sinkhorn step forms (0 max-shifted log, 1 shifted single-pass lse with its range guard)
+    against the float64 oracle, incl. inputs that trip the guards
+    (scale < 0: |scale| x randn with column 3 and row 5 set to -6, ~330 log2 units below the
+    row maxima)."""
+    g = torch.Generator().manual_seed(31 + iters + len(n1s))
+    B, n1max, n2max = len(n1s), max(n1s), max(n2s)
+    s = torch.randn(B, n1max, n2max, generator=g) * abs(scale)
+    if scale < 0:
+        s[:, :, 3] = -6.0
+        s[:, 5, :] = -6.0
+    ref = O.pygm_sinkhorn(s.double(), n1s, n2s, dummy_row=True, max_iter=iters, tau=tau)
+    prev = ops.set_tuning("sinkhorn_fast", form)
+    try:
+        out = ops.sinkhorn(s.to(DEV), _i32(n1s), _i32(n2s), iters, tau, True).cpu()
+        sT = s.transpose(1, 2).contiguous().to(DEV).transpose(1, 2)
+        o2 = torch.zeros(B, n2max, n1max, device=DEV).transpose(1, 2)
+        ops.sinkhorn(sT, _i32(n1s), _i32(n2s), iters, tau, True, out=o2)
+    finally:
+        ops.set_tuning("sinkhorn_fast", prev)
+    assert (out.double() - ref).abs().max() < 1e-4
+    assert (o2.cpu().double() - ref).abs().max() < 1e-4
+
+
 # ---------------------------------------------------------------------------------------- soft top-k
 def test_soft_topk_golden():
     z = np.load(os.path.join(GOLDEN, "soft_topk.npz"))
@@ -585,7 +618,7 @@ def test_gnn_kernel_variants_bit_identical(sd):
     bt = DeviceBatch.from_pairs(pairs, DEV)
     outs = []
     for key, val in (("gnn_group", 1), ("gnn_group", 2), ("gnn_unroll", 3), ("combine_npb", 16), ("gnn_wide", 1), ("gnn_il", 1),
-                     ("plan_graph", 0)):
+                     ("plan_graph", 0), ("combine_pf", 0), ("combine_pf", 1)):
         prev = ops.set_tuning(key, val)
         try:
             r = net.run(bt, chunks=1)

@@ -1,16 +1,18 @@
 #!/bin/bash
 # PMC passes on one kernel family of a short single-stream bench run:
-#   bash tools/pmc_kernel.sh <kernel-regex> <outdir>
+#   bash tools/pmc_kernel.sh <kernel-regex> <outdir> [bench args...]
+# Per-pass block limits (MI355X): <= 8 SQ, <= 4 TCC (FETCH_SIZE uses 3, WRITE_SIZE 2), <= 2 GRBM.
 set -o pipefail
 export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
-RE="$1"; OUT="$2"
+RE="$1"; OUT="$2"; shift 2
 mkdir -p "$OUT"
 run() {  # $1 = pass name, rest = counters
   local name=$1; shift
-  FPM_STREAMS=1 timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-include-regex "$RE" -d "$OUT/$name" -o run \
-    --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline > "$OUT/$name.log" 2>&1
+  FPM_STREAMS=1 timeout -s KILL 150 rocprofv3 --pmc "$@" --kernel-include-regex "$RE" -d "$OUT/$name" -o run \
+    --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-f32-line $BENCH_ARGS > "$OUT/$name.log" 2>&1
 }
 run sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU &&
-run mem FETCH_SIZE TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE &&
-run mem2 WRITE_SIZE SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM SQ_INSTS_SALU
+run sq2 SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE &&
+run fetch FETCH_SIZE TCC_HIT_sum &&
+run write WRITE_SIZE TCC_MISS_sum
