@@ -13,6 +13,7 @@
 // pair; reductions are fixed-order (wave trees, per-thread serial column sums), so the gradients
 // are deterministic.  Values are in log2 units as in the forward kernels.
 #include "fpm_common.h"
+#include <cstdlib>
 
 namespace {
 
@@ -356,9 +357,30 @@ __global__ __launch_bounds__(1024) void soft_topk_bwd_kernel(const float* __rest
 
 }  // namespace
 
+bool sinkhorn_reg_bwd(const float* s, long s_sb, long s_si, long s_sj, const float* dp, long d_sb, long d_si,
+                      long d_sj, float* ds, const int* n1, const int* n2, int B, int n1max, int n2max, int iters,
+                      float tau, int dummy_row, float* tile, float* hist, int H, hipStream_t st);
+
+// register-tile backward (sinkhorn.hip, n <= 256; 1, default) or the general kernel below (0).
+// Env FPM_SINKHORN_BWD_REG or fpm_set_tuning("sinkhorn_bwd_reg", v)
+int& sinkhorn_bwd_reg_flag() {
+    static int v = [] {
+        const char* e = getenv("FPM_SINKHORN_BWD_REG");
+        return e ? atoi(e) : 1;
+    }();
+    return v;
+}
+
+// elements of one pair's register tile in the n <= 256 backward (0: the general kernel's sizes)
+static long sk_tile_elems(int n1max, int n2max) {
+    const int n = n1max > n2max ? n1max : n2max;
+    return n <= 32 ? 1024 : n <= 64 ? 4096 : n <= 128 ? 16384 : n <= 256 ? 65536 : 0;
+}
+
 extern "C" long fpm_sinkhorn_bwd_ws_floats(int B, int n1max, int n2max, int iters) {
     const long H = (long)(n1max > n2max ? n1max : n2max) + 1;
-    return (long)B * n1max * n2max + (long)B * iters * H;
+    const long box = (long)n1max * n2max, tile = sk_tile_elems(n1max, n2max);
+    return (long)B * (box > tile ? box : tile) + (long)B * iters * H;
 }
 
 // s / dP: strided (B, n1max, n2max) views (input of the forward Sinkhorn and gradient of its
@@ -371,6 +393,12 @@ extern "C" int fpm_sinkhorn_log_bwd(const float* s, long s_sb, long s_si, long s
     FPM_CHECK_ARG(ws_floats >= fpm_sinkhorn_bwd_ws_floats(B, n1max, n2max, iters), "sinkhorn_bwd: workspace too small");
     FPM_CHECK_ARG(n1max <= 4096 && n2max <= 4096, "sinkhorn_bwd: n1max/n2max must be <= 4096");
     if (B == 0) return 0;
+    const long region = (long)B * ((long)n1max * n2max > sk_tile_elems(n1max, n2max) ? (long)n1max * n2max
+                                                                                     : sk_tile_elems(n1max, n2max));
+    if (sinkhorn_bwd_reg_flag() &&
+        sinkhorn_reg_bwd(s, s_sb, s_si, s_sj, dp, d_sb, d_si, d_sj, ds, n1, n2, B, n1max, n2max, iters, tau, dummy_row,
+                         ws, ws + region, (n1max > n2max ? n1max : n2max) + 1, (hipStream_t)stream))
+        return fpm::check_launch("fpm_sinkhorn_log_bwd");
     SinkBwdArgs a;
     a.s = s; a.s_sb = s_sb; a.s_si = s_si; a.s_sj = s_sj;
     a.dp = dp; a.d_sb = d_sb; a.d_si = d_si; a.d_sj = d_sj;
@@ -378,7 +406,7 @@ extern "C" int fpm_sinkhorn_log_bwd(const float* s, long s_sb, long s_si, long s
     a.dummy_row = dummy_row;
     a.H = (n1max > n2max ? n1max : n2max) + 1;
     a.dL = ws;
-    a.hist = ws + (long)B * n1max * n2max;
+    a.hist = ws + region;
     const size_t sh = (size_t)3 * a.H * sizeof(float);
     if (sh > 65536)
         (void)hipFuncSetAttribute((const void*)sinkhorn_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);

@@ -27,6 +27,14 @@ struct SinkArgs {
     int dummy_row;
     int contig_j;  // 1: j (column) is the unit-stride dimension of in/out
     int fast;      // shifted single-pass lse after the first step (sinkhorn_reg_kernel)
+    // backward (sinkhorn_reg_kernel<.., true>): dP view, dS out (contiguous B x n1max x n2max),
+    // potential history (B x iters x H floats; slot H - 1: the dummy rows' potential)
+    const float* dp;
+    long dp_sb, dp_si, dp_sj;
+    float* ds;
+    float* hist;
+    float* ds_tile;   // B x (1024 ER EC) scaled input tiles (replay -> sweep)
+    int H;
 };
 
 __device__ __forceinline__ void lse_combine(float& m, float& s, float mo, float so) {
@@ -67,7 +75,14 @@ __device__ __forceinline__ float xor32(float v) {
     return __int_as_float((threadIdx.x & 32) ? r[0] : r[1]);
 }
 
-template <int ER, int EC>
+// BWD = true: the training backward (reference gradient of pygm.sinkhorn through autograd):
+// the same forward steps replayed with every step's changed potentials kept in a.hist, then the
+// vector-Jacobian product walked in reverse with the gradient tile dL in registers (the input
+// block is re-read per step from L2 instead of held: M and dL together exceed the 128-register
+// budget of 1024-thread workgroups).  For a step L' = L - lse(L) along one axis,
+// dL = dL' - exp(L') * sum(dL') along that axis; the nd identical dummy rows carry one gradient
+// row dLd; dS = dL_0 / tau.  Reductions are fixed-order (deterministic).
+template <int ER, int EC, bool BWD = false>
 __global__ __launch_bounds__(1024) void sinkhorn_reg_kernel(SinkArgs a) {
     constexpr int NCOL = 32 * EC;
     __shared__ float red_m[16][NCOL];
@@ -278,6 +293,23 @@ __global__ __launch_bounds__(1024) void sinkhorn_reg_kernel(SinkArgs a) {
 
     if (tid == 0) redo_flag = 0;
     __syncthreads();
+    float* hist = BWD ? a.hist + (long)b * a.iters * a.H : nullptr;
+    // the physical side a step updates: R iff (row step) == u_on_R
+    auto save = [&](int it, bool Rside) {
+        float* h = hist + (long)it * a.H;
+        if (Rside) {
+            if (tc == 0) {
+#pragma unroll
+                for (int e = 0; e < ER; ++e)
+                    if (tr + 32 * e < boxPR) h[tr + 32 * e] = pR[e];
+            }
+        } else if (tr == 0) {
+#pragma unroll
+            for (int f = 0; f < EC; ++f)
+                if (tc + 32 * f < boxPC) h[tc + 32 * f] = pC[f];
+        }
+        if (tid == 0) h[a.H - 1] = ud;
+    };
     for (int it = 0; it < a.iters; ++it) {
         const bool fast = it > 0 && a.fast;
         if ((it & 1) == 0) {           // row normalisation: update u
@@ -286,8 +318,19 @@ __global__ __launch_bounds__(1024) void sinkhorn_reg_kernel(SinkArgs a) {
         } else {                       // column normalisation: update v
             if (u_on_R) update_C(nd > 0, fast); else update_R(nd > 0, fast);
         }
+        if constexpr (BWD) save(it, ((it & 1) == 0) == u_on_R);
     }
     (void)lognd;
+    if constexpr (BWD) {
+        // replay only: keep the scaled input tile (-inf padding included) for the sweep kernel,
+        // [e * EC + f][thread] -- coalesced, and re-read there without bounds checks
+        float* tile = a.ds_tile + (long)b * (1024 * ER * EC) + tid;
+#pragma unroll
+        for (int e = 0; e < ER; ++e)
+#pragma unroll
+            for (int f = 0; f < EC; ++f) tile[(e * EC + f) * 1024] = M[e][f];
+        return;                             // the reverse steps: sinkhorn_bwd_sweep_kernel
+    }
 
     float* out = a.out + (long)b * a.out_sb;
     const int opr = (int)(a.contig_j ? a.out_si : a.out_sj);
@@ -305,6 +348,213 @@ __global__ __launch_bounds__(1024) void sinkhorn_reg_kernel(SinkArgs a) {
             out[pr * opr + pc * opc] = v;
         }
     }
+}
+
+// Reverse sweep of the Sinkhorn backward (after sinkhorn_reg_kernel<ER, EC, true> replayed the
+// forward into a.hist): its own kernel so the gradient tile dL gets the register budget the
+// forward's tile M had (both phases in one kernel spilled ~300 VGPRs).
+template <int ER, int EC>
+__global__ __launch_bounds__(1024) void sinkhorn_bwd_sweep_kernel(SinkArgs a) {
+    constexpr int NCOL = 32 * EC;
+    __shared__ float red_s[16][NCOL];
+    __shared__ float fin[NCOL];
+    __shared__ float blk_s[16];
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int tr = tid >> 5, tc = tid & 31, wv = tid >> 6;
+    const int n1b = a.n1[b], n2b = a.n2[b];
+    const bool transposed = n1b > n2b;
+    const int R = transposed ? n2b : n1b;
+    const int C = transposed ? n1b : n2b;
+    const int nd = (a.dummy_row && C > R) ? (C - R) : 0;
+    const int limPR = a.contig_j ? n1b : n2b;
+    const int limPC = a.contig_j ? n2b : n1b;
+    const int boxPR = a.contig_j ? a.n1max : a.n2max;
+    const int boxPC = a.contig_j ? a.n2max : a.n1max;
+    const bool u_on_R = (a.contig_j != 0) == (!transposed);
+    const float* in = a.in + (long)b * a.in_sb;
+    const int ispr = (int)(a.contig_j ? a.in_si : a.in_sj);
+    const int ispc = (int)(a.contig_j ? a.in_sj : a.in_si);
+    const float DUMMY = -100.f * fpm::LOG2E_F;
+    const float* hist = a.hist + (long)b * a.iters * a.H;
+    // potentials after the last step: its side from hist[T-1], the other side from hist[T-2]
+    float pR[ER], pC[EC], ud = 0.f;
+    {
+        const int T = a.iters;
+        const bool lastR = T > 0 && (((T - 1) & 1) == 0) == u_on_R;
+        const int sR = lastR ? T - 1 : T - 2, sC = lastR ? T - 2 : T - 1;   // slot per side (< 0: none)
+        const float* hR = hist + (long)(sR > 0 ? sR : 0) * a.H;
+        const float* hC = hist + (long)(sC > 0 ? sC : 0) * a.H;
+#pragma unroll
+        for (int e = 0; e < ER; ++e) {
+            const int r = tr + 32 * e;
+            const float v = T > 0 ? hR[min(r, a.H - 2)] : 0.f;
+            pR[e] = (sR >= 0 && r < boxPR) ? v : 0.f;
+        }
+#pragma unroll
+        for (int f = 0; f < EC; ++f) {
+            const int c = tc + 32 * f;
+            const float v = T > 0 ? hC[min(c, a.H - 2)] : 0.f;
+            pC[f] = (sC >= 0 && c < boxPC) ? v : 0.f;
+        }
+        if (T > 0) ud = hist[(long)(T - 1) * a.H + a.H - 1];
+    }
+    // the scaled input tile the replay kept, re-read per step (unconditional coalesced loads; -inf
+    // in the padding).  z is an opaque 0 renewed every step so the loads stay inside the step loop
+    // (bounds-checked re-reads of the input, or hoisted loads, spilled ~250 VGPRs)
+    int z = 0;
+    const float* tileM = a.ds_tile + (long)b * (1024 * ER * EC) + tid;
+    auto Mv = [&](int e, int f) { return tileM[(e * EC + f) * 1024 + z]; };
+    (void)in; (void)ispr; (void)ispc;
+    auto validR = [&](int e) { return tr + 32 * e < limPR; };
+    auto validC = [&](int f) { return tc + 32 * f < limPC; };
+    // dL_T = dP o P_T on the real rows (dummy rows get no direct gradient)
+    const float* dpb = a.dp + (long)b * a.dp_sb;
+    const int dpr = (int)(a.contig_j ? a.dp_si : a.dp_sj), dpc = (int)(a.contig_j ? a.dp_sj : a.dp_si);
+    // dL: rows e < EREG in registers, the rest in LDS ([e - EREG][f][thread], conflict-free)
+    constexpr int EREG = ER >= 8 ? ER / 2 : ER;
+    extern __shared__ float dLs[];
+    float dLr[EREG][EC], dLd[ER];
+    auto DL = [&](int e, int f) -> float& {
+        return e < EREG ? dLr[e < EREG ? e : 0][f] : dLs[((e - EREG) * EC + f) * 1024 + tid];
+    };
+#pragma unroll
+    for (int e = 0; e < ER; ++e) {
+        dLd[e] = 0.f;
+        const int pr = tr + 32 * e;
+#pragma unroll
+        for (int f = 0; f < EC; ++f) {
+            const int pc = tc + 32 * f;
+            float g = 0.f;
+            if (pr < limPR && pc < limPC) g = dpb[pr * dpr + pc * dpc] * fpm::fast_exp2(Mv(e, f) - pR[e] - pC[f]);
+            DL(e, f) = g;
+        }
+    }
+        for (int t = a.iters - 1; t >= 0; --t) {
+            z = 0;
+            asm volatile("" : "+v"(z));
+            const bool algrow = (t & 1) == 0;
+            const bool Rside = algrow == u_on_R;          // physical side this step normalised
+            const bool dsum = !algrow && nd > 0;           // column step: dummy rows in the sums
+            if (Rside) {
+                float sr[ER];
+#pragma unroll
+                for (int e = 0; e < ER; ++e) {
+                    float t2 = 0.f;
+#pragma unroll
+                    for (int f = 0; f < EC; ++f) t2 += DL(e, f);
+                    sr[e] = t2;
+                }
+#pragma unroll
+                for (int e = 0; e < ER; ++e) sr[e] = lane32_sum(sr[e]);
+#pragma unroll
+                for (int e = 0; e < ER; ++e) {
+                    if (dsum) sr[e] = fmaf((float)nd, dLd[e], sr[e]);
+#pragma unroll
+                    for (int f = 0; f < EC; ++f) DL(e, f) -= fpm::fast_exp2(Mv(e, f) - pR[e] - pC[f]) * sr[e];
+                    if (dsum && validR(e)) dLd[e] -= fpm::fast_exp2(DUMMY - ud - pR[e]) * sr[e];
+                    __builtin_amdgcn_sched_barrier(0);     // one row's 8 loads in flight at a time
+                }
+            } else {
+                float cs[EC];
+#pragma unroll
+                for (int f = 0; f < EC; ++f) {
+                    float t2 = 0.f;
+#pragma unroll
+                    for (int e = 0; e < ER; ++e) t2 += DL(e, f);
+                    cs[f] = t2;
+                }
+#pragma unroll
+                for (int f = 0; f < EC; ++f) {
+                    const float v = cs[f] + xor32(cs[f]);
+                    if ((tid & 63) < 32) red_s[wv][tc + 32 * f] = v;
+                }
+                __syncthreads();
+                if (tid < NCOL) {
+                    float v = red_s[0][tid];
+                    for (int w = 1; w < 16; ++w) v += red_s[w][tid];
+                    fin[tid] = v;
+                }
+                __syncthreads();
+#pragma unroll
+                for (int f = 0; f < EC; ++f) {
+                    float sc = fin[tc + 32 * f];
+                    if (dsum) sc = fmaf((float)nd, dLd[f], sc);
+#pragma unroll
+                    for (int e = 0; e < ER; ++e) DL(e, f) -= fpm::fast_exp2(Mv(e, f) - pR[e] - pC[f]) * sc;
+                    if (dsum && validC(f)) dLd[f] -= fpm::fast_exp2(DUMMY - ud - pC[f]) * sc;
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                __syncthreads();                            // fin / red_s reused
+            }
+            if (algrow && nd > 0) {
+                // the dummy rows' own row step: their sum over the valid algorithmic columns
+                if (u_on_R) {
+                    float sd = 0.f;
+#pragma unroll
+                    for (int f = 0; f < EC; ++f)
+                        if (validC(f)) sd += dLd[f];
+                    sd = lane32_sum(sd);
+#pragma unroll
+                    for (int f = 0; f < EC; ++f)
+                        if (validC(f)) dLd[f] -= fpm::fast_exp2(DUMMY - ud - pC[f]) * sd;
+                } else {
+                    float sd = 0.f;
+                    if (tc == 0) {
+#pragma unroll
+                        for (int e = 0; e < ER; ++e)
+                            if (validR(e)) sd += dLd[e];
+                    }
+                    sd += xor32(sd);
+                    if ((tid & 63) == 0) blk_s[wv] = sd;
+                    __syncthreads();
+                    sd = blk_s[0];
+                    for (int w = 1; w < 16; ++w) sd += blk_s[w];
+                    __syncthreads();
+#pragma unroll
+                    for (int e = 0; e < ER; ++e)
+                        if (validR(e)) dLd[e] -= fpm::fast_exp2(DUMMY - ud - pR[e]) * sd;
+                }
+            }
+            // potentials in effect before step t (after step t - 2 on the same side, else 0);
+            // unconditional loads at a clamped slot, then selects (per-thread conditional loads
+            // here cost ~100 spilled VGPRs)
+            {
+                const bool have = t >= 2;
+                const float* h = hist + (long)(have ? t - 2 : 0) * a.H;
+                if (Rside) {
+#pragma unroll
+                    for (int e = 0; e < ER; ++e) {
+                        const int r = tr + 32 * e;
+                        const float v = h[min(r, a.H - 2)];
+                        pR[e] = (have && r < boxPR) ? v : 0.f;
+                    }
+                } else {
+#pragma unroll
+                    for (int f = 0; f < EC; ++f) {
+                        const int c = tc + 32 * f;
+                        const float v = h[min(c, a.H - 2)];
+                        pC[f] = (have && c < boxPC) ? v : 0.f;
+                    }
+                }
+                if (algrow) ud = have ? h[a.H - 1] : 0.f;
+            }
+        }
+        // dS = dL_0 / tau on the valid block, zeros in the padding (contiguous B x n1max x n2max)
+        float* dsb = a.ds + (long)b * a.n1max * a.n2max;
+        const float it_ = 1.f / a.tau;
+        const int opr = a.contig_j ? a.n2max : 1, opc = a.contig_j ? 1 : a.n2max;
+#pragma unroll
+        for (int e = 0; e < ER; ++e) {
+            const int pr = tr + 32 * e;
+            if (pr >= boxPR) continue;
+#pragma unroll
+            for (int f = 0; f < EC; ++f) {
+                const int pc = tc + 32 * f;
+                if (pc >= boxPC) continue;
+                dsb[pr * opr + pc * opc] = (pr < limPR && pc < limPC) ? DL(e, f) * it_ : 0.f;
+            }
+        }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -566,6 +816,37 @@ int& sinkhorn_fast_flag() {
         return e ? atoi(e) : 1;
     }();
     return v;
+}
+
+// register-tile backward for max(n1max, n2max) <= 256 (called by fpm_sinkhorn_log_bwd; tile:
+// B x sinkhorn_reg_tile_elems floats); returns false when the sizes need the general kernel
+bool sinkhorn_reg_bwd(const float* s, long s_sb, long s_si, long s_sj, const float* dp, long d_sb, long d_si,
+                      long d_sj, float* ds, const int* n1, const int* n2, int B, int n1max, int n2max, int iters,
+                      float tau, int dummy_row, float* tile, float* hist, int H, hipStream_t st) {
+    const int nmax = n1max > n2max ? n1max : n2max;
+    if (nmax > 256 || !(s_sj == 1 || s_si == 1)) return false;
+    SinkArgs a = {};
+    a.in = s; a.in_sb = s_sb; a.in_si = s_si; a.in_sj = s_sj;
+    a.n1 = n1; a.n2 = n2; a.n1max = n1max; a.n2max = n2max;
+    a.iters = iters; a.tau = tau; a.dummy_row = dummy_row;
+    a.contig_j = (s_sj == 1) ? 1 : 0;
+    a.fast = sinkhorn_fast_flag();
+    a.dp = dp; a.dp_sb = d_sb; a.dp_si = d_si; a.dp_sj = d_sj;
+    a.ds = ds; a.hist = hist; a.H = H; a.ds_tile = tile;
+    void (*k)(SinkArgs) = nullptr;
+    if (nmax <= 32) k = sinkhorn_reg_kernel<1, 1, true>;
+    else if (nmax <= 64) k = sinkhorn_reg_kernel<2, 2, true>;
+    else if (nmax <= 128) k = sinkhorn_reg_kernel<4, 4, true>;
+    else k = sinkhorn_reg_kernel<8, 8, true>;
+    void (*k2)(SinkArgs) = nmax <= 32 ? sinkhorn_bwd_sweep_kernel<1, 1>
+                           : nmax <= 64 ? sinkhorn_bwd_sweep_kernel<2, 2>
+                           : nmax <= 128 ? sinkhorn_bwd_sweep_kernel<4, 4> : sinkhorn_bwd_sweep_kernel<8, 8>;
+    const int er = nmax <= 32 ? 1 : nmax <= 64 ? 2 : nmax <= 128 ? 4 : 8;
+    const size_t lds = er >= 8 ? (size_t)(er - er / 2) * er * 1024 * sizeof(float) : 0;   // sweep's dL rows
+    if (lds > 65536) (void)hipFuncSetAttribute((const void*)k2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k, dim3(B), dim3(1024), 0, st, a);
+    hipLaunchKernelGGL(k2, dim3(B), dim3(1024), lds, st, a);
+    return true;
 }
 
 extern "C" int fpm_sinkhorn_log_fwd(const float* s, long s_sb, long s_si, long s_sj, float* out,

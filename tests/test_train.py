@@ -39,13 +39,18 @@ def sd():
 
 
 # ------------------------------------------------------------------------------------- Sinkhorn
+@pytest.mark.parametrize("reg", [1, 0])
 @pytest.mark.parametrize("n1s,n2s,iters,tau", [
     ((8, 8), (8, 8), 10, 0.05),
     ((32, 20, 32), (32, 32, 17), 20, 0.01),          # dummy rows + transposed pair
     ((64, 50), (64, 64), 10, 0.01),
     ((128,), (128,), 20, 0.01),
+    ((256, 200, 131), (256, 256, 240), 21, 0.02),    # register tile 8x8, odd steps, both dummy sides
+    ((90, 256), (256, 77), 1, 0.05),                 # a single step
 ])
-def test_sinkhorn_bwd_vs_autograd(n1s, n2s, iters, tau):
+def test_sinkhorn_bwd_vs_autograd(reg, n1s, n2s, iters, tau):
+    """Both backward kernels (register tile with the forward's replay, n <= 256; general) against
+    autograd through the float64 oracle, for contiguous and transposed-storage inputs."""
     g = torch.Generator().manual_seed(sum(n1s) + iters)
     B = len(n1s)
     n1max, n2max = max(n1s), max(n2s)
@@ -56,12 +61,21 @@ def test_sinkhorn_bwd_vs_autograd(n1s, n2s, iters, tau):
     (out * dp).sum().backward()
     ref = sl.grad
     sd_ = s.float().to(DEV)
-    ds = train.sinkhorn_bwd(sd_, dp.float().to(DEV), _i32(n1s), _i32(n2s), iters, tau, True)
+    prev = ops.set_tuning("sinkhorn_bwd_reg", reg)
+    try:
+        ds = train.sinkhorn_bwd(sd_, dp.float().to(DEV), _i32(n1s), _i32(n2s), iters, tau, True)
+        # strided (transposed-storage) input view: the same gradient (bit-identical for the general
+        # kernel, which walks algorithmic coordinates; the register tile reduces along the storage
+        # axes, so rounding may differ)
+        sT = sd_.transpose(1, 2).contiguous().transpose(1, 2)
+        ds2 = train.sinkhorn_bwd(sT, dp.float().to(DEV), _i32(n1s), _i32(n2s), iters, tau, True)
+    finally:
+        ops.set_tuning("sinkhorn_bwd_reg", prev)
     assert _rel(ds, ref) < 2e-4
-    # strided (transposed-storage) input view gives the same gradient
-    sT = sd_.transpose(1, 2).contiguous().transpose(1, 2)
-    ds2 = train.sinkhorn_bwd(sT, dp.float().to(DEV), _i32(n1s), _i32(n2s), iters, tau, True)
-    assert torch.equal(ds.cpu(), ds2.cpu())
+    if reg:
+        assert _rel(ds2, ref) < 2e-4 and _rel(ds2, ds.double().cpu()) < 1e-5
+    else:
+        assert torch.equal(ds.cpu(), ds2.cpu())
     # padding of the box stays zero
     for b in range(B):
         assert ds[b, n1s[b]:].abs().sum() == 0 and ds[b, :, n2s[b]:].abs().sum() == 0
