@@ -52,6 +52,9 @@ SIGNATURES = {
     "fpm_elementwise": (I, [P, P, L, I, P]),
     "fpm_outer_sum_parts": (L, [I, L]),
     "fpm_outer_sum": (I, [P, L, L, I, P, L, L, I, I, I, L, P, P]),
+    "fpm_bn_ws_floats": (L, [I, I]),
+    "fpm_bn_relu_train_fwd": (I, [P, I, I, L, P, P, F, F, P, P, P, P, P, P]),
+    "fpm_bn_relu_train_bwd": (I, [P, P, I, I, L, P, P, P, P, P, P, P]),
     "fpm_match_cls_ws_floats": (L, [I, I, I]),
     "fpm_match_cls_fwd": (I, [I, P, P, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),
     "fpm_lsa_batch_host": (I, [P, L, L, P, P, I, I, P, I]),

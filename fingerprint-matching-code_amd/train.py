@@ -387,15 +387,46 @@ class AfauFn(torch.autograd.Function):
         return (None, None, None) + tuple(total)
 
 
+class BnReluFn(torch.autograd.Function):
+    """BatchNorm2d(relu(x)) in train mode (batch statistics; running buffers updated with
+    momentum) on the HIP kernels fpm_bn_relu_train_fwd / _bwd (ngm.py:90-99)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, rmean, rvar, momentum, eps):
+        N, Cc, H, W = x.shape
+        xc = x.detach().contiguous()
+        y = torch.empty_like(xc)
+        stats = torch.empty(2 * Cc, device=x.device, dtype=torch.float32)
+        ws = torch.empty(int(_lib.load().fpm_bn_ws_floats(N, Cc)), device=x.device, dtype=torch.float32)
+        _lib.call("fpm_bn_relu_train_fwd", ops._p(xc), N, Cc, H * W, ops._p(gamma.detach().contiguous()),
+                  ops._p(beta.detach().contiguous()), float(eps), float(momentum), ops._p(rmean), ops._p(rvar),
+                  ops._p(y), ops._p(stats), ops._p(ws), ops._stream(xc))
+        ctx.save_for_backward(xc, gamma, stats)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        xc, gamma, stats = ctx.saved_tensors
+        N, Cc, H, W = xc.shape
+        gy = gy.contiguous()
+        dx = torch.empty_like(xc)
+        dg = torch.empty(Cc, device=xc.device, dtype=torch.float32)
+        db = torch.empty_like(dg)
+        ws = torch.empty(int(_lib.load().fpm_bn_ws_floats(N, Cc)), device=xc.device, dtype=torch.float32)
+        _lib.call("fpm_bn_relu_train_bwd", ops._p(xc), ops._p(gy), N, Cc, H * W, ops._p(gamma.detach().contiguous()),
+                  ops._p(stats), ops._p(dx), ops._p(dg), ops._p(db), ops._p(ws), ops._stream(xc))
+        return dx, dg, db, None, None, None, None
+
+
 def match_cls_train(m, P_, B_):
     """MatchClassifier.forward (ngm.py:75-106) with BatchNorm2d in train mode (batch statistics,
-    running buffers updated with momentum 0.1)."""
+    running buffers updated with momentum 0.1); ReLU + BatchNorm on the fused HIP kernels."""
     x = m.unsqueeze(1)
     for ci, bi in ((0, 2), (4, 6)):
         x = F.conv2d(x, P_("match_cls.conv.%d.weight" % ci), P_("match_cls.conv.%d.bias" % ci), padding=1)
-        x = F.relu(x)
-        x = F.batch_norm(x, B_("match_cls.conv.%d.running_mean" % bi), B_("match_cls.conv.%d.running_var" % bi),
-                         P_("match_cls.conv.%d.weight" % bi), P_("match_cls.conv.%d.bias" % bi), True, 0.1, C.BN_EPS)
+        x = BnReluFn.apply(x, P_("match_cls.conv.%d.weight" % bi), P_("match_cls.conv.%d.bias" % bi),
+                           B_("match_cls.conv.%d.running_mean" % bi), B_("match_cls.conv.%d.running_var" % bi), 0.1,
+                           C.BN_EPS)
         nbt = B_("match_cls.conv.%d.num_batches_tracked" % bi)
         nbt.add_(1)
         x = F.max_pool2d(x, 2)

@@ -210,6 +210,19 @@ long fpm_outer_sum_parts(int B, long N);
 int fpm_outer_sum(const float* U, long sUb, long sUo, int O, const float* V, long sVb, long sVc, int Cc, int ones,
                   int B, long N, float* part, void* stream);
 
+/* ---- MatchClassifier training: BatchNorm2d(train) fused with the ReLU before it ---------------
+ * (ngm.py:90-99 conv -> ReLU -> BatchNorm2d blocks; torch F.batch_norm(training=True) semantics)
+ * x: conv output (N, C, HW) fp32; y = BN(relu(x)) with batch statistics; stats (2C floats):
+ * (mean, invstd) for the backward; running_mean / running_var (nullable): momentum update with the
+ * unbiased variance.  Backward: dx = d/dx through the BN and the ReLU, dgamma, dbeta (C).
+ * ws: fpm_bn_ws_floats(N, C) floats.  Reductions are deterministic. */
+long fpm_bn_ws_floats(int N, int C);
+int fpm_bn_relu_train_fwd(const float* x, int N, int C, long HW, const float* gamma, const float* beta, float eps,
+                          float momentum, float* running_mean, float* running_var, float* y, float* stats, float* ws,
+                          void* stream);
+int fpm_bn_relu_train_bwd(const float* x, const float* dy, int N, int C, long HW, const float* gamma,
+                          const float* stats, float* dx, float* dgamma, float* dbeta, float* ws, void* stream);
+
 /* ---- MatchClassifier (ngm.py:75-106, applied at :451-455) -------------------------------------
  * dtype 0: conv2 on fp32 matrix cores (exact fp32 products, parity mode); 1: conv2 operands in
  * bf16 (fp32 accumulation, the bf16 throughput mode). */

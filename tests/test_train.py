@@ -10,6 +10,7 @@ so the end-to-end bound is looser than the per-op ones.
 import numpy as np
 import pytest
 import torch
+import torch.nn.functional as F_
 
 import fpm
 from fpm import ops, params, synth, train
@@ -425,3 +426,29 @@ def test_outer_sum_kernel():
         assert (w.cpu().double() - ref).abs().max() < 1e-4 * ref.abs().max()
         assert (bsum.cpu().double() - U.double().sum((0, 2))).abs().max() < 1e-6 * float(U.abs().sum())
         assert torch.equal(_outer_sum(U.to(DEV), V.to(DEV)), w)
+
+
+@pytest.mark.parametrize("shape", [(4, 16, 64, 64), (3, 32, 17, 19)])
+def test_bn_relu_train_vs_torch(shape):
+    """HIP BatchNorm2d(relu(x)) in train mode vs torch F.relu + F.batch_norm(training=True):
+    output, running buffers and the gradients of x, gamma, beta (ngm.py:90-99)."""
+    g = torch.Generator().manual_seed(sum(shape))
+    x = torch.randn(*shape, generator=g)
+    gamma = torch.rand(shape[1], generator=g) + 0.5
+    beta = torch.randn(shape[1], generator=g) * 0.1
+    gy = torch.randn(*shape, generator=g)
+    rm0, rv0 = torch.randn(shape[1], generator=g) * 0.1, torch.rand(shape[1], generator=g) + 0.5
+    # torch reference (float64 on CPU)
+    xr, gr, br = (t.double().clone().requires_grad_(True) for t in (x, gamma, beta))
+    rmr, rvr = rm0.double().clone(), rv0.double().clone()
+    yr = F_.batch_norm(F_.relu(xr), rmr, rvr, gr, br, True, 0.1, 1e-5)
+    (yr * gy.double()).sum().backward()
+    # HIP
+    xd, gd, bd = (t.to(DEV).clone().requires_grad_(True) for t in (x, gamma, beta))
+    rmd, rvd = rm0.to(DEV).clone(), rv0.to(DEV).clone()
+    y = train.BnReluFn.apply(xd, gd, bd, rmd, rvd, 0.1, 1e-5)
+    (y * gy.to(DEV)).sum().backward()
+    assert _rel(y, yr.detach()) < 1e-5
+    assert _rel(rmd, rmr) < 1e-5 and _rel(rvd, rvr) < 1e-5
+    assert _rel(xd.grad, xr.grad) < 1e-4
+    assert _rel(gd.grad, gr.grad) < 1e-4 and _rel(bd.grad, br.grad) < 1e-4
