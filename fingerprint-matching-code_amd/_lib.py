@@ -35,6 +35,7 @@ SIGNATURES = {
     "fpm_spline_plan_csr": (I, [P, L, L, ctypes.POINTER(P), ctypes.POINTER(P)]),
     "fpm_spline_y_bytes": (L, [I, L, L]),
     "fpm_spline_conv_fwd": (I, [I, P, P, L, L, I, P, P, P, P, L, I, P, P, P, P, P]),
+    "fpm_spline_conv_fwd_argmax": (I, [I, P, P, L, L, I, P, P, P, P, L, I, P, P, P, P, P, P]),
     "fpm_edge_diff": (I, [P, P, P, L, I, P, P]),
     "fpm_rows_bcast_scale": (I, [I, P, L, I, P, P, P, P]),
     "fpm_edge_diff_padded": (I, [P, P, P, P, P, P, L, I, P, P]),
@@ -80,6 +81,8 @@ SIGNATURES = {
     "fpm_soft_topk_bwd": (I, [P, L, L, P, P, P, P, I, I, I, F, P, L, L, P, P, L, P, P]),
     "fpm_spline_plan_rows": (I, [P, L, L, ctypes.POINTER(P), ctypes.POINTER(P)]),
     "fpm_spline_conv_bwd_data": (I, [I, P, L, L, I, P, P, P, I, P, P, P, P, P, P, I, P]),
+    "fpm_gather_transpose": (I, [I, P, L, P, L, I, P, L, P]),
+    "fpm_spline_conv_bwd_data_scatter": (I, [I, P, P, P, L, L, I, P, P, P, I, P, P, P, P, P, P, I, P]),
     "fpm_kron_agg": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, I, P, P]),
     "fpm_kron_gnn_layer_bwd_point": (I, [P, I, I, I, I, P, P, P, P, P, P, P]),
     "fpm_profile_enable": (I, [I]),

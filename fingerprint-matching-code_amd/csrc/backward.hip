@@ -441,15 +441,20 @@ extern "C" int fpm_soft_topk_bwd(const float* ss, long sb, long ld, const int* n
 // one accumulator; per-workgroup partials part[b * S + s][q] are summed in order by fpm_rows_sum.
 namespace {
 constexpr int OS_T = 256, OS_L = 4096, OS_MAXC = 17;
+// rows padded to OS_T + 4 floats: 16-B aligned float4 reads (4 FMAs per two ds_read_b128) into four
+// independent accumulators (the single fmaf chain per thread was latency-bound)
+constexpr int OS_LD = OS_T + 4;
 __global__ __launch_bounds__(512) void outer_sum_kernel(const float* __restrict__ U, long sUb, long sUo, int O,
                                                         const float* __restrict__ V, long sVb, long sVc, int Cc,
                                                         int ones, long N, int S, float* __restrict__ part) {
-    __shared__ float Ut[OS_MAXC][OS_T + 1], Vt[OS_MAXC][OS_T + 1];
+    __shared__ __attribute__((aligned(16))) float Ut[OS_MAXC][OS_LD];
+    __shared__ __attribute__((aligned(16))) float Vt[OS_MAXC][OS_LD];
     const int b = blockIdx.x / S, s = blockIdx.x % S, t = threadIdx.x;
     const int C1 = Cc + ones, nq = O * C1;
     const int o = t / C1, c = t - o * C1;
     const long p0 = (long)s * OS_L, p1 = min(N, p0 + OS_L);
     float acc = 0.f;
+    float4 a4 = make_float4(0.f, 0.f, 0.f, 0.f);
     for (long q0 = p0; q0 < p1; q0 += OS_T) {
         const int len = (int)min((long)OS_T, p1 - q0);
         for (int k = t; k < O * OS_T; k += 512) {
@@ -462,16 +467,31 @@ __global__ __launch_bounds__(512) void outer_sum_kernel(const float* __restrict_
         }
         __syncthreads();
         if (t < nq) {
+            const float4* u4 = (const float4*)&Ut[o][0];
             if (c < Cc) {
-#pragma unroll 8
-                for (int p = 0; p < OS_T; ++p) acc = fmaf(Ut[o][p], Vt[c][p], acc);
+                const float4* v4 = (const float4*)&Vt[c][0];
+#pragma unroll 4
+                for (int p = 0; p < OS_T / 4; ++p) {
+                    const float4 x = u4[p], y = v4[p];
+                    a4.x = fmaf(x.x, y.x, a4.x);
+                    a4.y = fmaf(x.y, y.y, a4.y);
+                    a4.z = fmaf(x.z, y.z, a4.z);
+                    a4.w = fmaf(x.w, y.w, a4.w);
+                }
             } else {
-#pragma unroll 8
-                for (int p = 0; p < OS_T; ++p) acc += Ut[o][p];
+#pragma unroll 4
+                for (int p = 0; p < OS_T / 4; ++p) {
+                    const float4 x = u4[p];
+                    a4.x += x.x;
+                    a4.y += x.y;
+                    a4.z += x.z;
+                    a4.w += x.w;
+                }
             }
         }
         __syncthreads();
     }
+    acc = (a4.x + a4.y) + (a4.z + a4.w);
     if (t < nq) part[(long)blockIdx.x * nq + t] = acc;
 }
 }  // namespace

@@ -574,14 +574,17 @@ __global__ __launch_bounds__(PG_THREADS) void plan_graph_rank_kernel(const int* 
 // PF: the node's in-edge row ids / basis weights are loaded once into lanes (one per edge) and
 // read back with v_readlane, and two in-edges' 8 product rows are loaded together (24 loads in
 // flight per lane instead of 12 behind a scalar rows4 load); same fma / max order, bit-identical.
-template <typename T, int NPB = 4, bool PF = false>
+// ARG (training forward): also record, per (node, channel), the CSR slot of the in-edge attaining
+// the max (the first one in CSR order, -1 without in-edges) for the scatter backward.
+template <typename T, int NPB = 4, bool PF = false, bool ARG = false>
 __global__ __launch_bounds__(64 * NPB) void combine_kernel(const T* __restrict__ Y, const int* __restrict__ cell_off,
                                                       const float* __restrict__ bias,
                                                       const int* __restrict__ dst_ptr, const int4* __restrict__ rows4,
                                                       const float4* __restrict__ basis4, long num_nodes, int nmax,
                                                       const int* __restrict__ nvalid, int mode,
                                                       const float* __restrict__ xres, const float* __restrict__ cscale,
-                                                      float* __restrict__ out_f, T* __restrict__ out_t) {
+                                                      float* __restrict__ out_f, T* __restrict__ out_t,
+                                                      int* __restrict__ argmax = nullptr) {
     const int lane = threadIdx.x & 63;
     // graph-per-XCD block order: XCD x = blockIdx % 8 takes graphs x, x+8, ... so a graph's product
     // rows (~3.7 MB at n = 256, each read ~2.4 times by its in-edges) stay in one L2
@@ -595,10 +598,15 @@ __global__ __launch_bounds__(64 * NPB) void combine_kernel(const T* __restrict__
     const int beg = dst_ptr[v], end = dst_ptr[v + 1];
     const long root_row = (long)cell_off[25] + v;
     float m[3][4];
+    int am[3][4];
 #pragma unroll
     for (int t = 0; t < 3; ++t)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) m[t][j] = beg < end ? -INFINITY : 0.f;   // torch_scatter: empty -> 0
+        for (int j = 0; j < 4; ++j) {
+            m[t][j] = beg < end ? -INFINITY : 0.f;   // torch_scatter: empty -> 0
+            am[t][j] = -1;
+        }
+    (void)am;
     if constexpr (PF) {
         const int deg = end - beg;
         int4 rl = make_int4(0, 0, 0, 0);
@@ -696,9 +704,17 @@ __global__ __launch_bounds__(64 * NPB) void combine_kernel(const T* __restrict__
                 msg = fmaf(bs.y, a1[j], msg);
                 msg = fmaf(bs.z, a2[j], msg);
                 msg = fmaf(bs.w, a3[j], msg);
+                if constexpr (ARG) {
+                    if (msg > m[t][j]) am[t][j] = e;    // strict: the first maximum in CSR order
+                }
                 m[t][j] = fmaxf(m[t][j], msg);
             }
         }
+    }
+    if constexpr (ARG) {
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+            *(int4*)(argmax + v * 768 + 4 * lane + 256 * t) = make_int4(am[t][0], am[t][1], am[t][2], am[t][3]);
     }
     const T* yr = Y + root_row * 768;
 #pragma unroll
@@ -792,6 +808,108 @@ __global__ __launch_bounds__(256) void combine_bwd_kernel(const T* __restrict__ 
             unsafeAtomicAdd(dY + (long)r.w * 768 + c0 + j, bs.w * g[j]);
         }
     }
+}
+
+// Scatter form of the same gradient without atomics (training forward recorded the argmax slots):
+// one 768-thread workgroup per SOURCE node u, thread = channel c; walking u's out-edges e = (u, v)
+// in a fixed order (the reversed plan's CSR), the slot p of e in v's in-edge list gets
+// dY[row(u, cell_s(e))][c] += basis_s(e) * g[v][c] wherever argmax[v][c] == p.  Accumulators are
+// LDS rows acc[cell][c] (each thread owns its channel column: no barriers, no bank conflicts);
+// every product row of u is written once (no memset), and the root row of u gets g[u].
+// Deterministic.  slot_of[e] = the CSR slot of edge e (fpm_spline_slot_of).
+__global__ __launch_bounds__(768) void combine_scatter_bwd_kernel(
+    const int* __restrict__ cell_off, const int* __restrict__ rowid, const int* __restrict__ mask,
+    const int* __restrict__ grp_e, const float* __restrict__ basis_e, const int* __restrict__ rptr,
+    const int* __restrict__ rcsr_e, const int* __restrict__ rnbr, const int* __restrict__ slot_of,
+    const int* __restrict__ argmax, long num_nodes, int nmax, const int* __restrict__ nvalid, int mode,
+    const float* __restrict__ gout, const float* __restrict__ hout, float* __restrict__ dY) {
+    extern __shared__ float acc[];                       // [NCELL - 1][768]
+    const long u = blockIdx.x;
+    const int c = threadIdx.x;
+    const int b = (int)(u / nmax);
+    const long base = (long)b * nmax;
+    const int nvb = nvalid[b];
+    auto gval = [&](long v) -> float {
+        if ((int)(v - base) >= nvb) return 0.f;
+        const float g = gout[v * 768 + c];
+        return mode == 0 ? (hout[v * 768 + c] > 0.f ? g : 0.f) : 0.1f * g;
+    };
+    const int m = mask[u];
+    for (int k = 0; k < NCELL - 1; ++k)
+        if ((m >> k) & 1) acc[k * 768 + c] = 0.f;
+    const int q0 = rptr[u], q1 = rptr[u + 1];
+    for (int q = q0; q < q1; ++q) {
+        const int e = rcsr_e[q];
+        const long v = base + rnbr[q];
+        const int p = slot_of[e];
+        if (argmax[v * 768 + c] != p) continue;
+        const float g = gval(v);
+        const int gg = grp_e[e];
+        const float4 bs = *(const float4*)(basis_e + 4 * (long)e);
+        acc[fpm::spline_cell(gg, 0) * 768 + c] += bs.x * g;
+        acc[fpm::spline_cell(gg, 1) * 768 + c] += bs.y * g;
+        acc[fpm::spline_cell(gg, 2) * 768 + c] += bs.z * g;
+        acc[fpm::spline_cell(gg, 3) * 768 + c] += bs.w * g;
+    }
+    for (int k = 0; k < NCELL - 1; ++k)
+        if ((m >> k) & 1) dY[(long)rowid[u * NCELL + k] * 768 + c] = acc[k * 768 + c];
+    dY[((long)cell_off[NCELL - 1] + u) * 768 + c] = gval(u);
+}
+
+// out[c][q] = rows[q] >= 0 ? in[rows[q]][c] : 0 for c < C, q < Q (ldo >= Q): the K-major operand
+// copies of the per-cell weight-gradient GEMMs (dW_cell = X_rows^T dY_rows as A B^T with
+// K = rows).  64 x 64 tiles through LDS (padded rows: conflict-free column reads).
+__global__ __launch_bounds__(256) void gather_transpose_f32_kernel(const float* __restrict__ in, long ldi,
+                                                                   const int* __restrict__ rows, long Q, int C,
+                                                                   float* __restrict__ out, long ldo) {
+    __shared__ float tile[64][65];
+    const long q0 = (long)blockIdx.x * 64;
+    const int c0 = blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int k = ty; k < 64; k += 4) {
+        const long q = q0 + k;
+        const int r = q < Q ? rows[q] : -1;
+        float v = 0.f;
+        if (r >= 0 && c0 + tx < C) v = in[(long)r * ldi + c0 + tx];
+        tile[k][tx] = v;
+    }
+    __syncthreads();
+    for (int k = ty; k < 64; k += 4) {
+        const int c = c0 + k;
+        if (c < C && q0 + tx < Q) out[(long)c * ldo + q0 + tx] = tile[tx][k];
+    }
+}
+
+// bf16: 32-bit global accesses on both sides (a channel pair per load, a row pair per store);
+// C % 64 == 0, Q % 2 == 0 and ldo even (the caller's padded chunks)
+__global__ __launch_bounds__(256) void gather_transpose_bf16_kernel(const bf16_t* __restrict__ in, long ldi,
+                                                                    const int* __restrict__ rows, long Q, int C,
+                                                                    bf16_t* __restrict__ out, long ldo) {
+    __shared__ uint32_t tile[64][33];                       // [q][channel pair]
+    const long q0 = (long)blockIdx.x * 64;
+    const int c0 = blockIdx.y * 64;
+    const int t = threadIdx.x, cp = t & 31, ry = t >> 5;    // 8 rows per pass
+    for (int k = ry; k < 64; k += 8) {
+        const long q = q0 + k;
+        const int r = q < Q ? rows[q] : -1;
+        uint32_t v = 0u;
+        if (r >= 0) v = *(const uint32_t*)(in + (long)r * ldi + c0 + 2 * cp);
+        tile[k][cp] = v;
+    }
+    __syncthreads();
+    const int qp = t & 31, cy = t >> 5;                     // 32 row pairs x 8 channels per pass
+    const bf16_t* T = (const bf16_t*)&tile[0][0];           // [q][66] halfwords
+    for (int c = cy; c < 64; c += 8) {
+        const long q = q0 + 2 * qp;
+        if (q >= Q) continue;
+        const uint32_t lo = T[(2 * qp) * 66 + c], hi = T[(2 * qp + 1) * 66 + c];
+        *(uint32_t*)(out + (long)(c0 + c) * ldo + q) = lo | (hi << 16);
+    }
+}
+
+__global__ void slot_of_kernel(const int* __restrict__ csr_e, long E, int* __restrict__ slot_of) {
+    const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < E) slot_of[csr_e[p]] = (int)p;
 }
 
 // dX[u] (+)= sum over u's product rows (cells in ascending order, then the root) of dXrows[row]:
@@ -896,6 +1014,26 @@ extern "C" int fpm_spline_plan(const int* src, const int* dst, const float* pseu
     return fpm::check_launch("fpm_spline_plan");
 }
 
+// K-major gather-transpose for the per-cell weight-gradient GEMMs (training): dtype 0 fp32, 1 bf16
+extern "C" int fpm_gather_transpose(int dtype, const void* in, long ldi, const int* rows, long Q, int C, void* out,
+                                    long ldo, void* stream) {
+    FPM_CHECK_ARG((dtype == 0 || dtype == 1) && Q >= 0 && C > 0 && ldo >= Q, "gather_transpose: bad args");
+    if (Q == 0) return 0;
+    const dim3 grid((unsigned)((Q + 63) / 64), (unsigned)((C + 63) / 64));
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == 0) {
+        hipLaunchKernelGGL(gather_transpose_f32_kernel, grid, dim3(256), 0, st, (const float*)in, ldi, rows, Q, C,
+                           (float*)out, ldo);
+    } else {
+        FPM_CHECK_ARG(C % 64 == 0 && Q % 2 == 0 && ldo % 2 == 0 && ldi % 2 == 0 && ((uintptr_t)in & 3) == 0 &&
+                          ((uintptr_t)out & 3) == 0,
+                      "gather_transpose: bf16 needs C %% 64 == 0, even Q / ldo / ldi, 4-B aligned buffers");
+        hipLaunchKernelGGL(gather_transpose_bf16_kernel, grid, dim3(256), 0, st, (const bf16_t*)in, ldi, rows, Q, C,
+                           (bf16_t*)out, ldo);
+    }
+    return fpm::check_launch("fpm_gather_transpose");
+}
+
 // Per-graph plan when every graph has <= 4096 edges and nmax <= 1024 (max_graph_edges: the
 // caller's bound, e.g. from the batch's host edge offsets); otherwise the global kernels.  The
 // scratch fields blk_cnt (per-graph cell counts / bases) and dslot (graph edge offsets) are reused.
@@ -952,10 +1090,25 @@ extern "C" int fpm_spline_plan_csr(void* ws, long E, long num_nodes, int** dst_p
 // x_op: operand copy of the input (dtype); W: (26, 768 out, 768 in) = the 25 spline cells then the
 // root weight transposed.  y_ws: fpm_spline_y_bytes bytes.  cscale (B,768) optionally scales the
 // operand output (X o c for the vertex affinity, affinity_layer.py:15).
+extern "C" int fpm_spline_conv_fwd_argmax(int dtype, const void* x_op, const void* plan_ws, long E, long num_nodes,
+                                          int nmax, const int* nvalid, const void* W, const float* bias, void* y_ws,
+                                          long y_ws_bytes, int mode, const float* xres, const float* cscale,
+                                          float* out_f, void* out_t, int* argmax, void* stream);
+
 extern "C" int fpm_spline_conv_fwd(int dtype, const void* x_op, const void* plan_ws, long E, long num_nodes, int nmax,
                                    const int* nvalid, const void* W, const float* bias, void* y_ws, long y_ws_bytes,
                                    int mode, const float* xres, const float* cscale, float* out_f, void* out_t,
                                    void* stream) {
+    return fpm_spline_conv_fwd_argmax(dtype, x_op, plan_ws, E, num_nodes, nmax, nvalid, W, bias, y_ws, y_ws_bytes, mode,
+                                      xres, cscale, out_f, out_t, nullptr, stream);
+}
+
+// the same, also writing argmax[num_nodes][768] (int32 CSR slot of each channel's max in-edge, -1
+// without in-edges) when argmax != nullptr -- the training forward, for the scatter backward
+extern "C" int fpm_spline_conv_fwd_argmax(int dtype, const void* x_op, const void* plan_ws, long E, long num_nodes,
+                                          int nmax, const int* nvalid, const void* W, const float* bias, void* y_ws,
+                                          long y_ws_bytes, int mode, const float* xres, const float* cscale,
+                                          float* out_f, void* out_t, int* argmax, void* stream) {
     using namespace fpm;
     FPM_CHECK_ARG(dtype == 0 || dtype == 1, "spline_conv: bad dtype");
     FPM_CHECK_ARG(mode == 0 || (mode == 1 && xres), "spline_conv: mode 1 needs xres");
@@ -1005,7 +1158,15 @@ extern "C" int fpm_spline_conv_fwd(int dtype, const void* x_op, const void* plan
                        (const int*)(w + L.dst_ptr), (const int4*)(w + L.rows4), (const float4*)(w + L.basis4),   \
                        num_nodes, nmax, nvalid, mode, xres, cscale, out_f, (T_*)out_t)
 #define FPM_COMB(T_, N_) do { if (pf) FPM_COMB1(T_, N_, true); else FPM_COMB1(T_, N_, false); } while (0)
-        if (dtype == 0) {
+        if (argmax) {
+#define FPM_COMBA(T_)                                                                                            \
+    hipLaunchKernelGGL((combine_kernel<T_, 4, false, true>), dim3((unsigned)(((graphs + 7) / 8) * 8 * ((nmax + 3) / 4))), \
+                       dim3(256), 0, st, (const T_*)y_ws, (const int*)(w + L.cell_off), bias,                    \
+                       (const int*)(w + L.dst_ptr), (const int4*)(w + L.rows4), (const float4*)(w + L.basis4),   \
+                       num_nodes, nmax, nvalid, mode, xres, cscale, out_f, (T_*)out_t, argmax)
+            if (dtype == 0) FPM_COMBA(float); else FPM_COMBA(bf16_t);
+#undef FPM_COMBA
+        } else if (dtype == 0) {
             if (npb == 16) FPM_COMB(float, 16); else if (npb == 8) FPM_COMB(float, 8); else FPM_COMB(float, 4);
         } else {
             if (npb == 16) FPM_COMB(bf16_t, 16); else if (npb == 8) FPM_COMB(bf16_t, 8); else FPM_COMB(bf16_t, 4);
@@ -1143,20 +1304,58 @@ extern "C" int fpm_spline_plan_rows(void* ws, long E, long num_nodes, int** arow
 //          reference's [cell][in][out] layout as the B operand (Wb, 26 x 768 x 768, operand dtype)
 //   dX   = per-node sum of its rows' dXr (accumulate: dX += ...)
 // y_ws: the forward's product rows of this layer; dY_op: bf16 copy of dY (dtype 1 only).
+extern "C" int fpm_spline_conv_bwd_data_scatter(int dtype, const void* plan_ws, const void* rplan_ws,
+                                                const int* argmax, long E, long num_nodes, int nmax,
+                                                const int* nvalid, const void* Wb, const void* y_ws, int mode,
+                                                const float* gout, const float* hout, float* dY, void* dY_op,
+                                                float* dXrows, float* dX, int accumulate, void* stream);
+
 extern "C" int fpm_spline_conv_bwd_data(int dtype, const void* plan_ws, long E, long num_nodes, int nmax,
                                         const int* nvalid, const void* Wb, const void* y_ws, int mode,
                                         const float* gout, const float* hout, float* dY, void* dY_op,
                                         float* dXrows, float* dX, int accumulate, void* stream) {
+    return fpm_spline_conv_bwd_data_scatter(dtype, plan_ws, nullptr, nullptr, E, num_nodes, nmax, nvalid, Wb, y_ws,
+                                            mode, gout, hout, dY, dY_op, dXrows, dX, accumulate, stream);
+}
+
+// rplan_ws (the plan of the reversed edges: its CSR lists each node's out-edges) + argmax (from
+// fpm_spline_conv_fwd_argmax): the atomic-free scatter backward; both null: the atomic one.
+extern "C" int fpm_spline_conv_bwd_data_scatter(int dtype, const void* plan_ws, const void* rplan_ws,
+                                                const int* argmax, long E, long num_nodes, int nmax,
+                                                const int* nvalid, const void* Wb, const void* y_ws, int mode,
+                                                const float* gout, const float* hout, float* dY, void* dY_op,
+                                                float* dXrows, float* dX, int accumulate, void* stream) {
     using namespace fpm;
     FPM_CHECK_ARG(dtype == 0 || dtype == 1, "spline_conv_bwd: bad dtype");
     FPM_CHECK_ARG(mode == 1 || (mode == 0 && hout), "spline_conv_bwd: mode 0 needs the layer output");
     FPM_CHECK_ARG(dtype == 0 || dY_op, "spline_conv_bwd: bf16 needs the dY operand buffer");
+    FPM_CHECK_ARG((rplan_ws == nullptr) == (argmax == nullptr), "spline_conv_bwd: rplan and argmax go together");
     PlanLayout L = plan_layout(E, num_nodes);
     const char* w = (const char*)plan_ws;
     hipStream_t st = (hipStream_t)stream;
     const int D = 768;
-    (void)hipMemsetAsync(dY, 0, (size_t)L.max_rows * D * sizeof(float), st);
     const unsigned nb = (unsigned)((num_nodes + 3) / 4);
+    if (argmax) {
+        // slot_of in the dXrows buffer (consumed before the GEMM overwrites it)
+        FPM_CHECK_ARG(L.max_rows * D >= E, "spline_conv_bwd: scratch too small");
+        int* slot_of = (int*)dXrows;
+        const char* rw = (const char*)rplan_ws;
+        hipLaunchKernelGGL(slot_of_kernel, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, st,
+                           (const int*)(w + L.csr_e), E, slot_of);
+        const size_t lds = (size_t)(NCELL - 1) * D * sizeof(float);
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute((const void*)combine_scatter_bwd_kernel,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            attr = true;
+        }
+        hipLaunchKernelGGL(combine_scatter_bwd_kernel, dim3((unsigned)num_nodes), dim3(D), lds, st,
+                           (const int*)(w + L.cell_off), (const int*)(w + L.rowid), (const int*)(w + L.mask),
+                           (const int*)(w + L.grp_e), (const float*)(w + L.basis_e), (const int*)(rw + L.dst_ptr),
+                           (const int*)(rw + L.csr_e), (const int*)(rw + L.nbr_local), (const int*)slot_of, argmax,
+                           num_nodes, nmax, nvalid, mode, gout, hout, dY);
+    } else {
+    (void)hipMemsetAsync(dY, 0, (size_t)L.max_rows * D * sizeof(float), st);
     if (dtype == 0)
         hipLaunchKernelGGL((combine_bwd_kernel<float>), dim3(nb), dim3(256), 0, st, (const float*)y_ws,
                            (const int*)(w + L.cell_off), (const int*)(w + L.dst_ptr), (const int4*)(w + L.rows4),
@@ -1165,6 +1364,7 @@ extern "C" int fpm_spline_conv_bwd_data(int dtype, const void* plan_ws, long E, 
         hipLaunchKernelGGL((combine_bwd_kernel<bf16_t>), dim3(nb), dim3(256), 0, st, (const bf16_t*)y_ws,
                            (const int*)(w + L.cell_off), (const int*)(w + L.dst_ptr), (const int4*)(w + L.rows4),
                            (const float4*)(w + L.basis4), num_nodes, nmax, nvalid, mode, gout, hout, dY);
+    }
     if (dtype == 1) {
         int rc = fpm_cast_bf16(dY, dY_op, L.max_rows * D, stream);
         if (rc) return rc;

@@ -160,14 +160,22 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
         if (fast) {
             anchors(mnl, mxl);
             float a0 = 0.f, a1 = 0.f;
+            // after a row step exp2(L_c) = exp2(a_c - lse(a_0, a_1)) is a two-way softmax: with
+            // t = exp2(-|a_1 - a_0|) the larger entry is 1 / (1 + t), the smaller t / (1 + t) -- one
+            // v_exp + one v_rcp per entry instead of urow's two v_exp + v_log and two more v_exp;
+            // the column targets exp2(-lcp_c) factor out of the sums
             forq([&](int k, float sv) {
-                float L0, L1;
-                Lpair(sv, mnl, mxl, L0, L1);
-                a0 += fpm::fast_exp2(L0 - lcp0);
-                a1 += fpm::fast_exp2(L1 - lcp1);
+                const float e0 = (-fabsf(sv - mnl)) * dscale - vu0, e1 = (-fabsf(sv - mxl)) * dscale - vu1;
+                if (e0 == -INFINITY && e1 == -INFINITY) return;   // the reference's NaN -> -inf entries
+                const float d = e1 - e0;
+                const float t = fpm::fast_exp2(-fabsf(d));
+                const float r = __builtin_amdgcn_rcpf(1.f + t);
+                const float lo = t * r;
+                a0 += d > 0.f ? lo : r;
+                a1 += d > 0.f ? r : lo;
             });
-            a0 = fpm::warp_sum(a0);
-            a1 = fpm::warp_sum(a1);
+            a0 = fpm::warp_sum(a0) * fpm::fast_exp2(-lcp0);
+            a1 = fpm::warp_sum(a1) * fpm::fast_exp2(-lcp1);
             if (lane == 0) { sa[wv] = a0; sb_[wv] = a1; }
             __syncthreads();
             a0 = 0.f; a1 = 0.f;

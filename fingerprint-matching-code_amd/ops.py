@@ -190,12 +190,21 @@ def spline_y_ws(dtype_code, E, num_nodes, device):
 
 
 def spline_conv(x_op, plan, E, num_nodes, nmax, nvalid, W, bias, y_ws, mode, xres=None, cscale=None, out_f=None,
-                out_t=None):
-    """W: (26, 768, 768) = spline cells [cell][out][in] then root^T."""
+                out_t=None, argmax=None):
+    """W: (26, 768, 768) = spline cells [cell][out][in] then root^T.  argmax (num_nodes, 768) int32:
+    optional per-channel max in-edge slots for spline_conv_bwd_data(..., rplan=, argmax=)."""
     _dev(x_op, plan, W, bias, y_ws)
     code = _code(x_op)
     if _code(W) != code or tuple(W.shape) != (26, 768, 768):
         raise _lib.FpmError("spline_conv: W must be (26, 768, 768) in the operand dtype")
+    if argmax is not None:
+        _shape(argmax, (num_nodes, 768), "spline_conv argmax")
+        if argmax.dtype != torch.int32:
+            raise _lib.FpmError("spline_conv: argmax must be int32")
+        _lib.call("fpm_spline_conv_fwd_argmax", code, _p(x_op), _p(plan), E, num_nodes, nmax, _p(nvalid), _p(W),
+                  _p(bias), _p(y_ws), y_ws.numel(), int(mode), _p(xres), _p(cscale), _p(out_f), _p(out_t),
+                  _p(argmax), _stream(x_op))
+        return
     _lib.call("fpm_spline_conv_fwd", code, _p(x_op), _p(plan), E, num_nodes, nmax, _p(nvalid), _p(W), _p(bias),
               _p(y_ws), y_ws.numel(), int(mode), _p(xres), _p(cscale), _p(out_f), _p(out_t), _stream(x_op))
 
@@ -392,16 +401,21 @@ def spline_plan_rows(plan, E, num_nodes):
 
 
 def spline_conv_bwd_data(x_op, plan, E, num_nodes, nmax, nvalid, Wb, y_ws, mode, gout, hout, dY, dY_op, dXrows, dX,
-                         accumulate=False):
-    """Input gradient of one SplineConv layer (see include/fpm.h); fills dY (product-row grads)."""
+                         accumulate=False, rplan=None, argmax=None):
+    """Input gradient of one SplineConv layer (see include/fpm.h); fills dY (product-row grads).
+    rplan (plan of the reversed edges) + argmax (from spline_conv(..., argmax=)): the atomic-free
+    scatter form."""
     _dev(plan, nvalid, Wb, y_ws, gout, dY, dXrows, dX)
     code = _code(x_op)
     if _code(Wb) != code or tuple(Wb.shape) != (26, 768, 768):
         raise _lib.FpmError("spline_conv_bwd: Wb must be (26, 768, 768) in the operand dtype")
     if mode == 0 and hout is None:
         raise _lib.FpmError("spline_conv_bwd: mode 0 needs the layer output")
-    _lib.call("fpm_spline_conv_bwd_data", code, _p(plan), E, num_nodes, nmax, _p(nvalid), _p(Wb), _p(y_ws), int(mode),
-              _p(gout), _p(hout), _p(dY), _p(dY_op), _p(dXrows), _p(dX), int(bool(accumulate)), _stream(gout))
+    if (rplan is None) != (argmax is None):
+        raise _lib.FpmError("spline_conv_bwd: rplan and argmax go together")
+    _lib.call("fpm_spline_conv_bwd_data_scatter", code, _p(plan), _p(rplan), _p(argmax), E, num_nodes, nmax,
+              _p(nvalid), _p(Wb), _p(y_ws), int(mode), _p(gout), _p(hout), _p(dY), _p(dY_op), _p(dXrows), _p(dX),
+              int(bool(accumulate)), _stream(gout))
 
 
 def kron_agg(X, C, B, n1max, n2max, tcsr1, tcsr2, q1, q2, n1, n2, adjoint, out):

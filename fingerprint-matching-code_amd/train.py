@@ -73,9 +73,14 @@ class SplineLayerFn(torch.autograd.Function):
         code = ops.BF16 if op == torch.bfloat16 else ops.F32
         yws = ops.spline_y_ws(code, sd.E, sd.num_nodes, x.device)
         out = torch.empty(sd.num_nodes, C.NODE_FEATURE_DIM, device=x.device, dtype=torch.float32)
+        # per-channel max in-edge slots for the atomic-free scatter backward (FPM_SPLINE_SCATTER=0:
+        # the atomic combine backward)
+        am = (torch.empty(sd.num_nodes, C.NODE_FEATURE_DIM, device=x.device, dtype=torch.int32)
+              if os.environ.get("FPM_SPLINE_SCATTER", "1") == "1" else None)
         ops.spline_conv(x_op, sd.plan, sd.E, sd.num_nodes, sd.nmax, sd.nvalid, Wf, bias.detach().contiguous(), yws,
-                        mode, xres=None if xres is None else xres.detach().contiguous(), out_f=out)
+                        mode, xres=None if xres is None else xres.detach().contiguous(), out_f=out, argmax=am)
         ctx.sd, ctx.mode, ctx.dmode, ctx.has_res = sd, mode, dmode, xres is not None
+        ctx.am = am
         ctx.save_for_backward(x_op, weight, root, out if mode == 0 else None)
         ctx.yws = yws
         return out
@@ -94,24 +99,81 @@ class SplineLayerFn(torch.autograd.Function):
         dXr = torch.empty_like(dY)
         dY_op = dY.to(op) if op == torch.bfloat16 else None
         dX = torch.empty(sd.num_nodes, C.NODE_FEATURE_DIM, device=dev, dtype=torch.float32)
+        rplan = None
+        if ctx.am is not None:
+            sd.out_csr()                                   # builds the reversed-edge plan once per side
+            rplan = sd._rplan
         ops.spline_conv_bwd_data(x_op, sd.plan, sd.E, sd.num_nodes, sd.nmax, sd.nvalid, Wb, ctx.yws, mode, gout,
-                                 out, dY, dY_op, dXr, dX)
+                                 out, dY, dY_op, dXr, dX, rplan=rplan, argmax=ctx.am)
         arows, cell_off = ops.spline_plan_rows(sd.plan, sd.E, sd.num_nodes)
         off = cell_off.cpu().tolist()
         total = off[-1]
-        rows = arows[:total].long()
-        dW = torch.zeros(C.SPLINE_CELLS + 1, C.NODE_FEATURE_DIM, C.NODE_FEATURE_DIM, device=dev, dtype=torch.float32)
-        if total > 0:
-            xg = x_op.index_select(0, rows)
-            dyg = dY_op[:total] if dY_op is not None else dY[:total]
-            for k in range(C.SPLINE_CELLS + 1):
-                r0, r1 = off[k], off[k + 1]
-                if r1 > r0:
-                    dW[k] = torch.mm(xg[r0:r1].t(), dyg[r0:r1]).float()   # [in][out], reference layout
+        dyg = dY_op if dY_op is not None else dY
+        if os.environ.get("FPM_SPLINE_WGRAD", "hip") == "hip":
+            dW = _spline_weight_grad(x_op, arows, dyg, off)
+        else:
+            # per-cell library products (bf16 outputs in the bf16 mode); A/B reference
+            rows = arows[:total].long()
+            dW = torch.zeros(C.SPLINE_CELLS + 1, C.NODE_FEATURE_DIM, C.NODE_FEATURE_DIM, device=dev,
+                             dtype=torch.float32)
+            if total > 0:
+                xg = x_op.index_select(0, rows)
+                for k in range(C.SPLINE_CELLS + 1):
+                    r0, r1 = off[k], off[k + 1]
+                    if r1 > r0:
+                        dW[k] = torch.mm(xg[r0:r1].t(), dyg[r0:r1]).float()   # [in][out], reference layout
         dbias = dY[off[25]:off[26]].sum(0)
         gx = dX
         gres = gout if ctx.has_res else None
         return gx, dW[:C.SPLINE_CELLS], dW[C.SPLINE_CELLS], dbias, gres, None, None, None
+
+
+_WG_KC = 4096
+
+
+def _spline_weight_grad(x_op, arows, dy, off):
+    """dW[k] = X[arows[rows of cell k]]^T dY[rows of cell k] for the 25 spline cells + root
+    ([in][out], the reference weight layout; spline_conv.py:28-41) on the library's MFMA GEMM:
+    both operands copied K-major (fpm_gather_transpose) with every cell's rows padded to whole
+    4096-row chunks, one batched A B^T over the chunks (fp32 accumulate and output), then the
+    chunk partials summed per cell in order (fpm_rows_sum)."""
+    dev = x_op.device
+    D = C.NODE_FEATURE_DIM
+    ncell = len(off) - 1
+    rows_k = [off[k + 1] - off[k] for k in range(ncell)]
+    nch = [(r + _WG_KC - 1) // _WG_KC for r in rows_k]
+    tot = sum(nch)
+    if tot == 0:
+        return torch.zeros(ncell, D, D, device=dev, dtype=torch.float32)
+    Q = tot * _WG_KC
+    P = [0]
+    for k in range(ncell):
+        P.append(P[-1] + nch[k] * _WG_KC)
+    Pd = torch.tensor(P, device=dev, dtype=torch.int64)
+    offd = torch.tensor(off, device=dev, dtype=torch.int64)
+    q = torch.arange(Q, device=dev, dtype=torch.int64)
+    k = torch.searchsorted(Pd, q, right=True) - 1
+    loc = q - Pd[k]
+    valid = loc < (offd[k + 1] - offd[k])
+    prow = torch.where(valid, offd[k] + loc, torch.zeros_like(loc))
+    ymap = torch.where(valid, prow, torch.full_like(prow, -1)).to(torch.int32)
+    xmap = torch.where(valid, arows[:max(off[-1], 1)].long()[prow.clamp(max=max(off[-1] - 1, 0))],
+                       torch.full_like(prow, -1)).to(torch.int32)
+    code = ops.BF16 if x_op.dtype == torch.bfloat16 else ops.F32
+    XT = torch.empty(D, Q, device=dev, dtype=x_op.dtype)
+    YT = torch.empty(D, Q, device=dev, dtype=dy.dtype)
+    _lib.call("fpm_gather_transpose", code, ops._p(x_op), x_op.stride(0), ops._p(xmap), Q, D, ops._p(XT), Q,
+              ops._stream(x_op))
+    _lib.call("fpm_gather_transpose", code, ops._p(dy), dy.stride(0), ops._p(ymap), Q, D, ops._p(YT), Q,
+              ops._stream(x_op))
+    part = torch.empty(tot, D, D, device=dev, dtype=torch.float32)
+    ops.gemm(XT, YT, D, D, _WG_KC, Q, Q, batch=tot, sA=_WG_KC, sB=_WG_KC, out_f=part, ldc=D, sC=D * D)
+    key = torch.tensor([kk for kk in range(ncell) for _ in range(nch[kk])], device=dev, dtype=torch.int32)
+    dW = afau_grad.rows_sum(part.view(tot, D * D), key, ncell).view(ncell, D, D)
+    for kk in range(ncell):
+        if nch[kk] == 0:
+            dW[kk].zero_()
+    return dW
 
 
 def _bmm_nn(A, Bm, op):

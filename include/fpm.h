@@ -126,6 +126,13 @@ int fpm_spline_plan_csr(void* ws, long E, long num_nodes, int** dst_ptr, int** n
 int fpm_spline_conv_fwd(int dtype, const void* x_op, const void* plan_ws, long E, long num_nodes, int nmax,
                         const int* nvalid, const void* W, const float* bias, void* y_ws, long y_ws_bytes, int mode,
                         const float* xres, const float* cscale, float* out_f, void* out_t, void* stream);
+/* the same, also writing argmax[num_nodes][768] (int32: CSR slot of the in-edge attaining each
+ * channel's max, the first in CSR order; -1 without in-edges) for fpm_spline_conv_bwd_data_scatter
+ * (the training forward) */
+int fpm_spline_conv_fwd_argmax(int dtype, const void* x_op, const void* plan_ws, long E, long num_nodes, int nmax,
+                               const int* nvalid, const void* W, const float* bias, void* y_ws, long y_ws_bytes,
+                               int mode, const float* xres, const float* cscale, float* out_f, void* out_t,
+                               int* argmax, void* stream);
 /* probe x gallery (C4): broadcast the shared source graph's SplineConv output y (rows x 768 fp32)
  * to B pairs: out_f[b] = y, out_t[b] = dtype(y o coef[b]) (coef may be NULL) -- the same values the
  * per-pair path's fused epilogue writes. */
@@ -349,6 +356,18 @@ int fpm_spline_plan_rows(void* plan_ws, long E, long num_nodes, int** arows, int
 int fpm_spline_conv_bwd_data(int dtype, const void* plan_ws, long E, long num_nodes, int nmax, const int* nvalid,
                              const void* Wb, const void* y_ws, int mode, const float* gout, const float* hout,
                              float* dY, void* dY_op, float* dXrows, float* dX, int accumulate, void* stream);
+/* the same without atomics: rplan_ws = the plan of the reversed edges (its CSR lists every node's
+ * out-edges), argmax from fpm_spline_conv_fwd_argmax; one workgroup per source node accumulates its
+ * product rows' gradients in LDS over its out-edges in a fixed order (deterministic, no memset) */
+int fpm_spline_conv_bwd_data_scatter(int dtype, const void* plan_ws, const void* rplan_ws, const int* argmax, long E,
+                                     long num_nodes, int nmax, const int* nvalid, const void* Wb, const void* y_ws,
+                                     int mode, const float* gout, const float* hout, float* dY, void* dY_op,
+                                     float* dXrows, float* dX, int accumulate, void* stream);
+/* out[c][q] = rows[q] >= 0 ? in[rows[q]][c] : 0 (c < C, q < Q; dtype 0 fp32, 1 bf16): K-major
+ * copies of the gathered node rows / product-row gradients for the per-cell SplineConv weight
+ * gradients dW_cell = X_rows^T dY_rows, run as fpm_gemm batches of fixed K chunks. */
+int fpm_gather_transpose(int dtype, const void* in, long ldi, const int* rows, long Q, int C, void* out, long ldo,
+                         void* stream);
 /* Factorised Kronecker SAGE-mean aggregation alone (SAGEConv mean over the association pattern,
  * gnn.py:208 / ngm.py:339-344): adjoint = 0 recomputes the forward's agg (T = in-edge CSRs);
  * adjoint = 1 with T = out-edge CSRs is its transpose (dX = A1^T (dagg / den) A2 + D o dagg / den).

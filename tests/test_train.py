@@ -7,6 +7,8 @@ Gradients are compared relative to their own scale: err = max|g - g_ref| / max|g
 tolerances are written per test; the tau = 0.01 Sinkhorns amplify fp32 forward differences,
 so the end-to-end bound is looser than the per-op ones.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -154,7 +156,11 @@ def test_kron_agg_forward_and_adjoint():
 
 
 # ---------------------------------------------------------------------------------- SplineConv
-def test_spline_layers_bwd_vs_autograd(sd):
+@pytest.mark.parametrize("scatter", ["1", "0"])
+def test_spline_layers_bwd_vs_autograd(sd, scatter, monkeypatch):
+    """Both SplineConv backward forms (atomic-free scatter over out-edges with the forward's argmax
+    slots; atomic combine backward) against autograd through the float64 oracle."""
+    monkeypatch.setenv("FPM_SPLINE_SCATTER", scatter)
     n1s = [40, 33, 21]
     pairs = synth.make_batch(11, 3, n1s, n2=[40, 33, 21])
     bt = DeviceBatch.from_pairs(pairs, DEV)
@@ -452,3 +458,32 @@ def test_bn_relu_train_vs_torch(shape):
     assert _rel(rmd, rmr) < 1e-5 and _rel(rvd, rvr) < 1e-5
     assert _rel(xd.grad, xr.grad) < 1e-4
     assert _rel(gd.grad, gr.grad) < 1e-4 and _rel(bd.grad, br.grad) < 1e-4
+
+
+def test_spline_scatter_bwd_matches_atomic(sd):
+    """At the C3 graph size (n = 256 Delaunay, bf16 operands) the scatter backward's input and
+    weight gradients equal the atomic form's up to summation order (the fp32 parity of both forms
+    against the oracle is test_spline_layers_bwd_vs_autograd)."""
+    pairs = synth.make_batch(19, 4, 256)
+    bt = DeviceBatch.from_pairs(pairs, DEV)
+    pre = params.SPLINE_PREFIX
+    res = {}
+    for scatter in ("1", "0"):
+        os.environ["FPM_SPLINE_SCATTER"] = scatter
+        try:
+            side = train._Side(bt, 1)
+            W = {k: sd[k].clone().to(DEV).requires_grad_(True) for k in sd if k.startswith(pre) and sd[k].is_floating_point()}
+            x0 = bt.x[1].clone().requires_grad_(True)
+            h = train.SplineLayerFn.apply(x0, W[pre + ".0.weight"], W[pre + ".0.root"], W[pre + ".0.bias"], None, side, 0,
+                                          "bf16")
+            o = train.SplineLayerFn.apply(h, W[pre + ".1.weight"], W[pre + ".1.root"], W[pre + ".1.bias"], x0, side, 1,
+                                          "bf16")
+            R = torch.randn(o.shape, generator=torch.Generator().manual_seed(4)).to(DEV)
+            (o * R).sum().backward()
+            res[scatter] = [x0.grad.clone()] + [W[k].grad.clone() for k in sorted(W)]
+        finally:
+            os.environ.pop("FPM_SPLINE_SCATTER", None)
+    # fp32 product-row gradients summed in another order, then rounded to bf16 for the grouped
+    # GEMM and the bf16 weight-gradient products: agreement at the bf16 ulp scale (2^-8)
+    for a, b in zip(res["1"], res["0"]):
+        assert _rel(a, b) < 1e-2
