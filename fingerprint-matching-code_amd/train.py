@@ -62,13 +62,34 @@ class _Side:
         return ops.plan_csr(self._rplan, self.E, self.num_nodes)
 
 
+_WCACHE = {}
+
+
+def _spline_w(weight, root, op, fwd):
+    """Operand copies of a SplineConv layer's weights: fwd (26, out, in) = cells transposed then
+    root^T (the forward GEMM's B), else (26, in, out) = the reference layout (the backward's B).
+    Both sides of the Siamese pair share the layer, so each copy is built once per weight version
+    (the optimizer step bumps ``_version``)."""
+    key = (weight.data_ptr(), root.data_ptr(), weight._version, root._version, op, fwd)
+    w = _WCACHE.get(key)
+    if w is None:
+        if len(_WCACHE) > 16:
+            _WCACHE.clear()
+        if fwd:
+            w = torch.cat([weight.detach().transpose(1, 2), root.detach().t()[None]]).contiguous().to(op)
+        else:
+            w = torch.cat([weight.detach(), root.detach()[None]]).contiguous().to(op)
+        _WCACHE[key] = w
+    return w
+
+
 class SplineLayerFn(torch.autograd.Function):
     """mode 0: relu(SplineConv(x)); mode 1: xres + 0.1 * SplineConv(x)   (spline_conv.py:33-38, 56)."""
 
     @staticmethod
     def forward(ctx, x, weight, root, bias, xres, sd, mode, dmode):
         op = _op_dtype(dmode)
-        Wf = torch.cat([weight.detach().transpose(1, 2), root.detach().t()[None]]).contiguous().to(op)
+        Wf = _spline_w(weight, root, op, True)
         x_op = x.detach().to(op).contiguous()
         code = ops.BF16 if op == torch.bfloat16 else ops.F32
         yws = ops.spline_y_ws(code, sd.E, sd.num_nodes, x.device)
@@ -92,7 +113,7 @@ class SplineLayerFn(torch.autograd.Function):
         op = _op_dtype(ctx.dmode)
         dev = gout.device
         gout = gout.contiguous().float()
-        Wb = torch.cat([weight.detach(), root.detach()[None]]).contiguous().to(op)
+        Wb = _spline_w(weight, root, op, False)
         nbytes = _lib.load().fpm_spline_y_bytes(ops.F32, sd.E, sd.num_nodes)
         rows_max = nbytes // (4 * C.NODE_FEATURE_DIM)
         dY = torch.empty(rows_max, C.NODE_FEATURE_DIM, device=dev, dtype=torch.float32)
