@@ -79,6 +79,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(PACKED ? 5
     float* Tg = T + (long)sub * n1max * TS;
     const long N = (long)n1max * n2max;
     const float* Xb = X + (long)b * C * N;
+    // the pair's C channels as one buffer resource (host check: C * N * 4 < 2^31)
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)Xb, (short)0, (int)(C * N * 4), 0x00020000);
+    const int N4 = (int)(N * 4);
     if (i == 0 && active) {
         const int beg = ptr2[(long)b * n2max + d], end = ptr2[(long)b * n2max + d + 1];
         nnb2_[sub] = end - beg;
@@ -134,11 +137,13 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(PACKED ? 5
         float acc[C];
 #pragma unroll
         for (int c = 0; c < C; ++c) acc[c] = 0.f;
+        // buffer loads: one 32-bit VGPR row offset + the channel as an SGPR offset, instead of
+        // 64-bit per-channel address math per load (~100 VALU per wave)
         auto add_row = [&](int nb) {
-            const float* row = Xb + (long)nb * n1max + i;
+            const int off = (nb * n1max + i) * 4;
             float v[C];
 #pragma unroll
-            for (int c = 0; c < C; ++c) v[c] = row[(long)c * N];
+            for (int c = 0; c < C; ++c) v[c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, off, c * N4, 0));
 #pragma unroll
             for (int c = 0; c < C; ++c) acc[c] += v[c];
         };
@@ -177,12 +182,18 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(PACKED ? 5
     if (i >= n1max || !active) return;
     const int n1b = n1[b], n2b = n2[b];
     const long p = (long)d * n1max + i;
+    // the pair's 17 output channels as one buffer resource: channel o at SGPR offset o * N4
+    const __amdgpu_buffer_rsrc_t orr = __builtin_amdgcn_make_buffer_rsrc((void*)(Xo + (long)b * 17 * N), (short)0,
+                                                                         (int)(17 * N * 4), 0x00020000);
+    auto store_o = [&](int o, float v) {
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), orr, (int)p * 4, o * N4, 0);
+    };
     const int beg = ptr1[(long)b * n1max + i], end = ptr1[(long)b * n1max + i + 1];
     const bool self = p < (long)n1b * n2b;
     float x[C], agg[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-        x[c] = Xb[(long)c * N + p];
+        x[c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, (int)p * 4, c * N4, 0));
         agg[c] = 0.f;
     }
     for (int e = beg; e < end; ++e) {
@@ -220,7 +231,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(PACKED ? 5
             h[m] = fmaxf(s, 0.f);
         }
         float z = 0.f, vp = 0.f;
-        float* Xob = Xo + (long)b * 17 * N + p;
 #pragma unroll
         for (int o = 0; o < 16; ++o) {
             float l = 0.f, r = 0.f, t = 0.f;
@@ -233,7 +243,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(PACKED ? 5
             for (int m = 0; m < 16; ++m) t += W[P::W2 + m * 16 + o] * h[m];
             float x1 = ((l + W[P::bl + o]) + r) + fmaxf(t + W[P::b2 + o], 0.f);
             if (vpart) vp = fmaf(cls_w[o], x1, vp);      // last layer: only w[0:16] . x1 is consumed
-            else Xob[(long)o * N] = x1;
+            else store_o(o, x1);
             z += W[P::wc + o] * x1;
         }
         if (vpart) vpart[(long)b * N + p] = vp;
@@ -266,7 +276,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(PACKED ? 5
 #pragma unroll
         for (int m = 0; m < 8; ++m) h[m] = (f2_t){fmaxf(h[m].x, 0.f), fmaxf(h[m].y, 0.f)};
         float z = 0.f, vp = 0.f;
-        float* Xob = Xo + (long)b * 17 * N + p;
         constexpr int OPB = 4;                            // output pairs per block (register budget)
 #pragma unroll
         for (int ob = 0; ob < 8; ob += OPB) {
@@ -294,8 +303,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(PACKED ? 5
                     vp = fmaf(cls_w[o], x1.x, vp);
                     vp = fmaf(cls_w[o + 1], x1.y, vp);
                 } else {
-                    Xob[(long)o * N] = x1.x;
-                    Xob[(long)(o + 1) * N] = x1.y;
+                    store_o(o, x1.x);
+                    store_o(o + 1, x1.y);
                 }
                 z = fmaf(W[P::wc + o], x1.x, z);
                 z = fmaf(W[P::wc + o + 1], x1.y, z);
@@ -314,7 +323,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(PACKED ? 5
         h[m] = (f2_t){fmaxf(s.x, 0.f), fmaxf(s.y, 0.f)};
     }
     float z = 0.f, vp = 0.f;
-    float* Xob = Xo + (long)b * 17 * N + p;
 #pragma unroll
     for (int op = 0; op < 8; ++op) {
         const int o = 2 * op;
@@ -332,8 +340,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(PACKED ? 5
             vp = fmaf(cls_w[o], x1.x, vp);
             vp = fmaf(cls_w[o + 1], x1.y, vp);
         } else {
-            Xob[(long)o * N] = x1.x;
-            Xob[(long)(o + 1) * N] = x1.y;
+            store_o(o, x1.x);
+            store_o(o + 1, x1.y);
         }
         z = fmaf(W[P::wc + o], x1.x, z);
         z = fmaf(W[P::wc + o + 1], x1.y, z);
@@ -434,6 +442,7 @@ extern "C" int fpm_kron_gnn_layer_fwd(const float* X, int C, int B, int n1max, i
     FPM_CHECK_ARG(!vpart || cls_w, "gnn_layer: vpart needs cls_w");
     if (B == 0) return 0;
     FPM_CHECK_ARG(n1max <= 1024, "gnn_layer: n1max must be <= 1024");
+    FPM_CHECK_ARG((long)C * n1max * n2max * 4 < (1L << 31), "gnn_layer: a pair's state must be < 2 GiB");
     dim3 grid(pair_grid(n2max, B));
     hipStream_t st = (hipStream_t)stream;
     const size_t sh = (size_t)(C == 1 ? 1 : 20) * n1max * 4;
