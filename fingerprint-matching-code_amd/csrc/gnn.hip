@@ -554,6 +554,80 @@ __global__ __launch_bounds__(1024) void kron_agg_kernel(const float* __restrict_
         out[(long)b * C * N + (long)c * N + (long)d * n1max + i] = adj ? acc : (dn > 0.f ? acc / dn : 0.f);
     }
 }
+// The same for C = 1 / 17 with the channel loops unrolled (C independent loads per neighbour row in
+// flight instead of a dependent per-channel loop) and the adjoint's per-element 1 / den(dd, i)
+// computed once per (neighbour, thread) from the thread's graph-1 degree and the neighbour's
+// graph-2 degree (multiplied, not divided: the gradient path has no bitwise contract).
+template <int C>
+__global__ __launch_bounds__(1024) void kron_agg_c_kernel(const float* __restrict__ X, int n1max, int n2max,
+                                                          const int* __restrict__ tptr1, const int* __restrict__ tnbr1,
+                                                          const int* __restrict__ tptr2, const int* __restrict__ tnbr2,
+                                                          const int* __restrict__ q1, const int* __restrict__ q2,
+                                                          const int* __restrict__ n1, const int* __restrict__ n2,
+                                                          int adj, float* __restrict__ out, int B) {
+    extern __shared__ float T[];                           // [i][C] node-major
+    int d, b;
+    if (!pair_block(n2max, B, b, d)) return;
+    const int i = threadIdx.x;
+    const long N = (long)n1max * n2max;
+    const float* Xb = X + (long)b * C * N;
+    const long nb1 = (long)b * n1max, nb2 = (long)b * n2max;
+    const long nn = (long)n1[b] * n2[b];
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)Xb, (short)0, (int)(C * N * 4), 0x00020000);
+    const int N4 = (int)(N * 4);
+    const int g1 = i < n1max ? q1[nb1 + i + 1] - q1[nb1 + i] : 0;
+    if (i < n1max) {
+        const int beg = tptr2[nb2 + d], end = tptr2[nb2 + d + 1];
+        float acc[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[c] = 0.f;
+        for (int e = beg; e < end; ++e) {
+            const int dd = tnbr2[e];
+            float sc = 1.f;
+            if (adj) {
+                const int g2 = q2[nb2 + dd + 1] - q2[nb2 + dd];
+                const float dn = (float)(g1 * g2 + (((long)dd * n1max + i) < nn ? 1 : 0));
+                sc = dn > 0.f ? 1.f / dn : 0.f;
+            }
+            const int off = (dd * n1max + i) * 4;
+            float v[C];
+#pragma unroll
+            for (int c = 0; c < C; ++c) v[c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, off, c * N4, 0));
+#pragma unroll
+            for (int c = 0; c < C; ++c) acc[c] = fmaf(v[c], sc, acc[c]);
+        }
+#pragma unroll
+        for (int c = 0; c < C; ++c) T[i * C + c] = acc[c];
+    }
+    __syncthreads();
+    if (i >= n1max) return;
+    const int beg = tptr1[nb1 + i], end = tptr1[nb1 + i + 1];
+    const long pos = (long)d * n1max + i;
+    const bool self = pos < nn;
+    const int g2d = q2[nb2 + d + 1] - q2[nb2 + d];
+    const float dn = (float)(g1 * g2d + (self ? 1 : 0));
+    const float rdn = dn > 0.f ? 1.f / dn : 0.f;
+    float acc[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc[c] = 0.f;
+    for (int e = beg; e < end; ++e) {
+        const float* Ta = T + tnbr1[e] * C;
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[c] += Ta[c];
+    }
+    const __amdgpu_buffer_rsrc_t orr = __builtin_amdgcn_make_buffer_rsrc((void*)(out + (long)b * C * N), (short)0,
+                                                                         (int)(C * N * 4), 0x00020000);
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        float a = acc[c];
+        if (self) {
+            const float x = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, (int)pos * 4, c * N4, 0));
+            a += adj ? x * rdn : x;
+        }
+        const float r = adj ? a : a * rdn;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r), orr, (int)pos * 4, c * N4, 0);
+    }
+}
 }  // namespace
 
 extern "C" int fpm_kron_agg(const float* X, int C, int B, int n1max, int n2max, const int* tptr1, const int* tnbr1,
@@ -566,6 +640,14 @@ extern "C" int fpm_kron_agg(const float* X, int C, int B, int n1max, int n2max, 
     if (sh > 65536)
         (void)hipFuncSetAttribute((const void*)kron_agg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
     const int threads = (n1max + 63) / 64 * 64;
+    if ((C == 1 || C == 17) && (long)C * n1max * n2max * 4 < (1L << 31)) {
+        void (*k)(const float*, int, int, const int*, const int*, const int*, const int*, const int*, const int*,
+                  const int*, const int*, int, float*, int) = C == 1 ? kron_agg_c_kernel<1> : kron_agg_c_kernel<17>;
+        if (sh > 65536) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
+        hipLaunchKernelGGL(k, dim3(pair_grid(n2max, B)), dim3(threads), sh, (hipStream_t)stream, X, n1max, n2max, tptr1,
+                           tnbr1, tptr2, tnbr2, q1, q2, n1, n2, adjoint, out, B);
+        return fpm::check_launch("fpm_kron_agg");
+    }
     hipLaunchKernelGGL(kron_agg_kernel, dim3(pair_grid(n2max, B)), dim3(threads), sh, (hipStream_t)stream, X, C, n1max,
                        n2max, tptr1, tnbr1, tptr2, tnbr2, q1, q2, n1, n2, adjoint, out, B);
     return fpm::check_launch("fpm_kron_agg");
