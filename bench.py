@@ -348,9 +348,11 @@ def main():
     # HBM bytes per launch of the same kernel from the committed rocprofv3 PMC pass (FETCH_SIZE x2 +
     # WRITE_SIZE, separate passes; tools/pmc_gemm.sh -> profiles/r01_pmc_product_gemm.json)
     traffic = None
-    pmc_file = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_pmc_product_gemm.json")
-    if args.dtype == "bf16" and args.config == "c3" and os.path.exists(pmc_file):
-        with open(pmc_file) as f:
+    pdir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
+    pmc_name = next((f for f in ("r02_pmc_product_gemm.json", "r01_pmc_product_gemm.json")
+                     if os.path.exists(os.path.join(pdir, f))), None)
+    if args.dtype == "bf16" and args.config == "c3" and pmc_name:
+        with open(os.path.join(pdir, pmc_name)) as f:
             traffic = json.load(f).get("traffic_bytes_per_launch")
 
     graph_build = None
@@ -400,7 +402,12 @@ def main():
             "roofline": {"kernel": "spline (node, cell) product GEMM (%s, grouped by cell)" % (("gemm_phase_kernel 256x256" if os.environ.get("FPM_GEMM_PHASE", "1") != "0" else "gemm_big_kernel<256>") if args.dtype == "bf16" else "gemm_kernel<f32>"),
                          "bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak, "traffic": traffic,
-                         "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, profiles/r01_pmc_product_gemm.json)",
+                         "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, profiles/%s)" % pmc_name,
+                         "traffic_source": "the committed PMC pass of the same kernel and config (separate FETCH_SIZE / "
+                                           "WRITE_SIZE runs, tools/pmc_gemm.sh); not measured in this run",
+                         "duration_note": "achieved / avg_launch_ms: HIP events around each launch on its stream in "
+                                          "the two-stream pipeline, so they include the co-running kernels' share of "
+                                          "the CUs; isolated_*: one extra single-stream forward",
                          "launches": cnt.value, "avg_launch_ms": ms.value / max(cnt.value, 1),
                          "algorithmic_flops_per_launch": fl.value / max(cnt.value, 1),
                          "isolated_achieved": (iso_fl.value / (iso_ms.value / 1e3)) / 1e12 if iso_ms.value > 0 else 0.0,
