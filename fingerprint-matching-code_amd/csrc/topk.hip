@@ -287,7 +287,8 @@ __global__ __launch_bounds__(256) void topk_select_kernel(const float* __restric
                                                           const int* __restrict__ assign, long asb,
                                                           const float* __restrict__ kvec, int n1max, int n2max,
                                                           float* __restrict__ perm, long pb, long pld,
-                                                          float* __restrict__ lsa_out, long lb, long lld) {
+                                                          float* __restrict__ lsa_out, long lb, long lld,
+                                                          int prezeroed) {
     __shared__ float val[kSelMax];
     __shared__ int key[kSelMax];
     __shared__ unsigned char rowt[kSelMax], colt[kSelMax];
@@ -306,8 +307,10 @@ __global__ __launch_bounds__(256) void topk_select_kernel(const float* __restric
                 for (int j = tid; j < n2max; j += 256) Z[i * zld + j] = 0.f;
         }
     };
-    zero_block(P, pld);
-    if (lsa_out) zero_block(lsa_out + (long)b * lb, lld);
+    if (!prezeroed) {
+        zero_block(P, pld);
+        if (lsa_out) zero_block(lsa_out + (long)b * lb, lld);
+    }
     for (int r = tid; r < kSelMax; r += 256) { rowt[r] = 0; colt[r] = 0; }
     int n = 1;
     while (n < n1max) n <<= 1;
@@ -331,47 +334,59 @@ __global__ __launch_bounds__(256) void topk_select_kernel(const float* __restric
             if (c >= 0) lsa_out[(long)b * lb + r * lld + c] = 1.f;
         }
     }
-    // bitonic sort: descending value, ascending flat index on ties
-    for (int size = 2; size <= n; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int t = tid; t < n / 2; t += 256) {
-                int lo = 2 * t - (t & (stride - 1));
-                int hi = lo + stride;
-                bool up = ((lo & size) == 0);
-                float va = val[lo], vb = val[hi];
-                int ka = key[lo], kb = key[hi];
-                bool a_first = (va > vb) || (va == vb && ka < kb);
-                if (a_first != up) {
-                    val[lo] = vb; val[hi] = va;
-                    key[lo] = kb; key[hi] = ka;
-                }
-            }
-            __syncthreads();
+    // The positive candidates are the assignment's matches (one per row, distinct columns), so the
+    // greedy walk over them in (value desc, flat index asc) order accepts the first K of them: a
+    // match is taken iff its rank in that order is < K.  Ranks by direct counting (each thread one
+    // or more rows against all n entries, LDS broadcast reads) instead of a bitonic sort and a
+    // serial walk; the zero-valued region (fewer than K positive matches) keeps the serial fill.
+    const int K = (int)rintf(kvec[b]);
+    __shared__ int nacc_s;
+    if (tid == 0) nacc_s = 0;
+    __syncthreads();
+    for (int r = tid; r < n1max; r += 256) {
+        const float v = val[r];
+        if (!(v > 0.f)) continue;
+        const int kr = key[r];
+        int rank = 0;
+        for (int t = 0; t < n1max; ++t) {
+            const float u = val[t];
+            rank += (u > v) || (u == v && key[t] < kr);
+        }
+        if (rank < K) {
+            const int c = kr - r * n2max;
+            rowt[r] = 1;
+            colt[c] = 1;
+            P[r * pld + c] = 1.f;
+            atomicAdd(&nacc_s, 1);
         }
     }
-    if (tid == 0) {
-        const int K = (int)rintf(kvec[b]);
-        int matched = 0;
-        for (int t = 0; t < n && matched < K; ++t) {
-            if (!(val[t] > 0.f)) break;
-            int q = key[t];
-            int r = q / n2max, c = q - r * n2max;
-            if (!rowt[r] && !colt[c]) {
-                rowt[r] = 1; colt[c] = 1;
-                P[r * pld + c] = 1.f;
-                ++matched;
-            }
+    __syncthreads();
+    // zero-valued region (fewer than K positive matches): the serial walk pairs the i-th free row
+    // with the i-th free column (both ascending) until K are taken -- done by one wave with ballot
+    // prefix counts (free columns listed in key[], no longer needed)
+    const int need = K - nacc_s;
+    if (need > 0 && tid < 64) {
+        const unsigned long long lt = (1ull << tid) - 1ull;
+        int nfc = 0;
+        for (int c0 = 0; c0 < n2max; c0 += 64) {
+            const int c = c0 + tid;
+            const bool f = c < n2max && !colt[c];
+            const unsigned long long m = __ballot(f);
+            if (f) key[nfc + __popcll(m & lt)] = c;
+            nfc += __popcll(m);
         }
-        int cp = 0;
-        for (int r = 0; r < n1max && matched < K; ++r) {
-            if (rowt[r]) continue;
-            while (cp < n2max && colt[cp]) ++cp;
-            if (cp >= n2max) break;
-            rowt[r] = 1; colt[cp] = 1;
-            P[r * pld + cp] = 1.f;
-            ++matched;
+        const int take = need < nfc ? need : nfc;
+        int i0 = 0;
+        for (int r0 = 0; r0 < n1max && i0 < take; r0 += 64) {
+            const int r = r0 + tid;
+            const bool f = r < n1max && !rowt[r];
+            const unsigned long long m = __ballot(f);
+            const int i = i0 + __popcll(m & lt);
+            if (f && i < take) P[r * pld + key[i]] = 1.f;
+            i0 += __popcll(m);
         }
     }
+    (void)n;
 }
 
 
@@ -466,8 +481,17 @@ extern "C" int fpm_topk_select(const float* ds, long d_sb, long d_ld, const int*
     FPM_CHECK_ARG(n1max > 0 && n2max > 0 && n1max <= kSelMax && n2max <= kSelMax,
                   "topk_select: 0 < n1max, n2max <= %d required (got %d, %d)", kSelMax, n1max, n2max);
     if (B == 0) return 0;
-    hipLaunchKernelGGL(topk_select_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, ds, d_sb, d_ld, assign, a_sb,
-                       k, n1max, n2max, perm, p_sb, p_ld, lsa_out, l_sb, l_ld);
+    // dense outputs: one wide fill of the whole batch range first (a workgroup per pair zeroing its
+    // 2 x n1max x n2max floats left half the CUs issuing stores: ~1 TB/s)
+    const long box = (long)n1max * n2max;
+    const bool dense = p_ld == n2max && p_sb == box && (!lsa_out || (l_ld == n2max && l_sb == box));
+    hipStream_t st = (hipStream_t)stream;
+    if (dense) {
+        (void)hipMemsetAsync(perm, 0, (size_t)B * box * sizeof(float), st);
+        if (lsa_out) (void)hipMemsetAsync(lsa_out, 0, (size_t)B * box * sizeof(float), st);
+    }
+    hipLaunchKernelGGL(topk_select_kernel, dim3(B), dim3(256), 0, st, ds, d_sb, d_ld, assign, a_sb, k, n1max, n2max,
+                       perm, p_sb, p_ld, lsa_out, l_sb, l_ld, dense ? 1 : 0);
     return fpm::check_launch("fpm_topk_select");
 }
 

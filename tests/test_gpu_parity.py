@@ -150,6 +150,34 @@ def test_topk_select_golden():
     np.testing.assert_array_equal(perm.cpu().numpy(), z["perm"])
 
 
+@pytest.mark.parametrize("n1s,n2s,ks", [
+    ((40, 31, 40), (40, 40, 22), (38.0, 30.5, 21.0)),     # k above the positive matches: zero-region fill
+    ((256, 200), (256, 256), (120.5, 199.0)),
+    ((64, 64), (64, 64), (7.0, 64.0)),
+])
+def test_topk_select_ranks_and_zero_region(n1s, n2s, ks):
+    """fpm_topk_select (parallel ranks of the matches + ballot-counted zero-region fill) against the
+    reference flow: prod = lsa * ds, stable descending argsort, greedy_perm (ngm.py:445-449,
+    soft_topk.py:56-77), on matrices with many exact zeros and tied values."""
+    g = torch.Generator().manual_seed(sum(n1s))
+    B, n1max, n2max = len(n1s), max(n1s), max(n2s)
+    ds = torch.rand(B, n1max, n2max, generator=g)
+    ds = torch.where(torch.rand(B, n1max, n2max, generator=g) < 0.6, torch.zeros_like(ds), ds)
+    ds = (ds * 8).round() / 8                                  # tied values
+    for b in range(B):
+        ds[b, n1s[b]:, :] = 0
+        ds[b, :, n2s[b]:] = 0
+    n1, n2 = torch.tensor(n1s, dtype=torch.int32), torch.tensor(n2s, dtype=torch.int32)
+    assign = ops.lsa_batch_host(ds, n1, n2)
+    kk = torch.tensor(ks)
+    perm = ops.topk_select(ds.to(DEV), assign.to(DEV), kk.to(DEV)).cpu()
+    lsa = O.hungarian(ds, n1s, n2s)
+    prod = (lsa * ds).reshape(B, -1)
+    top = torch.argsort(-prod, dim=-1, stable=True)
+    ref = O.greedy_perm(torch.zeros(B, n1max, n2max), top, kk)
+    assert torch.equal(perm, ref)
+
+
 # ---------------------------------------------------------------------------------------- GEMM
 @pytest.mark.parametrize("dt,tol", [(torch.float32, 2e-5), (torch.bfloat16, 2e-2)])
 def test_gemm_vs_torch(dt, tol):
