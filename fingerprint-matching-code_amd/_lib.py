@@ -28,6 +28,7 @@ SIGNATURES = {
     "fpm_global_weights": (I, [P, L, P, L, I, I, I, P, L, P]),
     "fpm_split_bf16x3": (I, [P, L, L, I, I, P, L, P]),
     "fpm_copy_async": (I, [P, P, L, I, P]),
+    "fpm_memcpy_async": (I, [P, P, L, I, P]),
     "fpm_set_tuning": (I, [ctypes.c_char_p, I]),
     "fpm_spline_plan_bytes": (L, [L, L]),
     "fpm_spline_plan": (I, [P, P, P, L, L, I, P, L, P]),

@@ -76,6 +76,28 @@ int& gemm_aff_big_flag() {
     return on;
 }
 
+int& gemm_persist_flag() {
+    static int on = [] {
+        const char* e = getenv("FPM_GEMM_PERSIST");
+        return e ? atoi(e) : 0;
+    }();
+    return on;
+}
+
+// one persistent workgroup per CU (whole rounds of the 8 XCDs)
+int gemm_persist_grid() {
+    static int g = [] {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 8)
+            cus = 256;
+        const char* e = getenv("FPM_GEMM_PERSIST_GRID");   // A/B: fewer workgroups than CUs
+        if (e && atoi(e) >= 8 && atoi(e) < cus) cus = atoi(e);
+        return cus / 8 * 8;
+    }();
+    return g;
+}
+
 int& gemm_phase_flag() {
     static int on = [] {
         const char* e = getenv("FPM_GEMM_PHASE");
@@ -102,6 +124,7 @@ int& soft_topk_fast_flag();
 extern "C" int fpm_set_tuning(const char* key, int value) {
     int* f = nullptr;
     if (key && !strcmp(key, "gemm_phase")) f = &fpm::gemm_phase_flag();
+    else if (key && !strcmp(key, "gemm_persist")) f = &fpm::gemm_persist_flag();
     else if (key && !strcmp(key, "gemm_aff_big")) f = &fpm::gemm_aff_big_flag();
     else if (key && !strcmp(key, "gnn_packed")) f = &gnn_packed_flag();
     else if (key && !strcmp(key, "gnn_unroll")) f = &gnn_unroll_flag();
@@ -132,10 +155,30 @@ __global__ void cast_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict
     long stride = (long)gridDim.x * blockDim.x;
     for (; i < n; i += stride) y[i] = fpm::f2bf(x[i]);
 }
+
+// 8 values per thread: two 16-B loads, one 16-B store (the scalar form ran at ~1.6 TB/s with 2-B
+// stores); same rounding, bit-identical
+__global__ __launch_bounds__(256) void cast_bf16_v8_kernel(const float4* __restrict__ x, uint4* __restrict__ y, long n8) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n8) return;
+    const float4 a = x[2 * i], b = x[2 * i + 1];
+    uint4 o;
+    o.x = (uint32_t)fpm::f2bf(a.x) | ((uint32_t)fpm::f2bf(a.y) << 16);
+    o.y = (uint32_t)fpm::f2bf(a.z) | ((uint32_t)fpm::f2bf(a.w) << 16);
+    o.z = (uint32_t)fpm::f2bf(b.x) | ((uint32_t)fpm::f2bf(b.y) << 16);
+    o.w = (uint32_t)fpm::f2bf(b.z) | ((uint32_t)fpm::f2bf(b.w) << 16);
+    y[i] = o;
+}
 }  // namespace
 
 extern "C" int fpm_cast_bf16(const float* x, void* y, long n, void* stream) {
     if (n <= 0) return 0;
+    if (n % 8 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0) {
+        const long n8 = n / 8;
+        hipLaunchKernelGGL(cast_bf16_v8_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                           (const float4*)x, (uint4*)y, n8);
+        return fpm::check_launch("fpm_cast_bf16");
+    }
     long blocks = (n + 255) / 256;
     if (blocks > 65536) blocks = 65536;
     hipLaunchKernelGGL(cast_bf16_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, (bf16_t*)y, n);
@@ -231,4 +274,18 @@ extern "C" int fpm_copy_async(const void* src, void* dst, long bytes, int nblock
     hipLaunchKernelGGL(copy16_kernel, dim3(nblocks), dim3(1024), 0, (hipStream_t)stream, (const u32x4_t*)src, (u32x4_t*)dst,
                        bytes / 16);
     return fpm::check_launch("fpm_copy_async");
+}
+
+// hipMemcpyAsync with an explicit copy kind (2 = device -> host, 1024 = hipMemcpyDeviceToDeviceNoCU:
+// a copy engine instead of a blit kernel, for a pinned host destination the device can address).
+// Used for the ds_mat hand-off to the host Hungarian pool (model.py, FPM_COPY_KIND).
+extern "C" int fpm_memcpy_async(void* dst, const void* src, long bytes, int kind, void* stream) {
+    FPM_CHECK_ARG(bytes >= 0, "memcpy_async: negative size");
+    if (bytes == 0) return 0;
+    const hipError_t e = hipMemcpyAsync(dst, src, (size_t)bytes, (hipMemcpyKind)kind, (hipStream_t)stream);
+    if (e != hipSuccess) {
+        fpm::set_error("fpm_memcpy_async(kind %d): %s", kind, hipGetErrorString(e));
+        return 1;
+    }
+    return 0;
 }

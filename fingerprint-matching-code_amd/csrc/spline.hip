@@ -142,8 +142,10 @@ __global__ __launch_bounds__(256) void plan_blkcount_kernel(const int* __restric
 
 // one block: per-cell exclusive scan over blocks (in place), cell offsets, GEMM tile table, and the
 // exclusive scan of in-degrees -> dst CSR pointers.
+// The number of real tiles is also stored at *count (cell_off[27] for 128-row tiles, [28] for
+// 256-row tiles): the persistent product GEMM walks only those.
 __device__ void build_tile_table(const int* coff, const int* cell_tot, int* tile_off, int tb, int* tile_info,
-                                 int max_tiles) {
+                                 int max_tiles, int* count) {
     const int tid = threadIdx.x;
     if (tid == 0) {
         int t = 0;
@@ -152,6 +154,7 @@ __device__ void build_tile_table(const int* coff, const int* cell_tot, int* tile
             t += (cell_tot[k] + tb - 1) / tb;
         }
         tile_off[NCELL] = t;
+        *count = t;
     }
     __syncthreads();
     for (int t = tid; t < max_tiles; t += blockDim.x) {
@@ -208,8 +211,8 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(int* blk_cnt, long nblk
         coff[NCELL] = off;
     }
     __syncthreads();
-    build_tile_table(coff, cell_tot, tile_off, fpm::GBM, tile_info, max_tiles);
-    build_tile_table(coff, cell_tot, tile_off, fpm::G2_BM, tile_info2, max_tiles2);
+    build_tile_table(coff, cell_tot, tile_off, fpm::GBM, tile_info, max_tiles, cell_off + NCELL + 1);
+    build_tile_table(coff, cell_tot, tile_off, fpm::G2_BM, tile_info2, max_tiles2, cell_off + NCELL + 2);
     // (2) exclusive scan of indeg -> dst_ptr, tiled through LDS (coalesced global reads/writes)
     constexpr int TILE = 16384, PER = TILE / 1024;
     int* buf = tilebuf;
@@ -499,8 +502,8 @@ __global__ __launch_bounds__(1024) void plan_graph_scan_kernel(int* cellcnt, int
         coff[NCELL] = off;
     }
     __syncthreads();
-    build_tile_table(coff, cell_tot, tile_off, fpm::GBM, tile_info, max_tiles);
-    build_tile_table(coff, cell_tot, tile_off, fpm::G2_BM, tile_info2, max_tiles2);
+    build_tile_table(coff, cell_tot, tile_off, fpm::GBM, tile_info, max_tiles, cell_off + NCELL + 1);
+    build_tile_table(coff, cell_tot, tile_off, fpm::G2_BM, tile_info2, max_tiles2, cell_off + NCELL + 2);
 }
 
 // K3: rowid / arows (ranks of the graph's nodes per cell, in node order), then the CSR slots'
@@ -1141,6 +1144,10 @@ extern "C" int fpm_spline_conv_fwd_argmax(int dtype, const void* x_op, const voi
             (void)hipEventRecord(rec.a, st);
         }
         if (dtype == 0) hipLaunchKernelGGL((gemm_kernel<float, false>), grid, dim3(GTHREADS), 0, st, p);
+        else if (use_gemm_phase(D) && gemm_persist_flag() && D / G2_BK >= 3 && D % 256 == 0 &&
+                 (long)p.M * p.ldc * 2 < (1L << 31))
+            hipLaunchKernelGGL(gemm_phase_persist_kernel<EPI_STORE>, dim3(gemm_persist_grid()), dim3(G2_THREADS), 0, st, p,
+                               (const int*)(w + L.cell_off) + NCELL + 2);
         else if (use_gemm_phase(D)) hipLaunchKernelGGL((gemm_phase_kernel<EPI_STORE, false>), grid, dim3(G2_THREADS), 0, st, p);
         else hipLaunchKernelGGL((gemm_big_kernel<256, EPI_STORE, false>), grid, dim3(G2_THREADS), 0, st, p);
         if (g_prof_on && g_prof_rows && rec.slot < PROF_MAX) {

@@ -123,6 +123,9 @@ class Net(nn.Module):
         self.copy_stream = os.environ.get("FPM_COPY_STREAM", "1") == "1"
         # > 0: ds_mat D2H on this many workgroups (fpm_copy_async) instead of the runtime's blit
         self.copy_blocks = int(os.environ.get("FPM_COPY_BLOCKS", "0"))
+        # > 0: ds_mat D2H through hipMemcpyAsync with this copy kind (fpm_memcpy_async; 1024 = the
+        # no-compute-unit device-to-device kind, i.e. a copy engine instead of the blit kernel)
+        self.copy_kind = int(os.environ.get("FPM_COPY_KIND", "0"))
         # the host thread waits for each chunk's ds_mat with a sleeping (not spinning) event wait,
         # leaving its core to the Hungarian pool
         self.blocking_wait = os.environ.get("FPM_BLOCKING_WAIT", "1") == "1"
@@ -490,7 +493,9 @@ class Net(nn.Module):
             cs = self._copy_stream(dev)
             cs.wait_event(done)
             with torch.cuda.stream(cs):
-                if self.copy_blocks > 0:
+                if self.copy_kind > 0:
+                    ops.memcpy_async(self._pinned[b0:b1], o["ds_mat"][b0:b1], self.copy_kind)
+                elif self.copy_blocks > 0:
                     ops.copy_async(self._pinned[b0:b1], o["ds_mat"][b0:b1], self.copy_blocks)
                 else:
                     self._pinned[b0:b1].copy_(o["ds_mat"][b0:b1], non_blocking=True)

@@ -571,3 +571,15 @@ def hungarian(s, n1=None, n2=None, nproc=1):
     perm[r[:, 0], r[:, 1], a[r[:, 0], r[:, 1]].long()] = 1.0
     perm = perm.to(device=s.device, dtype=s.dtype)
     return perm.squeeze(0) if matrix_input else perm
+
+
+def memcpy_async(dst, src, kind=2):
+    """dst.copy_(src) through hipMemcpyAsync with an explicit copy kind on the current stream
+    (fpm_memcpy_async): 2 = device -> host, 1024 = device-to-device without compute units."""
+    _dev(src)
+    if not (src.is_contiguous() and dst.is_contiguous()) or src.numel() * src.element_size() != dst.numel() * dst.element_size():
+        raise _lib.FpmError("memcpy_async: contiguous tensors of equal size expected")
+    if not dst.is_cuda and not dst.is_pinned():
+        raise _lib.FpmError("memcpy_async: host destination must be pinned")
+    _lib.call("fpm_memcpy_async", _p(dst), _p(src), src.numel() * src.element_size(), int(kind), _stream(src))
+    return dst

@@ -86,11 +86,18 @@ int fpm_cast_bf16(const float* x, void* y, long n, void* stream);
  * the host Hungarian (ngm.py:444 -> utils/hungarian.py:44 .cpu()) without the runtime's
  * one-workgroup-per-CU blit.  16-B aligned pointers, bytes % 16 == 0. */
 int fpm_copy_async(const void* src, void* dst, long bytes, int nblocks, void* stream);
+/* hipMemcpyAsync with an explicit kind (2 = device -> host, 1024 = device-to-device without compute
+ * units, i.e. a copy engine, for a device-addressable pinned host destination): the same hand-off. */
+int fpm_memcpy_async(void* dst, const void* src, long bytes, int kind, void* stream);
 
 /* Kernel-variant switches for A/B timing.  Returns the
  * previous value, or -1 (error channel set) for an unknown key.  No reference counterpart.
  *   "gemm_phase" (env FPM_GEMM_PHASE, default 1): 256x256 bf16 GEMM tiles on the phase-pipelined
  *                kernel (1) or the two-stage kernel (0)
+ *   "gemm_persist" (env FPM_GEMM_PERSIST, default 0): the SplineConv product GEMM as a persistent
+ *                kernel (one workgroup per CU over the plan's real tiles, next tile's DMA prologue under
+ *                the current epilogue; bit-identical; +9 % alone, -1.5 % inside the two-stream forward);
+ *                env FPM_GEMM_PERSIST_GRID caps its workgroup count
  *   "gnn_packed" (env FPM_GNN_PACKED, default 1): GNN-layer MLPs on packed (1) or scalar (0) FMAs
  *   "gnn_group"  (FPM_GNN_GROUP, default 2): graph-2 nodes per GNN workgroup (1, 2, 4; n1max <= 256)
  *   "gnn_group1" (FPM_GNN_GROUP1, default 0): the same for the 1-channel first layer

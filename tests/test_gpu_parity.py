@@ -646,7 +646,7 @@ def test_gnn_kernel_variants_bit_identical(sd):
     bt = DeviceBatch.from_pairs(pairs, DEV)
     outs = []
     for key, val in (("gnn_group", 1), ("gnn_group", 2), ("gnn_unroll", 3), ("combine_npb", 16), ("gnn_wide", 1), ("gnn_il", 1),
-                     ("plan_graph", 0), ("combine_pf", 0), ("combine_pf", 1)):
+                     ("plan_graph", 0), ("combine_pf", 0), ("combine_pf", 1), ("gemm_persist", 1)):
         prev = ops.set_tuning(key, val)
         try:
             r = net.run(bt, chunks=1)
@@ -753,3 +753,50 @@ def test_plan_per_graph_equals_global(n, n2):
             ops.set_tuning("plan_graph", prev)
     for k in ("feat0", "feat1", "s", "ss"):
         assert torch.equal(outs[0][k], outs[1][k]), k
+
+
+# ------------------------------------------------------------------------------------- bf16 cast
+@pytest.mark.parametrize("n", [768 * 300, 8 * 7, 13, 1000003])
+def test_cast_bf16_round_to_nearest_even(n):
+    """fpm_cast_bf16 (16-B vector path when n % 8 == 0, scalar tail path otherwise) equals torch's
+    round-to-nearest-even float32 -> bfloat16 conversion bit for bit."""
+    g = torch.Generator().manual_seed(n)
+    x = (torch.randn(n, generator=g) * torch.exp(torch.randn(n, generator=g) * 4)).to(DEV)
+    y = ops.cast_bf16(x)
+    torch.cuda.synchronize()
+    assert torch.equal(y.view(torch.int16), x.to(torch.bfloat16).view(torch.int16))
+
+
+@pytest.mark.parametrize("kind", [2, 1024])
+def test_memcpy_async_kinds_to_pinned(kind):
+    """The ds_mat hand-off copy through fpm_memcpy_async (device -> host, and the
+    no-compute-unit kind) delivers the same bytes into pinned host memory."""
+    x = torch.randn(64, 256, 256, device=DEV)
+    h = torch.empty(x.shape, dtype=x.dtype, pin_memory=True)
+    ops.memcpy_async(h, x, kind)
+    torch.cuda.synchronize()
+    assert torch.equal(h, x.cpu())
+
+
+@pytest.mark.parametrize("npairs,n", [(24, 256), (5, 100), (1, 32)])
+def test_gemm_persist_bit_identical(sd, npairs, n):
+    """The persistent product GEMM (one workgroup per CU walking the plan's real tiles, next tile's
+    prologue under the current epilogue) against the one-shot phase kernel: identical forwards.
+    24 pairs of n = 256 give ~700 tiles (several per workgroup: the tile-boundary path), the small
+    batches fewer tiles than workgroups."""
+    pairs = synth.make_batch(29 + n, npairs, n)
+    net = fpm.Net(regression=True, backbone=False, dtype="bf16")
+    net.load_state_dict(sd)
+    bt = DeviceBatch.from_pairs(pairs, DEV)
+    outs = []
+    for val in (0, 1, 0, 1):
+        prev = ops.set_tuning("gemm_persist", val)
+        try:
+            r = net.run(bt, chunks=1)
+            torch.cuda.synchronize()
+        finally:
+            ops.set_tuning("gemm_persist", prev)
+        outs.append(r)
+    for r in outs[1:]:
+        for k in ("s", "ss", "ds_mat", "k_prob", "perm_mat"):
+            assert torch.equal(r[k], outs[0][k]), k
