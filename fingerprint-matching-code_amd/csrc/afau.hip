@@ -10,6 +10,7 @@
 // The projections/FFN are MFMA GEMMs through fpm_gemm.
 #include "fpm_common.h"
 #include <cstdlib>
+#include <type_traits>
 
 namespace {
 
@@ -56,7 +57,8 @@ __global__ __launch_bounds__(256) void afau_row_attn_kernel(const float* __restr
     const int b = blockIdx.x, i0 = blockIdx.y * 16, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int n2b = n2[b];
 
-    // ---- score LUTs of the 16 heads
+    // ---- score LUTs of the 16 heads (LUT mode only)
+    if (use_lut) {
     {
         const int hh = tid >> 4, m = tid & 15;
         const float w = mix1w[(hh * 2 + 1) * 16 + m];
@@ -110,6 +112,7 @@ __global__ __launch_bounds__(256) void afau_row_attn_kernel(const float* __restr
         S.lbp[hh][bk] = make_float4(bp[0], bp[1], bp[2], bp[3]);
     }
     __syncthreads();
+    }
 
     // ---- costs and the first head's V (B operand: V[j][d], d = lane & 15)
     const int r = lane & 15, i = i0 + r, jbase = wv * 4 * TJ + (lane >> 4);
@@ -121,9 +124,41 @@ __global__ __launch_bounds__(256) void afau_row_attn_kernel(const float* __restr
         creg[t] = (i < n1max && j < n2max) ? Cb[j] : 0.f;
         vreg[t] = j < n2b ? Wv[(long)r * emb + j] : 0.f;
     }
+    typedef float f2v __attribute__((ext_vector_type(2)));
     for (int h = 0; h < 16; ++h) {
         float p[TJ];
         float mloc = -INFINITY;
+        if (!use_lut) {
+            // the 16-term sum, m outer: the head's 48 weights are wave-uniform (scalar operands),
+            // element pairs on v_pk_fma_f32; per element the same fma chain as the scalar form
+            // sc = sum_m fma(relu(fma(c, w1, b1)), w2, sc) + b2 (no LDS lookups, no dependent loads)
+            f2v acc2[TJ / 2];
+#pragma unroll
+            for (int t2 = 0; t2 < TJ / 2; ++t2) acc2[t2] = (f2v){0.f, 0.f};
+            const float* w1p = mix1w + (h * 2 + 1) * 16;
+            const float* b1p = mix1b + h * 16;
+            const float* w2p = mix2w + h * 16;
+#pragma unroll
+            for (int m = 0; m < 16; ++m) {
+                const float w1 = w1p[m], b1 = b1p[m], w2 = w2p[m];
+#pragma unroll
+                for (int t2 = 0; t2 < TJ / 2; ++t2) {
+                    f2v u = (f2v){creg[2 * t2], creg[2 * t2 + 1]} * w1 + b1;
+                    u.x = fmaxf(u.x, 0.f);
+                    u.y = fmaxf(u.y, 0.f);
+                    acc2[t2] = u * w2 + acc2[t2];
+                }
+            }
+            const float b2 = mix2b[h];
+#pragma unroll
+            for (int t2 = 0; t2 < TJ / 2; ++t2) {
+                p[2 * t2] = acc2[t2].x + b2;
+                p[2 * t2 + 1] = acc2[t2].y + b2;
+            }
+#pragma unroll
+            for (int t = 0; t < TJ; ++t)
+                if (jbase + 4 * t < n2max) mloc = fmaxf(mloc, p[t]);
+        } else
 #pragma unroll
         for (int t = 0; t < TJ; ++t) {
             const float c = creg[t];
@@ -174,7 +209,11 @@ __global__ __launch_bounds__(256) void afau_row_attn_kernel(const float* __restr
 #pragma unroll
         for (int k = 0; k < 4; ++k) S.part[buf][wv][(4 * (lane >> 4) + k) * 16 + r] = acc[k];
         if (lane < 16) S.rowms[buf][wv][lane] = make_float2(mloc, sloc);
-        __syncthreads();
+        // LDS-only barrier: __syncthreads() would also wait for the next head's V loads just
+        // issued and for this head's output stores (vmcnt(0)), exposing their latency every head
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
         {
             const int rr = tid >> 4, d = tid & 15, ii = i0 + rr;
             float M = -INFINITY;
@@ -187,6 +226,229 @@ __global__ __launch_bounds__(256) void afau_row_attn_kernel(const float* __restr
                 const float sc = fpm::fast_exp2((ms.x - M) * fpm::LOG2E_F);
                 sum = fmaf(ms.y, sc, sum);
                 o = fmaf(S.part[buf][w][tid], sc, o);
+            }
+            if (stats && d == 0 && ii < n1max) stats[((long)b * n1max + ii) * 16 + h] = make_float2(M, sum);
+            if (ii < n1max) {
+                const float v = o / sum;
+                if constexpr (SPLIT) {
+                    T* orow = out + ((long)b * n1max + ii) * 768 + h * 16 + d;
+                    const bf16_t hi = fpm::f2bf(v);
+                    orow[0] = hi;
+                    orow[256] = fpm::f2bf(v - fpm::bf2f(hi));
+                    orow[512] = hi;
+                } else {
+                    out[((long)b * n1max + ii) * 256 + h * 16 + d] = fpm::from_f<T>(v);
+                }
+            }
+        }
+    }
+}
+
+// The same attention for n2max <= 256 with the 16-term scores (no LUT) and V staged in LDS.
+// afau_row_attn_kernel reads its B operand V[j][d] = Wv[h*16 + d][j] straight from global memory,
+// 16 B of each of 16 rows per load instruction (16 cache lines per wave instruction, every line
+// touched 8 times per head): an L2-request-bound gather that held the kernel at ~10 % VALU issue.
+// Here each head's 16 x 256 slice of Wv is copied once per workgroup with 16-B coalesced loads
+// (issued one head ahead, written to the other LDS buffer after the head's MFMAs), and a lane's
+// 16 B-operand values are 4 ds_read_b128 (rows padded to 260 floats: conflict-free).  Lane group
+// q = lane >> 4 of wave wv owns the 16 CONTIGUOUS columns j = wv*64 + q*16 + t (the other kernel
+// interleaves them with stride 4), so the costs are 16-B loads too; the P . V sum over j runs in
+// a different order (fp32 rounding only).
+template <typename T, bool SPLIT, bool FAST>
+__global__ __launch_bounds__(256) void afau_row_attn_v_kernel(const float* __restrict__ cost, long c_sb, long c_ld,
+                                                              int n1max, int n2max, const int* __restrict__ n2,
+                                                              const float* __restrict__ Wv, int emb,
+                                                              const float* __restrict__ mix1w,
+                                                              const float* __restrict__ mix1b,
+                                                              const float* __restrict__ mix2w,
+                                                              const float* __restrict__ mix2b, T* __restrict__ out,
+                                                              float2* __restrict__ stats) {
+    typedef float f32x4_t __attribute__((ext_vector_type(4)));
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    constexpr int TJ = 16, VS = 260;
+    __shared__ __attribute__((aligned(16))) float vbuf[2][16 * VS];
+    __shared__ float part[2][4][256];
+    __shared__ float2 rowms[2][4][16];
+    const int b = blockIdx.x, i0 = blockIdx.y * 16, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int n2b = n2[b];
+    const int r = lane & 15, i = i0 + r, jl = wv * 64 + (lane >> 4) * 16;
+
+    // V staging: thread copies row vr, columns [vc, vc + 16) of the head's slice (zero past n2b)
+    const int vr = tid >> 4, vc = (tid & 15) * 16;
+    float4 vnext[4];
+    auto load_v = [&](int h) {
+        const float* src = Wv + (long)(h * 16 + vr) * emb + vc;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float4 v = *(const float4*)(src + 4 * k);
+            const int j = vc + 4 * k;
+            if (j + 0 >= n2b) v.x = 0.f;
+            if (j + 1 >= n2b) v.y = 0.f;
+            if (j + 2 >= n2b) v.z = 0.f;
+            if (j + 3 >= n2b) v.w = 0.f;
+            vnext[k] = v;
+        }
+    };
+    auto store_v = [&](int buf) {
+        float* dst = &vbuf[buf][vr * VS + vc];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) *(float4*)(dst + 4 * k) = vnext[k];
+    };
+    load_v(0);
+    // costs: this lane's 16 contiguous columns of row i
+    float creg[TJ];
+    {
+        const float* Cb = cost + (long)b * c_sb + (long)i * c_ld + jl;
+        const bool vec = i < n1max && jl + TJ <= n2max && (((uintptr_t)Cb) & 15) == 0;
+        if (vec) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float4 c4 = *(const float4*)(Cb + 4 * k);
+                creg[4 * k] = c4.x; creg[4 * k + 1] = c4.y; creg[4 * k + 2] = c4.z; creg[4 * k + 3] = c4.w;
+            }
+        } else {
+#pragma unroll
+            for (int t = 0; t < TJ; ++t) creg[t] = (i < n1max && jl + t < n2max) ? Cb[t] : 0.f;
+        }
+    }
+    store_v(0);
+    // FAST (bf16 modes): the wave's cost range [cmin, cmax]; a hidden unit m whose pre-activation
+    // fma(c, w1, b1) has one sign at both ends (fma is monotone in c) is active or inactive for every
+    // cost of the wave, so its relu term is linear (summed into A + B c once per head) or zero; only
+    // units with a breakpoint inside the range are evaluated per element.  Exact up to fp32
+    // reassociation (the fp32 parity mode keeps the per-element 16-term chain).
+    float cmin = INFINITY, cmax = -INFINITY;
+    if (FAST) {
+#pragma unroll
+        for (int t = 0; t < TJ; ++t) {
+            cmin = fminf(cmin, creg[t]);
+            cmax = fmaxf(cmax, creg[t]);
+        }
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            cmin = fminf(cmin, __shfl_xor(cmin, o));
+            cmax = fmaxf(cmax, __shfl_xor(cmax, o));
+        }
+    }
+    __syncthreads();
+    for (int h = 0; h < 16; ++h) {
+        if (h + 1 < 16) load_v(h + 1);                    // lands during this head's scores
+        float p[TJ];
+        float mloc = -INFINITY;
+        if (FAST) {
+            const float* w1p = mix1w + (h * 2 + 1) * 16;
+            const float* b1p = mix1b + h * 16;
+            const float* w2p = mix2w + h * 16;
+            float A = mix2b[h], Bl = 0.f;
+            f2v acc2[TJ / 2];
+#pragma unroll
+            for (int t2 = 0; t2 < TJ / 2; ++t2) acc2[t2] = (f2v){0.f, 0.f};
+            // the head's 48 weights in one batch of scalar loads (a rolled loop paid one scalar-load
+            // latency per unit: ~800 dependent s_loads per wave)
+            float w1a[16], b1a[16], w2a[16];
+#pragma unroll
+            for (int m = 0; m < 16; ++m) {
+                w1a[m] = w1p[m];
+                b1a[m] = b1p[m];
+                w2a[m] = w2p[m];
+            }
+#pragma unroll
+            for (int m = 0; m < 16; ++m) {
+                const float w1 = w1a[m], b1 = b1a[m], w2 = w2a[m];
+                const float lo = fmaf(cmin, w1, b1), hi = fmaf(cmax, w1, b1);
+                if (lo > 0.f && hi > 0.f) {               // active for the whole range
+                    A = fmaf(w2, b1, A);
+                    Bl = fmaf(w2, w1, Bl);
+                } else if (lo > 0.f || hi > 0.f) {        // breakpoint inside: per element
+#pragma unroll
+                    for (int t2 = 0; t2 < TJ / 2; ++t2) {
+                        f2v u = (f2v){creg[2 * t2], creg[2 * t2 + 1]} * w1 + b1;
+                        u.x = fmaxf(u.x, 0.f);
+                        u.y = fmaxf(u.y, 0.f);
+                        acc2[t2] = u * w2 + acc2[t2];
+                    }
+                }
+            }
+#pragma unroll
+            for (int t2 = 0; t2 < TJ / 2; ++t2) {
+                p[2 * t2] = fmaf(Bl, creg[2 * t2], A) + acc2[t2].x;
+                p[2 * t2 + 1] = fmaf(Bl, creg[2 * t2 + 1], A) + acc2[t2].y;
+            }
+#pragma unroll
+            for (int t = 0; t < TJ; ++t)
+                if (jl + t < n2max) mloc = fmaxf(mloc, p[t]);
+        } else {
+            f2v acc2[TJ / 2];
+#pragma unroll
+            for (int t2 = 0; t2 < TJ / 2; ++t2) acc2[t2] = (f2v){0.f, 0.f};
+            const float* w1p = mix1w + (h * 2 + 1) * 16;
+            const float* b1p = mix1b + h * 16;
+            const float* w2p = mix2w + h * 16;
+#pragma unroll
+            for (int m = 0; m < 16; ++m) {
+                const float w1 = w1p[m], b1 = b1p[m], w2 = w2p[m];
+#pragma unroll
+                for (int t2 = 0; t2 < TJ / 2; ++t2) {
+                    f2v u = (f2v){creg[2 * t2], creg[2 * t2 + 1]} * w1 + b1;
+                    u.x = fmaxf(u.x, 0.f);
+                    u.y = fmaxf(u.y, 0.f);
+                    acc2[t2] = u * w2 + acc2[t2];
+                }
+            }
+            const float b2 = mix2b[h];
+#pragma unroll
+            for (int t2 = 0; t2 < TJ / 2; ++t2) {
+                p[2 * t2] = acc2[t2].x + b2;
+                p[2 * t2 + 1] = acc2[t2].y + b2;
+            }
+#pragma unroll
+            for (int t = 0; t < TJ; ++t)
+                if (jl + t < n2max) mloc = fmaxf(mloc, p[t]);
+        }
+        mloc = fmaxf(mloc, __shfl_xor(mloc, 16));
+        mloc = fmaxf(mloc, __shfl_xor(mloc, 32));
+        float sloc = 0.f;
+#pragma unroll
+        for (int t = 0; t < TJ; ++t) {
+            const float e = jl + t < n2max ? fpm::fast_exp2((p[t] - mloc) * fpm::LOG2E_F) : 0.f;
+            p[t] = e;
+            sloc += e;
+        }
+        sloc += __shfl_xor(sloc, 16);
+        sloc += __shfl_xor(sloc, 32);
+        const int buf = h & 1;
+        float vreg[TJ];
+        {
+            const float* vs = &vbuf[buf][r * VS + jl];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float4 v4 = *(const float4*)(vs + 4 * k);
+                vreg[4 * k] = v4.x; vreg[4 * k + 1] = v4.y; vreg[4 * k + 2] = v4.z; vreg[4 * k + 3] = v4.w;
+            }
+        }
+        f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < TJ; ++t) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(p[t], vreg[t], acc, 0, 0, 0);
+        if (h + 1 < 16) store_v(buf ^ 1);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) part[buf][wv][(4 * (lane >> 4) + k) * 16 + r] = acc[k];
+        if (lane < 16) rowms[buf][wv][lane] = make_float2(mloc, sloc);
+        // LDS-only barrier (no vmcnt(0): this head's output stores stay in flight)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        {
+            const int rr = tid >> 4, d = tid & 15, ii = i0 + rr;
+            float M = -INFINITY;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) M = fmaxf(M, rowms[buf][w][rr].x);
+            float o = 0.f, sum = 0.f;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const float2 ms = rowms[buf][w][rr];
+                const float sc = fpm::fast_exp2((ms.x - M) * fpm::LOG2E_F);
+                sum = fmaf(ms.y, sc, sum);
+                o = fmaf(part[buf][w][tid], sc, o);
             }
             if (stats && d == 0 && ii < n1max) stats[((long)b * n1max + ii) * 16 + h] = make_float2(M, sum);
             if (ii < n1max) {
@@ -316,6 +578,14 @@ __global__ __launch_bounds__(64) void afau_head_kernel(const float* __restrict__
 
 }  // namespace
 
+int& afau_attn_v_flag() {
+    static int v = [] {
+        const char* e = getenv("FPM_AFAU_ATTN_V");
+        return e ? atoi(e) : 1;
+    }();
+    return v;
+}
+
 int& afau_lut_flag() {
     static int v = [] {
         const char* e = getenv("FPM_AFAU_LUT");
@@ -334,10 +604,23 @@ extern "C" int fpm_crossset_attn_fwd(int dtype, const float* cost, long c_sb, lo
     FPM_CHECK_ARG(n2max <= 640, "crossset_attn: n2max %d > 640", n2max);
     // fp32 (parity) mode scores with the 16-term sum (the reference's operation order); the LUT is
     // the bf16 throughput mode's (env FPM_AFAU_LUT / fpm_set_tuning("afau_lut") override)
-    const int lut = afau_lut_flag() != 2 ? afau_lut_flag() : (dtype != 0);
+    const bool v_ok = n2max <= 256 && emb >= 256 && emb % 4 == 0 && ((uintptr_t)Wv & 15) == 0 && afau_attn_v_flag() != 0;
+    const int lut = afau_lut_flag() != 2 ? afau_lut_flag() : (dtype != 0 && !v_ok);
 #define FPM_ATT(TT, TJ_, SP_)                                                                                    \
     hipLaunchKernelGGL((afau_row_attn_kernel<TT, TJ_, SP_>), grid, dim3(256), 0, st, cost, c_sb, c_ld, n1max, n2max, \
                        n2, Wv, emb, mix1w, mix1b, mix2w, mix2b, (TT*)out, lut, (float2*)stats)
+    // the LDS-staged-V kernel (16-term scores) where it applies; env FPM_AFAU_ATTN_V=0 keeps the other
+    const bool vpath = !lut && v_ok;
+#define FPM_ATTV(TT, SP_)                                                                                        \
+    hipLaunchKernelGGL((afau_row_attn_v_kernel<TT, SP_, !std::is_same<TT, float>::value>), grid, dim3(256), 0, st, cost, c_sb, c_ld, n1max, n2max,  \
+                       n2, Wv, emb, mix1w, mix1b, mix2w, mix2b, (TT*)out, (float2*)stats)
+    if (vpath) {
+        if (dtype == 0) FPM_ATTV(float, false);
+        else if (dtype == 1) FPM_ATTV(bf16_t, false);
+        else FPM_ATTV(bf16_t, true);
+        return fpm::check_launch("fpm_crossset_attn_fwd");
+    }
+#undef FPM_ATTV
     if (dtype == 0) { if (n2max <= 256) FPM_ATT(float, 16, false); else FPM_ATT(float, 40, false); }
     else if (dtype == 1) { if (n2max <= 256) FPM_ATT(bf16_t, 16, false); else FPM_ATT(bf16_t, 40, false); }
     else { if (n2max <= 256) FPM_ATT(bf16_t, 16, true); else FPM_ATT(bf16_t, 40, true); }

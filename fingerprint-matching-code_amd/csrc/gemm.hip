@@ -118,6 +118,7 @@ int& combine_npb_flag();
 int& combine_pf_flag();
 int& sinkhorn_bwd_reg_flag();
 int& afau_lut_flag();
+int& afau_attn_v_flag();
 int& sinkhorn_fast_flag();
 int& soft_topk_fast_flag();
 
@@ -137,6 +138,7 @@ extern "C" int fpm_set_tuning(const char* key, int value) {
     else if (key && !strcmp(key, "combine_pf")) f = &combine_pf_flag();
     else if (key && !strcmp(key, "sinkhorn_bwd_reg")) f = &sinkhorn_bwd_reg_flag();
     else if (key && !strcmp(key, "afau_lut")) f = &afau_lut_flag();
+    else if (key && !strcmp(key, "afau_attn_v")) f = &afau_attn_v_flag();
     else if (key && !strcmp(key, "sinkhorn_fast")) f = &sinkhorn_fast_flag();
     else if (key && !strcmp(key, "topk_fast")) f = &soft_topk_fast_flag();
     if (!f) {

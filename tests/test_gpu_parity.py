@@ -800,3 +800,36 @@ def test_gemm_persist_bit_identical(sd, npairs, n):
     for r in outs[1:]:
         for k in ("s", "ss", "ds_mat", "k_prob", "perm_mat"):
             assert torch.equal(r[k], outs[0][k]), k
+
+
+@pytest.mark.parametrize("B,n1,n2max,n2s", [(3, 64, 64, [64, 50, 61]), (2, 200, 256, [256, 233]), (2, 37, 45, [45, 20])])
+def test_crossset_attn_lds_v_kernel(sd, B, n1, n2max, n2s):
+    """The LDS-staged-V attention kernel (n2max <= 256) against the global-V kernel with the same
+    16-term scores: fp32 outputs and softmax stats within fp32 summation-order rounding; the bf16
+    mode's interval-classified scores (exact up to reassociation) against the fp32 kernel."""
+    net = fpm.Net(regression=True, dtype="bf16", backbone=False)
+    net.load_state_dict(sd)
+    wp = net.packed(DEV)
+    g = torch.Generator().manual_seed(n1 + n2max)
+    ss = (torch.rand(B, n1, n2max, generator=g) ** 4).to(DEV)
+    n2 = _i32(n2s)
+    args = [wp[k] for k in ("row_Wv", "row_mix1w", "row_mix1b", "row_mix2w", "row_mix2b")]
+    res = {}
+    for v in (0, 1):
+        pv, pl = ops.set_tuning("afau_attn_v", v), ops.set_tuning("afau_lut", 0)
+        try:
+            o32 = torch.empty(B * n1, 256, device=DEV)
+            st = torch.empty(B * n1, 16, 2, device=DEV)
+            ops.crossset_attn(ss, n2, *args, o32, stats=st)
+            o3 = torch.empty(B * n1, 768, device=DEV, dtype=torch.bfloat16)
+            ops.crossset_attn(ss, n2, *args, o3, split=True)
+            torch.cuda.synchronize()
+        finally:
+            ops.set_tuning("afau_attn_v", pv)
+            ops.set_tuning("afau_lut", pl)
+        res[v] = (o32, st, o3[:, :256].float() + o3[:, 256:512].float())
+    (a0, s0, _), (a1, s1, h1) = res[0], res[1]
+    scale = a0.abs().max()
+    assert (a1 - a0).abs().max() <= 1e-5 * scale
+    assert torch.allclose(s1, s0, rtol=1e-5, atol=1e-6)
+    assert (h1 - a0).abs().max() <= 2e-5 * scale
