@@ -267,13 +267,67 @@ class Net(nn.Module):
         ops.rows_bcast_scale(y, bt.B, coef=cscale, out_f=outf, out_t=out)
         return out, outf
 
-    def _afau(self, wp, ss, bt):
-        """AFA-U k regression (ngm.py:386-412) -> ks (B,)."""
+    def _afau_block(self, wp, blk, nb_, P_, mh=None, n2u_d=None):
+        """One AFA-U encoder block's instance norms + FFN (afau.py:145-199) -> max over positions
+        (nb_, E).  "row": on the attention-combine output mh; "col": the synthesised one-hot input
+        C0 + combine bias of each distinct n2 (n2u_d)."""
+        dev = wp["row_Wc"].device
+        op = torch.bfloat16 if self.afau_mode in ("bf16", "bf16s") else torch.float32
+        E, FF = C.AFAU_EMB, C.AFAU_FF
+        x3 = self.afau_mode == "bf16x3"
+        mask = int(os.environ.get("FPM_AFAU_X3_MASK", "7"))
+        kx = lambda bit, kp: 3 * kp if mask & bit else kp
+        rows = nb_ * P_
+        o1f = torch.empty(rows, E, device=dev, dtype=torch.float32)
+        KE = E if op == torch.float32 else C.AFAU_EMB_PAD      # bf16 operand copy: zero-padded K
+        o1t = o1f if op == torch.float32 else torch.empty(rows, KE, device=dev, dtype=op)
+        if blk == "row":
+            ops.instnorm(mh, nb_, P_, E, wp["row_n1w"], wp["row_n1b"], out_f=o1f,
+                         out_t=None if op == torch.float32 else o1t, ldt=KE)
+        else:
+            ops.instnorm(None, nb_, P_, E, wp["col_n1w"], wp["col_n1b"], nvalid=n2u_d, onehot_bias=wp["col_bc"],
+                         out_f=o1f, out_t=None if op == torch.float32 else o1t, ldt=KE)
+        ff = torch.empty(rows, E, device=dev, dtype=torch.float32)
+        if x3:
+            o13 = ops.split_bf16x3(o1f, C.AFAU_EMB_PAD)
+            hf = torch.empty(rows, FF, device=dev, dtype=torch.float32)
+            ops.gemm(o13, wp[blk + "_W1"], rows, FF, kx(2, C.AFAU_EMB_PAD), o13.shape[1], o13.shape[1],
+                     epi=ops.EPI_RELU, bias=wp[blk + "_b1"], out_f=hf, ldc=FF)
+            h3 = ops.split_bf16x3(hf, FF)
+            ops.gemm(h3, wp[blk + "_W2"], rows, E, kx(4, FF), h3.shape[1], h3.shape[1], bias=wp[blk + "_b2"],
+                     out_f=ff, ldc=E)
+        else:
+            hbuf = torch.empty(rows, FF, device=dev, dtype=op)
+            ops.gemm(o1t, wp[blk + "_W1"], rows, FF, KE, KE, KE, epi=ops.EPI_RELU, bias=wp[blk + "_b1"],
+                     out_t=hbuf if op != torch.float32 else None, out_f=hbuf if op == torch.float32 else None,
+                     ldc=FF)
+            ops.gemm(hbuf, wp[blk + "_W2"], rows, E, FF, FF, FF, bias=wp[blk + "_b2"], out_f=ff, ldc=E)
+        gm = torch.empty(nb_, E, device=dev, dtype=torch.float32)
+        ops.instnorm(o1f, nb_, P_, E, wp[blk + "_n2w"], wp[blk + "_n2b"], in2=ff, gmax=gm)
+        return gm
+
+    def _afau_col(self, wp, bt):
+        """The AFA-U column block for every distinct n2 of a batch: (n2u, gmax per n2u, n2max).
+        The column block sees a = one-hot rows and b = zero rows, so k = v = 0 and its attention
+        output is exactly the combine bias (afau.py:99-142): its result depends on n2 and the batch's
+        n2max only, not on ss.  A forward computes it once per distinct n2 and gathers it for every
+        pair and pipeline chunk -- the same arithmetic on the same inputs, bit-identical to the
+        per-pair evaluation."""
+        if os.environ.get("FPM_AFAU_COLDEDUP", "1") == "1":
+            n2u = np.unique(bt.n_host[1].numpy())
+        else:
+            n2u = bt.n_host[1].numpy()
+        n2u_d = torch.as_tensor(n2u, dtype=torch.int32).to(bt.device, non_blocking=True)
+        return n2u, self._afau_block(wp, "col", len(n2u), bt.n2max, n2u_d=n2u_d), bt.n2max
+
+    def _afau(self, wp, ss, bt, col=None):
+        """AFA-U k regression (ngm.py:386-412) -> ks (B,).  ``col``: the forward's _afau_col result
+        (computed here for this batch when None)."""
         dev = ss.device
         B, n1max, n2max = bt.B, bt.n1max, bt.n2max
         # f32 / bf16x3: fp32 activations; bf16 / bf16s: bf16 FFN operands
         op = torch.bfloat16 if self.afau_mode in ("bf16", "bf16s") else torch.float32
-        E, HD, FF = C.AFAU_EMB, C.AFAU_HEADS * C.AFAU_QKV, C.AFAU_FF
+        E, HD = C.AFAU_EMB, C.AFAU_HEADS * C.AFAU_QKV
         if max(n1max, n2max) > self.univ_size:
             raise AssertionError("UNIV_SIZE cap: n1max/n2max must be <= %d (ngm.py:387-389)" % self.univ_size)
         x3 = self.afau_mode == "bf16x3"          # near-fp32 products on bf16 MFMA (split operands)
@@ -292,52 +346,16 @@ class Net(nn.Module):
         # bf16s: hi*W_hi + lo*W_hi (2 terms; the W_lo term changed nothing measurable, +0.7 % time)
         kc = int(os.environ.get("FPM_AFAU_SPLIT_TERMS", "2")) * HD if split else (kx(1, HD) if x3 else HD)
         ops.gemm(att, wp["row_Wc"], B * n1max, E, kc, att.shape[1], att.shape[1], bias=wp["row_bc"], out_f=mh, ldc=E)
-        gmax = {}
-        # The column block sees a = one-hot rows and b = zero rows, so k = v = 0 and its attention
-        # output is exactly the combine bias (afau.py:99-142): its result depends on n2 (and the
-        # batch's n2max) only, not on ss.  It is computed once per distinct n2 of the batch and
-        # gathered -- the same arithmetic on the same inputs, so bit-identical to the per-pair run.
-        if os.environ.get("FPM_AFAU_COLDEDUP", "1") == "1":
-            n2u, inv = np.unique(bt.n_host[1].numpy(), return_inverse=True)
-        else:
-            n2u, inv = bt.n_host[1].numpy(), np.arange(B)
-        Bu = len(n2u)
-        n2u_d = torch.as_tensor(n2u, dtype=torch.int32).to(dev, non_blocking=True)
-        for blk, rows, P_ in (("row", B * n1max, n1max), ("col", Bu * n2max, n2max)):
-            o1f = torch.empty(rows, E, device=dev, dtype=torch.float32)
-            KE = E if op == torch.float32 else C.AFAU_EMB_PAD      # bf16 operand copy: zero-padded K
-            o1t = o1f if op == torch.float32 else torch.empty(rows, KE, device=dev, dtype=op)
-            nb_ = B if blk == "row" else Bu
-            if blk == "row":
-                ops.instnorm(mh, B, P_, E, wp["row_n1w"], wp["row_n1b"], out_f=o1f,
-                             out_t=None if op == torch.float32 else o1t, ldt=KE)
-            else:
-                ops.instnorm(None, Bu, P_, E, wp["col_n1w"], wp["col_n1b"], nvalid=n2u_d, onehot_bias=wp["col_bc"],
-                             out_f=o1f, out_t=None if op == torch.float32 else o1t, ldt=KE)
-            ff = torch.empty(rows, E, device=dev, dtype=torch.float32)
-            if x3:
-                o13 = ops.split_bf16x3(o1f, C.AFAU_EMB_PAD)
-                hf = torch.empty(rows, FF, device=dev, dtype=torch.float32)
-                ops.gemm(o13, wp[blk + "_W1"], rows, FF, kx(2, C.AFAU_EMB_PAD), o13.shape[1], o13.shape[1],
-                         epi=ops.EPI_RELU, bias=wp[blk + "_b1"], out_f=hf, ldc=FF)
-                h3 = ops.split_bf16x3(hf, FF)
-                ops.gemm(h3, wp[blk + "_W2"], rows, E, kx(4, FF), h3.shape[1], h3.shape[1], bias=wp[blk + "_b2"],
-                         out_f=ff, ldc=E)
-            else:
-                hbuf = torch.empty(rows, FF, device=dev, dtype=op)
-                ops.gemm(o1t, wp[blk + "_W1"], rows, FF, KE, KE, KE, epi=ops.EPI_RELU, bias=wp[blk + "_b1"],
-                         out_t=hbuf if op != torch.float32 else None, out_f=hbuf if op == torch.float32 else None,
-                         ldc=FF)
-                ops.gemm(hbuf, wp[blk + "_W2"], rows, E, FF, FF, FF, bias=wp[blk + "_b2"], out_f=ff, ldc=E)
-            gm = torch.empty(nb_, E, device=dev, dtype=torch.float32)
-            ops.instnorm(o1f, nb_, P_, E, wp[blk + "_n2w"], wp[blk + "_n2b"], in2=ff, gmax=gm)
-            if blk == "col" and Bu != B:
-                gm = gm.index_select(0, torch.as_tensor(inv, dtype=torch.long).to(dev, non_blocking=True))
-            elif blk == "col" and Bu == B and not np.array_equal(inv, np.arange(B)):
-                gm = gm.index_select(0, torch.as_tensor(inv, dtype=torch.long).to(dev, non_blocking=True))
-            gmax[blk] = gm
+        g_row = self._afau_block(wp, "row", B, n1max, mh=mh)
+        if col is None or col[2] != n2max:
+            col = self._afau_col(wp, bt)
+        n2u, gm_u, _ = col
+        n2c = bt.n_host[1].numpy()
+        inv = np.searchsorted(n2u, n2c) if len(n2u) != len(n2c) or not np.array_equal(n2u, n2c) else None
+        g_col = gm_u if inv is None else gm_u.index_select(0, torch.as_tensor(inv, dtype=torch.long).to(
+            dev, non_blocking=True))
         ks = torch.empty(B, device=dev, dtype=torch.float32)
-        ops.afau_head(gmax["row"], gmax["col"], B, E, wp["final_row0w"], wp["final_row0b"], wp["final_row2w"],
+        ops.afau_head(g_row, g_col, B, E, wp["final_row0w"], wp["final_row0b"], wp["final_row2w"],
                       wp["final_row2b"], wp["final_col0w"], wp["final_col0b"], wp["final_col2w"], wp["final_col2b"], ks)
         return ks
 
@@ -457,14 +475,14 @@ class Net(nn.Module):
             return max(1, min(int(os.environ["FPM_CHUNKS"]), B))
         return max(1, min(8, B // 128))
 
-    def _stage_a(self, part, b0, b1, o, keep_feats, gt_ks, min_pt, st, gc):
+    def _stage_a(self, part, b0, b1, o, keep_feats, gt_ks, min_pt, st, gc, col=None):
         """GPU stage of one chunk (on its stream): everything up to ds_mat, then its D2H copy."""
         dev = part.device
         r = self.run_gpu_stage(part, keep_feats, s_out=o["s"][b0:b1], ss_out=o["ss"][b0:b1],
                                gc=(gc[0][b0:b1], gc[1][b0:b1]))
         ks = o["k_prob"][b0:b1]
         if self.regression:
-            ks.copy_(self._afau(self.packed(dev), o["ss"][b0:b1], part))
+            ks.copy_(self._afau(self.packed(dev), o["ss"][b0:b1], part, col=col))
         else:
             ks.copy_(gt_ks[b0:b1] / min_pt[b0:b1])
         self._mark("afau")
@@ -576,6 +594,10 @@ class Net(nn.Module):
         ev_start = torch.cuda.Event(enable_timing=True)
         ev_start.record(main)
         gc = self.global_coef(bt)
+        # the AFA-U column block once for the whole batch (per distinct n2), before the chunks
+        col = (self._afau_col(self.packed(dev), bt)
+               if self.regression and os.environ.get("FPM_AFAU_COLDEDUP", "1") == "1"
+               and os.environ.get("FPM_AFAU_COLFWD", "1") == "1" else None)
         ev_coef = torch.cuda.Event()
         ev_coef.record(main)
         streams = self._streams(dev) if (len(parts) > 1 and self.n_streams > 1) else [main]
@@ -587,7 +609,7 @@ class Net(nn.Module):
             st = streams[c % len(streams)]
             b0, b1 = (0, B) if part is bt else part.pair_range     # a chunk's range inside bt
             with torch.cuda.stream(st):
-                r, ev = self._stage_a(part, b0, b1, o, keep_feats, gt_ks, min_pt, st, gc)
+                r, ev = self._stage_a(part, b0, b1, o, keep_feats, gt_ks, min_pt, st, gc, col=col)
             outs.append(r)
             events.append(ev)
         t_enq = time.perf_counter()
