@@ -576,6 +576,42 @@ __global__ __launch_bounds__(64) void afau_head_kernel(const float* __restrict__
     if (lane == 0) ks[b] = 1.f / (1.f + expf(-((kr + kc) / 2.f)));
 }
 
+// The same with the 8 hidden units on 8 waves (the one-wave form ran the 16 dot products of length
+// E back to back: ~60 us per launch, latency-bound on 1 wave per pair).  Each unit's dot product and
+// lane-0 sum are those of afau_head_kernel; the units are then combined in the same order:
+// bit-identical.
+__global__ __launch_bounds__(512) void afau_head8_kernel(const float* __restrict__ gr, const float* __restrict__ gc,
+                                                         int E, const float* __restrict__ r0w, const float* __restrict__ r0b,
+                                                         const float* __restrict__ r2w, const float* __restrict__ r2b,
+                                                         const float* __restrict__ c0w, const float* __restrict__ c0b,
+                                                         const float* __restrict__ c2w, const float* __restrict__ c2b,
+                                                         float* __restrict__ ks) {
+    __shared__ float hid[2][8];
+    const int b = blockIdx.x, lane = threadIdx.x & 63, m = threadIdx.x >> 6;
+    float sr = 0.f, sc = 0.f;
+    for (int k = lane; k < E; k += 64) {
+        sr += r0w[m * E + k] * gr[(long)b * E + k];
+        sc += c0w[m * E + k] * gc[(long)b * E + k];
+    }
+    sr = fpm::warp_sum(sr) + r0b[m];
+    sc = fpm::warp_sum(sc) + c0b[m];
+    if (lane == 0) {
+        hid[0][m] = sr;
+        hid[1][m] = sc;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float kr = 0.f, kc = 0.f;
+        for (int u = 0; u < 8; ++u) {
+            kr += r2w[u] * fmaxf(hid[0][u], 0.f);
+            kc += c2w[u] * fmaxf(hid[1][u], 0.f);
+        }
+        kr += r2b[0];
+        kc += c2b[0];
+        ks[b] = 1.f / (1.f + expf(-((kr + kc) / 2.f)));
+    }
+}
+
 }  // namespace
 
 int& afau_attn_v_flag() {
@@ -651,7 +687,11 @@ extern "C" int fpm_afau_head(const float* gr, const float* gc, int B, int E, con
                              const float* r2w, const float* r2b, const float* c0w, const float* c0b, const float* c2w,
                              const float* c2b, float* ks, void* stream) {
     if (B == 0) return 0;
-    hipLaunchKernelGGL(afau_head_kernel, dim3(B), dim3(64), 0, (hipStream_t)stream, gr, gc, E, r0w, r0b, r2w, r2b, c0w,
-                       c0b, c2w, c2b, ks);
+    if (getenv("FPM_AFAU_HEAD1") == nullptr)
+        hipLaunchKernelGGL(afau_head8_kernel, dim3(B), dim3(512), 0, (hipStream_t)stream, gr, gc, E, r0w, r0b, r2w, r2b,
+                           c0w, c0b, c2w, c2b, ks);
+    else
+        hipLaunchKernelGGL(afau_head_kernel, dim3(B), dim3(64), 0, (hipStream_t)stream, gr, gc, E, r0w, r0b, r2w, r2b,
+                           c0w, c0b, c2w, c2b, ks);
     return fpm::check_launch("fpm_afau_head");
 }

@@ -113,6 +113,7 @@ int& gnn_group_flag();
 int& gnn_group1_flag();
 int& gnn_wide_flag();
 int& gnn_il_flag();
+int& nodecls_t_flag();
 int& plan_graph_flag();
 int& combine_npb_flag();
 int& combine_pf_flag();
@@ -133,6 +134,7 @@ extern "C" int fpm_set_tuning(const char* key, int value) {
     else if (key && !strcmp(key, "gnn_group1")) f = &gnn_group1_flag();
     else if (key && !strcmp(key, "gnn_wide")) f = &gnn_wide_flag();
     else if (key && !strcmp(key, "gnn_il")) f = &gnn_il_flag();
+    else if (key && !strcmp(key, "nodecls_t")) f = &nodecls_t_flag();
     else if (key && !strcmp(key, "plan_graph")) f = &plan_graph_flag();
     else if (key && !strcmp(key, "combine_npb")) f = &combine_npb_flag();
     else if (key && !strcmp(key, "combine_pf")) f = &combine_pf_flag();

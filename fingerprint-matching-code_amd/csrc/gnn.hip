@@ -373,7 +373,56 @@ __global__ __launch_bounds__(256) void node_classifier_kernel(const float* __res
     }
 }
 
+// The same on 64 x 64 (d, i) tiles transposed through LDS: reads along i and writes s along d are
+// both coalesced (the per-(pair, d) form wrote each value to its own cache line, 4 B per lane at
+// a 4 n2max-byte stride).  Same arithmetic per element, bit-identical.
+__global__ __launch_bounds__(256) void node_classifier_t_kernel(const float* __restrict__ X, int n1max, int n2max,
+                                                                const float* __restrict__ w,
+                                                                const float* __restrict__ bias,
+                                                                const float* __restrict__ vpart,
+                                                                float* __restrict__ s) {
+    __shared__ float tile[64][65];                        // [i - i0][d - d0]
+    const int b = blockIdx.z, d0 = blockIdx.y * 64, i0 = blockIdx.x * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const long N = (long)n1max * n2max;
+    const float* Xb = X + (long)b * 17 * N;
+    const int i = i0 + tx;
+#pragma unroll 4
+    for (int r = 0; r < 16; ++r) {
+        const int d = d0 + ty + 4 * r;
+        if (d < n2max && i < n1max) {
+            const long p = (long)d * n1max + i;
+            float acc;
+            if (vpart) {
+                acc = fmaf(w[16], Xb[16L * N + p], vpart[(long)b * N + p]);
+            } else {
+                acc = 0.f;
+#pragma unroll
+                for (int c = 0; c < 17; ++c) acc += w[c] * Xb[(long)c * N + p];
+            }
+            tile[tx][ty + 4 * r] = acc + bias[0];
+        }
+    }
+    __syncthreads();
+    const int d = d0 + tx;
+#pragma unroll 4
+    for (int r = 0; r < 16; ++r) {
+        const int ii = i0 + ty + 4 * r;
+        if (ii < n1max && d < n2max) s[(long)b * N + (long)ii * n2max + d] = tile[ty + 4 * r][tx];
+    }
+}
+
 }  // namespace
+
+// node classifier through the LDS transpose (1, default) or the per-(pair, d) form (0);
+// env FPM_NODECLS_T or fpm_set_tuning("nodecls_t", v)
+int& nodecls_t_flag() {
+    static int on = [] {
+        const char* e = getenv("FPM_NODECLS_T");
+        return e ? atoi(e) : 1;
+    }();
+    return on;
+}
 
 // MLP on packed fp32 FMAs (default) or scalar FMAs (bit-identical); env FPM_GNN_PACKED or
 // fpm_set_tuning("gnn_packed", v)
@@ -494,6 +543,12 @@ extern "C" int fpm_gnn_param_count(int C) { return C == 1 ? GnnPack<1>::total : 
 extern "C" int fpm_node_classifier(const float* X, int B, int n1max, int n2max, const float* w, const float* bias,
                                    const float* vpart, float* s, void* stream) {
     if (B == 0) return 0;
+    if (nodecls_t_flag() && B <= 65535) {
+        const dim3 grid((unsigned)((n1max + 63) / 64), (unsigned)((n2max + 63) / 64), (unsigned)B);
+        hipLaunchKernelGGL(node_classifier_t_kernel, grid, dim3(256), 0, (hipStream_t)stream, X, n1max, n2max, w, bias,
+                           vpart, s);
+        return fpm::check_launch("fpm_node_classifier");
+    }
     hipLaunchKernelGGL(node_classifier_kernel, dim3(pair_grid(n2max, B)), dim3(256), 0, (hipStream_t)stream, X, n1max,
                        n2max, w, bias, vpart, s, B);
     return fpm::check_launch("fpm_node_classifier");

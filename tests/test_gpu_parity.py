@@ -646,7 +646,7 @@ def test_gnn_kernel_variants_bit_identical(sd):
     bt = DeviceBatch.from_pairs(pairs, DEV)
     outs = []
     for key, val in (("gnn_group", 1), ("gnn_group", 2), ("gnn_unroll", 3), ("combine_npb", 16), ("gnn_wide", 1), ("gnn_il", 1),
-                     ("plan_graph", 0), ("combine_pf", 0), ("combine_pf", 1), ("gemm_persist", 1)):
+                     ("plan_graph", 0), ("combine_pf", 0), ("combine_pf", 1), ("gemm_persist", 1), ("nodecls_t", 0)):
         prev = ops.set_tuning(key, val)
         try:
             r = net.run(bt, chunks=1)
@@ -833,3 +833,24 @@ def test_crossset_attn_lds_v_kernel(sd, B, n1, n2max, n2s):
     assert (a1 - a0).abs().max() <= 1e-5 * scale
     assert torch.allclose(s1, s0, rtol=1e-5, atol=1e-6)
     assert (h1 - a0).abs().max() <= 2e-5 * scale
+
+
+def test_afau_head_and_nodecls_variants_bit_identical(sd):
+    """The 8-wave AFA-U head (FPM_AFAU_HEAD1 selects the one-wave form) and the LDS-transposed node
+    classifier (nodecls_t) reproduce the other forms bit for bit (k_prob, s)."""
+    pairs = synth.make_batch(23, 5, 100, n2=[100, 90, 77, 100, 64])
+    net = fpm.Net(regression=True, backbone=False, dtype="bf16")
+    net.load_state_dict(sd)
+    bt = DeviceBatch.from_pairs(pairs, DEV)
+    r8 = net.run(bt, chunks=1)
+    torch.cuda.synchronize()
+    os.environ["FPM_AFAU_HEAD1"] = "1"
+    prev = ops.set_tuning("nodecls_t", 0)
+    try:
+        r1 = net.run(bt, chunks=1)
+        torch.cuda.synchronize()
+    finally:
+        del os.environ["FPM_AFAU_HEAD1"]
+        ops.set_tuning("nodecls_t", prev)
+    for k in ("k_prob", "s", "ss", "ds_mat", "perm_mat"):
+        assert torch.equal(r8[k], r1[k]), k
