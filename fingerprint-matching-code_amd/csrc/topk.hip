@@ -475,6 +475,16 @@ extern "C" int fpm_soft_topk_fwd(const float* ss, long s_sb, long s_ld, const in
     return fpm::check_launch("fpm_soft_topk_fwd");
 }
 
+namespace {
+__global__ __launch_bounds__(256) void zero2_kernel(float4* __restrict__ a, float4* __restrict__ b, long n4) {
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (long k = (long)blockIdx.x * 256 + threadIdx.x; k < n4; k += (long)gridDim.x * 256) {
+        a[k] = z;
+        if (b) b[k] = z;
+    }
+}
+}  // namespace
+
 extern "C" int fpm_topk_select(const float* ds, long d_sb, long d_ld, const int* assign, long a_sb,
                                const float* k, int B, int n1max, int n2max, float* perm, long p_sb, long p_ld,
                                float* lsa_out, long l_sb, long l_ld, void* stream) {
@@ -487,8 +497,16 @@ extern "C" int fpm_topk_select(const float* ds, long d_sb, long d_ld, const int*
     const bool dense = p_ld == n2max && p_sb == box && (!lsa_out || (l_ld == n2max && l_sb == box));
     hipStream_t st = (hipStream_t)stream;
     if (dense) {
-        (void)hipMemsetAsync(perm, 0, (size_t)B * box * sizeof(float), st);
-        if (lsa_out) (void)hipMemsetAsync(lsa_out, 0, (size_t)B * box * sizeof(float), st);
+        // one wide 16-B-store fill of both outputs (the runtime's fill ran at ~0.9 TB/s, twice)
+        const long n4 = (long)B * box / 4;
+        const bool v4 = ((long)B * box) % 4 == 0 && ((uintptr_t)perm & 15) == 0 && (!lsa_out || ((uintptr_t)lsa_out & 15) == 0);
+        if (v4) {
+            const long blocks = (n4 + 255) / 256 < 8192 ? (n4 + 255) / 256 : 8192;
+            hipLaunchKernelGGL(zero2_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (float4*)perm, (float4*)lsa_out, n4);
+        } else {
+            (void)hipMemsetAsync(perm, 0, (size_t)B * box * sizeof(float), st);
+            if (lsa_out) (void)hipMemsetAsync(lsa_out, 0, (size_t)B * box * sizeof(float), st);
+        }
     }
     hipLaunchKernelGGL(topk_select_kernel, dim3(B), dim3(256), 0, st, ds, d_sb, d_ld, assign, a_sb, k, n1max, n2max,
                        perm, p_sb, p_ld, lsa_out, l_sb, l_ld, dense ? 1 : 0);
