@@ -126,6 +126,11 @@ class Net(nn.Module):
         # > 0: ds_mat D2H through hipMemcpyAsync with this copy kind (fpm_memcpy_async; 1024 = the
         # no-compute-unit device-to-device kind, i.e. a copy engine instead of the blit kernel)
         self.copy_kind = int(os.environ.get("FPM_COPY_KIND", "0"))
+        # defer each chunk's ds_mat D2H until the side-0 spline plan of the chunk queued two places
+        # later (same compute stream) has run: that latency-bound kernel otherwise runs beside the
+        # copy's blit kernel and stalls ~25x
+        self.copy_defer = int(os.environ.get("FPM_COPY_DEFER", "1"))
+        self._plan_events = None
         # the host thread waits for each chunk's ds_mat with a sleeping (not spinning) event wait,
         # leaving its core to the Hungarian pool
         self.blocking_wait = os.environ.get("FPM_BLOCKING_WAIT", "1") == "1"
@@ -232,6 +237,10 @@ class Net(nn.Module):
         E = bt.E[side]
         plan = ops.spline_plan(bt.src[side], bt.dst[side], bt.pseudo[side], nn_, bt.nmax[side],
                                bt.max_graph_edges(side))
+        if side == 0 and self._plan_events is not None:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(dev))
+            self._plan_events.append(ev)
         if side == 0 and bt.shared0 and bt.B > 1:
             return (plan,) + self._spline_shared(wp, bt, cscale)
         x0 = bt.x[side]
@@ -475,7 +484,25 @@ class Net(nn.Module):
             return max(1, min(int(os.environ["FPM_CHUNKS"]), B))
         return max(1, min(8, B // 128))
 
-    def _stage_a(self, part, b0, b1, o, keep_feats, gt_ks, min_pt, st, gc, col=None):
+    def _enqueue_copy(self, dev, b0, b1, o, done, after=None):
+        """ds_mat[b0:b1] -> pinned host memory on the copy stream once ``done`` (and ``after``, if
+        given) have fired; returns the copy's completion event."""
+        cs = self._copy_stream(dev)
+        cs.wait_event(done)
+        if after is not None:
+            cs.wait_event(after)
+        with torch.cuda.stream(cs):
+            if self.copy_kind > 0:
+                ops.memcpy_async(self._pinned[b0:b1], o["ds_mat"][b0:b1], self.copy_kind)
+            elif self.copy_blocks > 0:
+                ops.copy_async(self._pinned[b0:b1], o["ds_mat"][b0:b1], self.copy_blocks)
+            else:
+                self._pinned[b0:b1].copy_(o["ds_mat"][b0:b1], non_blocking=True)
+        ev = torch.cuda.Event(enable_timing=True, blocking=self.blocking_wait)
+        ev.record(cs)
+        return ev
+
+    def _stage_a(self, part, b0, b1, o, keep_feats, gt_ks, min_pt, st, gc, col=None, defer=None):
         """GPU stage of one chunk (on its stream): everything up to ds_mat, then its D2H copy."""
         dev = part.device
         r = self.run_gpu_stage(part, keep_feats, s_out=o["s"][b0:b1], ss_out=o["ss"][b0:b1],
@@ -508,18 +535,10 @@ class Net(nn.Module):
             # chunk queued on this compute stream
             done = torch.cuda.Event()
             done.record(st)
-            cs = self._copy_stream(dev)
-            cs.wait_event(done)
-            with torch.cuda.stream(cs):
-                if self.copy_kind > 0:
-                    ops.memcpy_async(self._pinned[b0:b1], o["ds_mat"][b0:b1], self.copy_kind)
-                elif self.copy_blocks > 0:
-                    ops.copy_async(self._pinned[b0:b1], o["ds_mat"][b0:b1], self.copy_blocks)
-                else:
-                    self._pinned[b0:b1].copy_(o["ds_mat"][b0:b1], non_blocking=True)
-            ev = torch.cuda.Event(enable_timing=True, blocking=self.blocking_wait)
-            ev.record(cs)
-            return r, ev
+            if defer is not None:
+                defer.append((b0, b1, done))
+                return r, None
+            return r, self._enqueue_copy(dev, b0, b1, o, done)
         if not self.zero_copy:
             self._pinned[b0:b1].copy_(o["ds_mat"][b0:b1], non_blocking=True)
         ev = torch.cuda.Event(enable_timing=True, blocking=self.blocking_wait)
@@ -605,13 +624,28 @@ class Net(nn.Module):
             if st is not main:
                 st.wait_event(ev_coef)
         outs, events = [], []
-        for c, part in enumerate(parts):
-            st = streams[c % len(streams)]
-            b0, b1 = (0, B) if part is bt else part.pair_range     # a chunk's range inside bt
-            with torch.cuda.stream(st):
-                r, ev = self._stage_a(part, b0, b1, o, keep_feats, gt_ks, min_pt, st, gc, col=col)
-            outs.append(r)
-            events.append(ev)
+        lag = 2 if (self.copy_defer and len(parts) > 2 and len(streams) == 2 and self.copy_stream
+                    and not self.zero_copy and not device_lsa) else 0
+        pending = [] if lag else None
+        self._plan_events = [] if lag else None
+        try:
+            for c, part in enumerate(parts):
+                st = streams[c % len(streams)]
+                b0, b1 = (0, B) if part is bt else part.pair_range     # a chunk's range inside bt
+                with torch.cuda.stream(st):
+                    r, ev = self._stage_a(part, b0, b1, o, keep_feats, gt_ks, min_pt, st, gc, col=col, defer=pending)
+                outs.append(r)
+                events.append(ev)
+                if lag and c >= lag:
+                    # chunk c - lag's copy after chunk c's first plan (same stream as chunk c - lag)
+                    pb0, pb1, pdone = pending[c - lag]
+                    events[c - lag] = self._enqueue_copy(dev, pb0, pb1, o, pdone, after=self._plan_events[c])
+            if lag:
+                for c in range(max(0, len(parts) - lag), len(parts)):
+                    pb0, pb1, pdone = pending[c]
+                    events[c] = self._enqueue_copy(dev, pb0, pb1, o, pdone)
+        finally:
+            self._plan_events = None
         t_enq = time.perf_counter()
         t_lsa, t_first = 0.0, None
         for c, (part, ev) in enumerate(zip(parts, events)):
