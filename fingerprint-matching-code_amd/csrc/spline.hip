@@ -825,7 +825,10 @@ __global__ __launch_bounds__(768) void combine_scatter_bwd_kernel(
     const int* __restrict__ grp_e, const float* __restrict__ basis_e, const int* __restrict__ rptr,
     const int* __restrict__ rcsr_e, const int* __restrict__ rnbr, const int* __restrict__ slot_of,
     const int* __restrict__ argmax, long num_nodes, int nmax, const int* __restrict__ nvalid, int mode,
-    const float* __restrict__ gout, const float* __restrict__ hout, float* __restrict__ dY) {
+    const float* __restrict__ gout, const float* __restrict__ hout, float* __restrict__ dY,
+    bf16_t* __restrict__ dYb) {
+    // dYb (bf16 mode): the same rows' bf16 operand copy for the dX product GEMM, written here
+    // instead of a separate cast pass over the plan's row bound (~2.5x the real rows)
     extern __shared__ float acc[];                       // [NCELL - 1][768]
     const long u = blockIdx.x;
     const int c = threadIdx.x;
@@ -855,8 +858,15 @@ __global__ __launch_bounds__(768) void combine_scatter_bwd_kernel(
         acc[fpm::spline_cell(gg, 3) * 768 + c] += bs.w * g;
     }
     for (int k = 0; k < NCELL - 1; ++k)
-        if ((m >> k) & 1) dY[(long)rowid[u * NCELL + k] * 768 + c] = acc[k * 768 + c];
-    dY[((long)cell_off[NCELL - 1] + u) * 768 + c] = gval(u);
+        if ((m >> k) & 1) {
+            const long o = (long)rowid[u * NCELL + k] * 768 + c;
+            dY[o] = acc[k * 768 + c];
+            if (dYb) dYb[o] = fpm::f2bf(acc[k * 768 + c]);
+        }
+    const long o = ((long)cell_off[NCELL - 1] + u) * 768 + c;
+    const float gu = gval(u);
+    dY[o] = gu;
+    if (dYb) dYb[o] = fpm::f2bf(gu);
 }
 
 // out[c][q] = rows[q] >= 0 ? in[rows[q]][c] : 0 for c < C, q < Q (ldo >= Q): the K-major operand
@@ -1360,7 +1370,7 @@ extern "C" int fpm_spline_conv_bwd_data_scatter(int dtype, const void* plan_ws, 
                            (const int*)(w + L.cell_off), (const int*)(w + L.rowid), (const int*)(w + L.mask),
                            (const int*)(w + L.grp_e), (const float*)(w + L.basis_e), (const int*)(rw + L.dst_ptr),
                            (const int*)(rw + L.csr_e), (const int*)(rw + L.nbr_local), (const int*)slot_of, argmax,
-                           num_nodes, nmax, nvalid, mode, gout, hout, dY);
+                           num_nodes, nmax, nvalid, mode, gout, hout, dY, dtype == 1 ? (bf16_t*)dY_op : nullptr);
     } else {
     (void)hipMemsetAsync(dY, 0, (size_t)L.max_rows * D * sizeof(float), st);
     if (dtype == 0)
@@ -1372,7 +1382,7 @@ extern "C" int fpm_spline_conv_bwd_data_scatter(int dtype, const void* plan_ws, 
                            (const int*)(w + L.cell_off), (const int*)(w + L.dst_ptr), (const int4*)(w + L.rows4),
                            (const float4*)(w + L.basis4), num_nodes, nmax, nvalid, mode, gout, hout, dY);
     }
-    if (dtype == 1) {
+    if (dtype == 1 && !argmax) {
         int rc = fpm_cast_bf16(dY, dY_op, L.max_rows * D, stream);
         if (rc) return rc;
     }

@@ -118,7 +118,8 @@ class SplineLayerFn(torch.autograd.Function):
         rows_max = nbytes // (4 * C.NODE_FEATURE_DIM)
         dY = torch.empty(rows_max, C.NODE_FEATURE_DIM, device=dev, dtype=torch.float32)
         dXr = torch.empty_like(dY)
-        dY_op = dY.to(op) if op == torch.bfloat16 else None
+        # the bf16 operand copy is written by the backward kernel (no cast of the fp32 rows here)
+        dY_op = torch.empty(rows_max, C.NODE_FEATURE_DIM, device=dev, dtype=op) if op == torch.bfloat16 else None
         dX = torch.empty(sd.num_nodes, C.NODE_FEATURE_DIM, device=dev, dtype=torch.float32)
         rplan = None
         if ctx.am is not None:
