@@ -467,7 +467,10 @@ class Net(nn.Module):
     def _streams(self, dev):
         key = str(dev)
         if key not in self._stream_cache:
-            self._stream_cache[key] = [torch.cuda.Stream(dev) for _ in range(self.n_streams)]
+            # FPM_STREAM_PRIO=1: compute streams at high priority (the ds_mat copy stream stays at
+            # the default) -- A/B switch for the copy blit's interference
+            prio = -1 if os.environ.get("FPM_STREAM_PRIO", "0") == "1" else 0
+            self._stream_cache[key] = [torch.cuda.Stream(dev, priority=prio) for _ in range(self.n_streams)]
         return self._stream_cache[key]
 
     def _lsa_streams(self, dev):
