@@ -237,7 +237,9 @@ class Net(nn.Module):
         E = bt.E[side]
         plan = ops.spline_plan(bt.src[side], bt.dst[side], bt.pseudo[side], nn_, bt.nmax[side],
                                bt.max_graph_edges(side))
-        if side == 0 and self._plan_events is not None:
+        # FPM_COPY_DEFER=1: the previous-but-one chunk's D2H starts after this side-0 plan;
+        # 2: after the side-0 bf16 cast too (the product GEMM then runs beside the copy's blit)
+        if side == 0 and self._plan_events is not None and (self.copy_defer == 1 or bt.shared0):
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(dev))
             self._plan_events.append(ev)
@@ -245,6 +247,10 @@ class Net(nn.Module):
             return (plan,) + self._spline_shared(wp, bt, cscale)
         x0 = bt.x[side]
         x_op = ops.cast_bf16(x0) if op == torch.bfloat16 else x0
+        if side == 0 and self._plan_events is not None and self.copy_defer == 2 and not bt.shared0:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(dev))
+            self._plan_events.append(ev)
         yws = ops.spline_y_ws(ops.BF16 if op == torch.bfloat16 else ops.F32, E, nn_, dev)
         h = torch.empty(nn_, C.NODE_FEATURE_DIM, device=dev, dtype=op)
         ops.spline_conv(x_op, plan, E, nn_, bt.nmax[side], bt.n[side], wp["W0"], wp["bias0"], yws, 0, out_t=h)
