@@ -114,7 +114,7 @@ class Net(nn.Module):
         self._pinned = None
         self._stream_cache = {}
         self.n_streams = max(1, int(os.environ.get("FPM_STREAMS", "2")))
-        self.tail_splits = int(os.environ.get("FPM_TAIL", "1"))
+        self.tail_splits = int(os.environ.get("FPM_TAIL", "2"))
         self.head_splits = int(os.environ.get("FPM_HEAD", "0"))
         # FPM_ZERO_COPY=1: soft_topk writes ds_mat straight into pinned host memory instead of a
         # stream copy.  Measured slower (21.2K -> 19.7K pairs/s: the kernel stalls on PCIe writes
