@@ -131,6 +131,11 @@ class Net(nn.Module):
         # copy's blit kernel and stalls ~25x
         self.copy_defer = int(os.environ.get("FPM_COPY_DEFER", "1"))
         self._plan_events = None
+        # FPM_OFFSET=1: the second stream starts its first chunk after the first chunk's SplineConv,
+        # so the streams' phases interleave (MFMA-heavy SplineConv beside the VALU / memory-bound GNN,
+        # Sinkhorn and soft top-k) instead of running the same stages side by side
+        self.stream_offset = int(os.environ.get("FPM_OFFSET", "0"))
+        self._offset_events = None
         # the host thread waits for each chunk's ds_mat with a sleeping (not spinning) event wait,
         # leaving its core to the Hungarian pool
         self.blocking_wait = os.environ.get("FPM_BLOCKING_WAIT", "1") == "1"
@@ -435,6 +440,10 @@ class Net(nn.Module):
         plan0, x1c, f1 = self._spline_side(wp, bt, 0, coef)
         plan1, x2, f2 = self._spline_side(wp, bt, 1, None)
         self._mark("splineconv")
+        if self._offset_events is not None:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(dev))
+            self._offset_events.append(ev)
         # Kp^T per pair: emb0[b][j][i] = softplus((x1_i o c) . x2_j) - 0.5 on the valid block (ngm.py:277-321)
         X = torch.empty(B, 1, n2max, n1max, device=dev, dtype=torch.float32)
         ops.gemm(x2, x1c, n2max, n1max, C.NODE_FEATURE_DIM, C.NODE_FEATURE_DIM, C.NODE_FEATURE_DIM, batch=B,
@@ -637,10 +646,14 @@ class Net(nn.Module):
                     and not self.zero_copy and not device_lsa) else 0
         pending = [] if lag else None
         self._plan_events = [] if lag else None
+        self._offset_events = [] if (self.stream_offset and len(streams) == 2 and len(parts) > 1) else None
         try:
             for c, part in enumerate(parts):
                 st = streams[c % len(streams)]
                 b0, b1 = (0, B) if part is bt else part.pair_range     # a chunk's range inside bt
+                if c == 1 and self._offset_events:
+                    st.wait_event(self._offset_events[0])
+                    self._offset_events = None
                 with torch.cuda.stream(st):
                     r, ev = self._stage_a(part, b0, b1, o, keep_feats, gt_ks, min_pt, st, gc, col=col, defer=pending)
                 outs.append(r)
@@ -655,6 +668,7 @@ class Net(nn.Module):
                     events[c] = self._enqueue_copy(dev, pb0, pb1, o, pdone)
         finally:
             self._plan_events = None
+            self._offset_events = None
         t_enq = time.perf_counter()
         t_lsa, t_first = 0.0, None
         for c, (part, ev) in enumerate(zip(parts, events)):
