@@ -254,7 +254,7 @@ __global__ __launch_bounds__(256) void afau_row_attn_kernel(const float* __restr
 // q = lane >> 4 of wave wv owns the 16 CONTIGUOUS columns j = wv*64 + q*16 + t (the other kernel
 // interleaves them with stride 4), so the costs are 16-B loads too; the P . V sum over j runs in
 // a different order (fp32 rounding only).
-template <typename T, bool SPLIT, bool FAST>
+template <typename T, bool SPLIT, bool FAST, int TJ = 16>
 __global__ __launch_bounds__(256) void afau_row_attn_v_kernel(const float* __restrict__ cost, long c_sb, long c_ld,
                                                               int n1max, int n2max, const int* __restrict__ n2,
                                                               const float* __restrict__ Wv, int emb,
@@ -265,34 +265,37 @@ __global__ __launch_bounds__(256) void afau_row_attn_v_kernel(const float* __res
                                                               float2* __restrict__ stats) {
     typedef float f32x4_t __attribute__((ext_vector_type(4)));
     typedef float f2v __attribute__((ext_vector_type(2)));
-    constexpr int TJ = 16, VS = 260;
+    constexpr int VS = 16 * TJ + 4;                       // padded V row (floats)
     __shared__ __attribute__((aligned(16))) float vbuf[2][16 * VS];
     __shared__ float part[2][4][256];
     __shared__ float2 rowms[2][4][16];
     const int b = blockIdx.x, i0 = blockIdx.y * 16, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int n2b = n2[b];
-    const int r = lane & 15, i = i0 + r, jl = wv * 64 + (lane >> 4) * 16;
+    const int r = lane & 15, i = i0 + r, jl = wv * 4 * TJ + (lane >> 4) * TJ;
 
     // V staging: thread copies row vr, columns [vc, vc + 16) of the head's slice (zero past n2b)
-    const int vr = tid >> 4, vc = (tid & 15) * 16;
-    float4 vnext[4];
+    const int vr = tid >> 4, vc = (tid & 15) * TJ;
+    float4 vnext[TJ / 4];
     auto load_v = [&](int h) {
         const float* src = Wv + (long)(h * 16 + vr) * emb + vc;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            float4 v = *(const float4*)(src + 4 * k);
+        for (int k = 0; k < TJ / 4; ++k) {
             const int j = vc + 4 * k;
-            if (j + 0 >= n2b) v.x = 0.f;
-            if (j + 1 >= n2b) v.y = 0.f;
-            if (j + 2 >= n2b) v.z = 0.f;
-            if (j + 3 >= n2b) v.w = 0.f;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (j + 3 < n2b) {                            // n2b <= n2max <= emb: inside the row
+                v = *(const float4*)(src + 4 * k);
+            } else if (j < n2b) {
+                v.x = src[4 * k];
+                if (j + 1 < n2b) v.y = src[4 * k + 1];
+                if (j + 2 < n2b) v.z = src[4 * k + 2];
+            }
             vnext[k] = v;
         }
     };
     auto store_v = [&](int buf) {
         float* dst = &vbuf[buf][vr * VS + vc];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) *(float4*)(dst + 4 * k) = vnext[k];
+        for (int k = 0; k < TJ / 4; ++k) *(float4*)(dst + 4 * k) = vnext[k];
     };
     load_v(0);
     // costs: this lane's 16 contiguous columns of row i
@@ -302,7 +305,7 @@ __global__ __launch_bounds__(256) void afau_row_attn_v_kernel(const float* __res
         const bool vec = i < n1max && jl + TJ <= n2max && (((uintptr_t)Cb) & 15) == 0;
         if (vec) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < TJ / 4; ++k) {
                 const float4 c4 = *(const float4*)(Cb + 4 * k);
                 creg[4 * k] = c4.x; creg[4 * k + 1] = c4.y; creg[4 * k + 2] = c4.z; creg[4 * k + 3] = c4.w;
             }
@@ -421,7 +424,7 @@ __global__ __launch_bounds__(256) void afau_row_attn_v_kernel(const float* __res
         {
             const float* vs = &vbuf[buf][r * VS + jl];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < TJ / 4; ++k) {
                 const float4 v4 = *(const float4*)(vs + 4 * k);
                 vreg[4 * k] = v4.x; vreg[4 * k + 1] = v4.y; vreg[4 * k + 2] = v4.z; vreg[4 * k + 3] = v4.w;
             }
@@ -640,7 +643,7 @@ extern "C" int fpm_crossset_attn_fwd(int dtype, const float* cost, long c_sb, lo
     FPM_CHECK_ARG(n2max <= 640, "crossset_attn: n2max %d > 640", n2max);
     // fp32 (parity) mode scores with the 16-term sum (the reference's operation order); the LUT is
     // the bf16 throughput mode's (env FPM_AFAU_LUT / fpm_set_tuning("afau_lut") override)
-    const bool v_ok = n2max <= 256 && emb >= 256 && emb % 4 == 0 && ((uintptr_t)Wv & 15) == 0 && afau_attn_v_flag() != 0;
+    const bool v_ok = n2max <= 512 && emb >= n2max && emb % 4 == 0 && ((uintptr_t)Wv & 15) == 0 && afau_attn_v_flag() != 0;
     const int lut = afau_lut_flag() != 2 ? afau_lut_flag() : (dtype != 0 && !v_ok);
 #define FPM_ATT(TT, TJ_, SP_)                                                                                    \
     hipLaunchKernelGGL((afau_row_attn_kernel<TT, TJ_, SP_>), grid, dim3(256), 0, st, cost, c_sb, c_ld, n1max, n2max, \
@@ -648,8 +651,16 @@ extern "C" int fpm_crossset_attn_fwd(int dtype, const float* cost, long c_sb, lo
     // the LDS-staged-V kernel (16-term scores) where it applies; env FPM_AFAU_ATTN_V=0 keeps the other
     const bool vpath = !lut && v_ok;
 #define FPM_ATTV(TT, SP_)                                                                                        \
-    hipLaunchKernelGGL((afau_row_attn_v_kernel<TT, SP_, !std::is_same<TT, float>::value>), grid, dim3(256), 0, st, cost, c_sb, c_ld, n1max, n2max,  \
-                       n2, Wv, emb, mix1w, mix1b, mix2w, mix2b, (TT*)out, (float2*)stats)
+    do {                                                                                                         \
+        if (n2max <= 256)                                                                                        \
+            hipLaunchKernelGGL((afau_row_attn_v_kernel<TT, SP_, !std::is_same<TT, float>::value, 16>), grid,     \
+                               dim3(256), 0, st, cost, c_sb, c_ld, n1max, n2max, n2, Wv, emb, mix1w, mix1b,      \
+                               mix2w, mix2b, (TT*)out, (float2*)stats);                                          \
+        else                                                                                                     \
+            hipLaunchKernelGGL((afau_row_attn_v_kernel<TT, SP_, !std::is_same<TT, float>::value, 32>), grid,     \
+                               dim3(256), 0, st, cost, c_sb, c_ld, n1max, n2max, n2, Wv, emb, mix1w, mix1b,      \
+                               mix2w, mix2b, (TT*)out, (float2*)stats);                                          \
+    } while (0)
     if (vpath) {
         if (dtype == 0) FPM_ATTV(float, false);
         else if (dtype == 1) FPM_ATTV(bf16_t, false);

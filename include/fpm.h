@@ -108,9 +108,9 @@ int fpm_memcpy_async(void* dst, const void* src, long bytes, int kind, void* str
  *       (0 = max-shifted lse every step; 2 = 1 with scalar loads in the n > 256 streaming kernel)
  *   "topk_fast" (FPM_TOPK_FAST, default 1): shifted single-pass early soft top-k column steps
  *   "afau_lut" (FPM_AFAU_LUT, default 2 = by dtype): AFA-U score lookup table (1) or 16-term sum (0);
- *                by dtype: the LUT only for bf16 rows the LDS-V kernel cannot take (n2max > 256)
+ *                by dtype: the LUT only for bf16 rows the LDS-V kernel cannot take (n2max > 512)
  *   "afau_attn_v" (FPM_AFAU_ATTN_V, default 1): the cross-set attention with V staged in LDS and the
- *                range-classified scores (bf16) / 16-term chain (fp32) for n2max <= 256 */
+ *                range-classified scores (bf16) / 16-term chain (fp32) for n2max <= 512 */
 int fpm_set_tuning(const char* key, int value);
 
 /* ---- SplineConv message passing ---------------------------------------------------------------

@@ -802,7 +802,8 @@ def test_gemm_persist_bit_identical(sd, npairs, n):
             assert torch.equal(r[k], outs[0][k]), k
 
 
-@pytest.mark.parametrize("B,n1,n2max,n2s", [(3, 64, 64, [64, 50, 61]), (2, 200, 256, [256, 233]), (2, 37, 45, [45, 20])])
+@pytest.mark.parametrize("B,n1,n2max,n2s", [(3, 64, 64, [64, 50, 61]), (2, 200, 256, [256, 233]), (2, 37, 45, [45, 20]),
+                                             (2, 100, 512, [512, 437]), (1, 40, 301, [301])])
 def test_crossset_attn_lds_v_kernel(sd, B, n1, n2max, n2s):
     """The LDS-staged-V attention kernel (n2max <= 256) against the global-V kernel with the same
     16-term scores: fp32 outputs and softmax stats within fp32 summation-order rounding; the bf16
