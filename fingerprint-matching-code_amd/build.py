@@ -1,10 +1,16 @@
 """Build ``libfpm_hip.so`` (HIP kernels for gfx950 + host C++) in-tree with hipcc.
 
-    python fingerprint-matching-code_amd/build.py [--jobs N] [--debug]
+    python fingerprint-matching-code_amd/build.py [--jobs N] [--debug] [--asan]
 
 Objects go to ``csrc/build/``; the shared library lands next to this file so it travels to the
 GPU box with the repo snapshot.  Incremental: a source is recompiled when it (or a header) is
 newer than its object.
+
+``--asan``: a host-only build of the C-ABI's CPU code (``csrc/lsa.cpp``, ``csrc/sparse_host.cpp``)
+with AddressSanitizer + UBSan, linked with the driver ``tests/asan/host_driver.cpp`` into
+``csrc/build/asan_host_driver`` (run by ``tests/test_asan_host.py``); ``--tsan``: the same with
+ThreadSanitizer (``tsan_host_driver``, the LSA thread pool).  GPU sanitizers are not
+available on the pool; the device code is not part of this build.
 """
 import argparse
 import glob
@@ -53,6 +59,35 @@ def _compile(src, debug):
     return obj
 
 
+ASAN_SRCS = ("lsa.cpp", "sparse_host.cpp")
+SANITIZERS = {"asan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"],
+              "tsan": ["-fsanitize=thread"]}
+
+
+def build_asan(verbose=True, kind="asan"):
+    """Host-only sanitizer build of the CPU sources + the C driver (g++, no HIP).  ``kind``:
+    "asan" (AddressSanitizer + UBSan) or "tsan" (ThreadSanitizer, for the LSA thread pool)."""
+    os.makedirs(OBJ, exist_ok=True)
+    ASAN_BIN = os.path.join(OBJ, "%s_host_driver" % kind)
+    repo = os.path.dirname(HERE)
+    driver = os.path.join(repo, "tests", "asan", "host_driver.cpp")
+    srcs = [os.path.join(CSRC, f) for f in ASAN_SRCS] + [driver]
+    hdrs = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(repo, "include", "*.h"))
+    newest = max(os.path.getmtime(f) for f in srcs + hdrs)
+    if os.path.exists(ASAN_BIN) and os.path.getmtime(ASAN_BIN) >= newest:
+        return ASAN_BIN
+    cmd = [os.environ.get("CXX", "g++"), "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer"] + SANITIZERS[kind] + [
+           "-pthread",
+           "-I" + CSRC, "-I" + os.path.join(repo, "include")] + srcs + ["-o", ASAN_BIN + ".tmp"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("asan build failed: %s\n%s" % (" ".join(cmd), r.stderr))
+    os.replace(ASAN_BIN + ".tmp", ASAN_BIN)
+    if verbose:
+        print("built %s" % ASAN_BIN)
+    return ASAN_BIN
+
+
 def build(jobs=8, debug=False, force=False, verbose=True):
     os.makedirs(OBJ, exist_ok=True)
     hdrs = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(os.path.dirname(HERE), "include", "*.h"))
@@ -78,5 +113,13 @@ if __name__ == "__main__":
     ap.add_argument("--jobs", type=int, default=8)
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--force", action="store_true")
+    ap.add_argument("--asan", action="store_true", help="host-only ASan/UBSan build of the CPU sources + driver")
+    ap.add_argument("--tsan", action="store_true", help="host-only ThreadSanitizer build of the same")
     a = ap.parse_args()
-    build(a.jobs, a.debug, a.force)
+    if a.asan or a.tsan:
+        if a.asan:
+            build_asan(kind="asan")
+        if a.tsan:
+            build_asan(kind="tsan")
+    else:
+        build(a.jobs, a.debug, a.force)

@@ -7,7 +7,10 @@
 //
 // NCHW fp32.  Per-channel sums are deterministic: one workgroup per (sample, channel) plane sums
 // it (float4 loads, wave shuffle trees, fixed order) into part[n][c][2]; a second pass combines the N
-// partials per channel in order in fp64.
+// partials per channel in order in fp64.  Forward statistics are centred: each plane stores its sum
+// and the sum of squares about its own mean (a second pass over the plane), and the channel pass
+// merges them with Chan's formula, M2 = sum_n [M2_n + HW (mean_n - mean)^2] -- no E[r^2] - mean^2
+// cancellation when |mean| >> std (torch's batch_norm is Welford-based).
 //   forward:  r = relu(x);  mean, var over (n, h, w);  y = (r - mean) * invstd * gamma + beta
 //   backward: xhat = (r - mean) * invstd;  sdy = sum dy, sdx = sum dy * xhat (per channel);
 //             dx = [x > 0] * gamma * invstd * (dy - sdy / M - xhat * sdx / M);
@@ -38,42 +41,52 @@ __global__ __launch_bounds__(BN_T) void bn_plane_sums_kernel(const float* __rest
         mean = stats[2 * c];
         inv = stats[2 * c + 1];
     }
+    // pass 0 (MODE 0): plane sum; MODE 0 pass 1: squares about the plane mean; MODE 1: both sums
     float a0 = 0.f, a1 = 0.f;
-    auto acc = [&](float xv, float dv) {
+    float pm = 0.f;
+    auto acc = [&](int pass, float xv, float dv) {
         const float r = fmaxf(xv, 0.f);
         if (MODE == 0) {
-            a0 += r;
-            a1 = fmaf(r, r, a1);
+            if (pass == 0) {
+                a0 += r;
+            } else {
+                const float d = r - pm;
+                a1 = fmaf(d, d, a1);
+            }
         } else {
             a0 += dv;
             a1 = fmaf(dv, (r - mean) * inv, a1);
         }
     };
-    const bool vec = (HW & 3) == 0;
-    if (vec) {
-        for (long i = 4 * (long)threadIdx.x; i < HW; i += 4 * BN_T) {
-            const float4 v = *(const float4*)(xp + i);
-            float4 d = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (MODE == 1) d = *(const float4*)(dp + i);
-            acc(v.x, d.x); acc(v.y, d.y); acc(v.z, d.z); acc(v.w, d.w);
+    auto sweep = [&](int pass) {
+        if ((HW & 3) == 0) {
+            for (long i = 4 * (long)threadIdx.x; i < HW; i += 4 * BN_T) {
+                const float4 v = *(const float4*)(xp + i);
+                float4 d = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (MODE == 1) d = *(const float4*)(dp + i);
+                acc(pass, v.x, d.x); acc(pass, v.y, d.y); acc(pass, v.z, d.z); acc(pass, v.w, d.w);
+            }
+        } else {
+            for (long i = threadIdx.x; i < HW; i += BN_T) acc(pass, xp[i], MODE == 1 ? dp[i] : 0.f);
         }
-    } else {
-        for (long i = threadIdx.x; i < HW; i += BN_T) acc(xp[i], MODE == 1 ? dp[i] : 0.f);
+    };
+    // fixed-order block sum of v (every thread gets the result)
+    auto bsum = [&](float v, int slot) {
+        v = wsum(v);
+        if ((threadIdx.x & 63) == 0) red[slot][threadIdx.x >> 6] = v;
+        __syncthreads();
+        float s = 0.f;
+        for (int k = 0; k < BN_T / 64; ++k) s += red[slot][k];
+        return s;
+    };
+    sweep(0);
+    const float s0 = bsum(a0, 0);
+    if (MODE == 0) {
+        pm = s0 / (float)HW;
+        sweep(1);
     }
-    a0 = wsum(a0);
-    a1 = wsum(a1);
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) {
-        red[0][w] = a0;
-        red[1][w] = a1;
-    }
-    __syncthreads();
+    const float s1 = bsum(a1, 1);
     if (threadIdx.x == 0) {
-        float s0 = 0.f, s1 = 0.f;
-        for (int k = 0; k < BN_T / 64; ++k) {
-            s0 += red[0][k];
-            s1 += red[1][k];
-        }
         part[2 * (long)nc] = s0;
         part[2 * (long)nc + 1] = s1;
     }
@@ -97,8 +110,13 @@ __global__ void bn_channel_kernel(const float* __restrict__ part, int N, int C, 
     const double M = (double)N * (double)HW;
     if (MODE == 0) {
         const double mean = s0 / M;
-        double var = s1 / M - mean * mean;
-        if (var < 0.0) var = 0.0;
+        // Chan merge of the planes' centred sums (the plane means as the fp32 values pass 1 used)
+        double m2 = 0.0;
+        for (int n = 0; n < N; ++n) {
+            const double d = (double)(part[2 * ((long)n * C + c)] / (float)HW) - mean;
+            m2 += (double)part[2 * ((long)n * C + c) + 1] + (double)HW * d * d;
+        }
+        const double var = m2 / M;
         stats[2 * c] = (float)mean;
         stats[2 * c + 1] = (float)(1.0 / sqrt(var + (double)eps));
         if (running_mean) {

@@ -7,6 +7,35 @@
 // column among equal reduced costs) and the transpose of tall matrices follow that published
 // method so that, on inputs with ties, the same optimum is returned.  Costs are evaluated in
 // double from the float32 input (-s), as scipy converts its input to float64.
+//
+// Third-party notice.  The scalar solver lsap_solve() below restates scipy's
+// scipy/optimize/rectangular_lsap/rectangular_lsap.cpp (P. M. Larsen's implementation of Crouse's
+// pseudocode) closely, including its variable names; it is kept as the bit-exact reference of the
+// vectorised solvers further down.  scipy is distributed under the BSD 3-Clause licence:
+//
+//   Copyright (c) 2001-2002 Enthought, Inc. 2003, SciPy Developers.
+//   All rights reserved.
+//
+//   Redistribution and use in source and binary forms, with or without modification, are
+//   permitted provided that the following conditions are met:
+//   1. Redistributions of source code must retain the above copyright notice, this list of
+//      conditions and the following disclaimer.
+//   2. Redistributions in binary form must reproduce the above copyright notice, this list of
+//      conditions and the following disclaimer in the documentation and/or other materials
+//      provided with the distribution.
+//   3. Neither the name of the copyright holder nor the names of its contributors may be used to
+//      endorse or promote products derived from this software without specific prior written
+//      permission.
+//
+//   THIS SOFTWARE IS PROVIDED BY THE COPYRIGHT HOLDERS AND CONTRIBUTORS "AS IS" AND ANY EXPRESS
+//   OR IMPLIED WARRANTIES, INCLUDING, BUT NOT LIMITED TO, THE IMPLIED WARRANTIES OF
+//   MERCHANTABILITY AND FITNESS FOR A PARTICULAR PURPOSE ARE DISCLAIMED. IN NO EVENT SHALL THE
+//   COPYRIGHT HOLDER OR CONTRIBUTORS BE LIABLE FOR ANY DIRECT, INDIRECT, INCIDENTAL, SPECIAL,
+//   EXEMPLARY, OR CONSEQUENTIAL DAMAGES (INCLUDING, BUT NOT LIMITED TO, PROCUREMENT OF SUBSTITUTE
+//   GOODS OR SERVICES; LOSS OF USE, DATA, OR PROFITS; OR BUSINESS INTERRUPTION) HOWEVER CAUSED
+//   AND ON ANY THEORY OF LIABILITY, WHETHER IN CONTRACT, STRICT LIABILITY, OR TORT (INCLUDING
+//   NEGLIGENCE OR OTHERWISE) ARISING IN ANY WAY OUT OF THE USE OF THIS SOFTWARE, EVEN IF ADVISED
+//   OF THE POSSIBILITY OF SUCH DAMAGE.
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>

@@ -1360,12 +1360,10 @@ extern "C" int fpm_spline_conv_bwd_data_scatter(int dtype, const void* plan_ws, 
         hipLaunchKernelGGL(slot_of_kernel, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, st,
                            (const int*)(w + L.csr_e), E, slot_of);
         const size_t lds = (size_t)(NCELL - 1) * D * sizeof(float);
-        static bool attr = false;
-        if (!attr) {
-            (void)hipFuncSetAttribute((const void*)combine_scatter_bwd_kernel,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            attr = true;
-        }
+        // every call (the attribute is per device; the call is cheap), like the forward kernels
+        const hipError_t ae = hipFuncSetAttribute((const void*)combine_scatter_bwd_kernel,
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        FPM_CHECK_ARG(ae == hipSuccess, "spline_conv_bwd: %zu B of LDS refused: %s", lds, hipGetErrorString(ae));
         hipLaunchKernelGGL(combine_scatter_bwd_kernel, dim3((unsigned)num_nodes), dim3(D), lds, st,
                            (const int*)(w + L.cell_off), (const int*)(w + L.rowid), (const int*)(w + L.mask),
                            (const int*)(w + L.grp_e), (const float*)(w + L.basis_e), (const int*)(rw + L.dst_ptr),

@@ -79,6 +79,12 @@ class Net(nn.Module):
             # ResNet18_final split (feature_extractor.py:7-75), reference parameter names
             from .backbone import build_resnet18_split
             self.node_layers, self.edge_layers, self.final_layers = build_resnet18_split(seed)
+        # train.py's parameter groups (train.py:157-239).  backbone_params: the backbone's own
+        # parameters (feature_extractor.py:19 takes list(self.parameters()) before the matcher
+        # modules exist); k_params_id / k_params: encoder_k + final_row + final_col (ngm.py:174-199)
+        self.backbone_params = ([p for m in (self.node_layers, self.edge_layers, self.final_layers)
+                                 for p in m.parameters()] if backbone else [])
+        self.k_params_id = [id(p) for m in self._k_modules() for p in m.parameters()]
         self._backbone_dev = None
         # Hungarian step (utils/hungarian.py): "host" = C++ thread pool over a pinned ds_mat copy,
         # "device" = the same solver restated per wavefront (fpm_lsa_batch_device, bit-identical)
@@ -147,6 +153,17 @@ class Net(nn.Module):
         self.eval()
 
     # ------------------------------------------------------------------------------------------
+    def _k_modules(self):
+        return (self.encoder_k, self.final_row, self.final_col)
+
+    @property
+    def k_params(self):
+        """The k regressor's optimizer groups (ngm.py:195-199): encoder_k, final_row, final_col.
+        The reference stores generators (consumed by the first pass over them); every access here
+        returns fresh lists of the same parameters, so stage 1's freeze loop and a later
+        ``optim.AdamW(model.k_params)`` both see them."""
+        return [{"params": list(m.parameters())} for m in self._k_modules()]
+
     def _sd(self):
         return dict(self.state_dict())
 

@@ -43,8 +43,9 @@ def _op_dtype(mode):
 class _Side:
     """Per-side graph context: spline plan (in-edge CSR), reversed plan (out-edge CSR)."""
 
-    def __init__(self, bt, side):
+    def __init__(self, bt, side, wcache=None):
         self.bt, self.side = bt, side
+        self.wcache = {} if wcache is None else wcache   # this step's weight operand copies (_spline_w)
         self.nmax = bt.nmax[side]
         self.num_nodes = bt.B * self.nmax
         self.E = bt.E[side]
@@ -62,24 +63,21 @@ class _Side:
         return ops.plan_csr(self._rplan, self.E, self.num_nodes)
 
 
-_WCACHE = {}
-
-
-def _spline_w(weight, root, op, fwd):
+def _spline_w(cache, weight, root, op, fwd):
     """Operand copies of a SplineConv layer's weights: fwd (26, out, in) = cells transposed then
     root^T (the forward GEMM's B), else (26, in, out) = the reference layout (the backward's B).
-    Both sides of the Siamese pair share the layer, so each copy is built once per weight version
-    (the optimizer step bumps ``_version``)."""
-    key = (weight.data_ptr(), root.data_ptr(), weight._version, root._version, op, fwd)
-    w = _WCACHE.get(key)
+    Both sides of the Siamese pair share the layer, so each copy is built once per training step:
+    ``cache`` is the step's own dict (``run_train`` makes a fresh one per call and the forward /
+    backward of that step read it), keyed by the Parameter objects, so nothing carries over to a
+    later step, another Net or weights changed in place through ``.data``."""
+    key = (id(weight), id(root), op, fwd)
+    w = cache.get(key)
     if w is None:
-        if len(_WCACHE) > 16:
-            _WCACHE.clear()
         if fwd:
             w = torch.cat([weight.detach().transpose(1, 2), root.detach().t()[None]]).contiguous().to(op)
         else:
             w = torch.cat([weight.detach(), root.detach()[None]]).contiguous().to(op)
-        _WCACHE[key] = w
+        cache[key] = w
     return w
 
 
@@ -89,7 +87,7 @@ class SplineLayerFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, root, bias, xres, sd, mode, dmode):
         op = _op_dtype(dmode)
-        Wf = _spline_w(weight, root, op, True)
+        Wf = _spline_w(sd.wcache, weight, root, op, True)
         x_op = x.detach().to(op).contiguous()
         code = ops.BF16 if op == torch.bfloat16 else ops.F32
         yws = ops.spline_y_ws(code, sd.E, sd.num_nodes, x.device)
@@ -113,7 +111,7 @@ class SplineLayerFn(torch.autograd.Function):
         op = _op_dtype(ctx.dmode)
         dev = gout.device
         gout = gout.contiguous().float()
-        Wb = _spline_w(weight, root, op, False)
+        Wb = _spline_w(sd.wcache, weight, root, op, False)
         nbytes = _lib.load().fpm_spline_y_bytes(ops.F32, sd.E, sd.num_nodes)
         rows_max = nbytes // (4 * C.NODE_FEATURE_DIM)
         dY = torch.empty(rows_max, C.NODE_FEATURE_DIM, device=dev, dtype=torch.float32)
@@ -543,7 +541,8 @@ def run_train(net, bt, gt_perm=None, label=None):
     gw = torch.cat([bt.w[0], bt.w[1]], dim=1)
     gw = gw / torch.norm(gw, dim=1, keepdim=True)
     coef = torch.tanh(F.linear(gw, Pm("vertex_affinity.A.weight"), Pm("vertex_affinity.A.bias")))
-    sides = [_Side(bt, 0), _Side(bt, 1)]
+    wcache = {}                          # per step: both sides share the SplineConv operand copies
+    sides = [_Side(bt, 0, wcache), _Side(bt, 1, wcache)]
     feats = []
     for side in range(2):
         sd = sides[side]

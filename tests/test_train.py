@@ -434,12 +434,13 @@ def test_outer_sum_kernel():
         assert torch.equal(_outer_sum(U.to(DEV), V.to(DEV)), w)
 
 
-@pytest.mark.parametrize("shape", [(4, 16, 64, 64), (3, 32, 17, 19)])
-def test_bn_relu_train_vs_torch(shape):
+@pytest.mark.parametrize("shape,off", [((4, 16, 64, 64), 0.0), ((3, 32, 17, 19), 0.0), ((4, 16, 64, 64), 100.0)])
+def test_bn_relu_train_vs_torch(shape, off):
     """HIP BatchNorm2d(relu(x)) in train mode vs torch F.relu + F.batch_norm(training=True):
-    output, running buffers and the gradients of x, gamma, beta (ngm.py:90-99)."""
+    output, running buffers and the gradients of x, gamma, beta (ngm.py:90-99).  ``off``: a large
+    per-channel offset (|mean| >> std), where E[r^2] - mean^2 would cancel."""
     g = torch.Generator().manual_seed(sum(shape))
-    x = torch.randn(*shape, generator=g)
+    x = torch.randn(*shape, generator=g) + off * (1.0 + torch.rand(shape[1], generator=g))[None, :, None, None]
     gamma = torch.rand(shape[1], generator=g) + 0.5
     beta = torch.randn(shape[1], generator=g) * 0.1
     gy = torch.randn(*shape, generator=g)
@@ -487,3 +488,26 @@ def test_spline_scatter_bwd_matches_atomic(sd):
     # GEMM and the bf16 weight-gradient products: agreement at the bf16 ulp scale (2^-8)
     for a, b in zip(res["1"], res["0"]):
         assert _rel(a, b) < 1e-2
+
+
+def test_train_second_net_uses_its_own_weights():
+    """Two Nets trained one after the other in one process (the second from another seed, loaded
+    with load_state_dict, and one weight changed in place through ``.data``): each training
+    forward uses its own current SplineConv weights (the operand copies live for one step only)."""
+    pairs = synth.make_batch(24, 2, 32)
+    gt, n1, n2 = _gt(pairs)
+    for seed in (7, 8):
+        sdx = params.init_params(seed)
+        net = fpm.Net(regression=True, backbone=False, dtype="f32")
+        net.load_state_dict(sdx)
+        net.to(DEV).train()
+        for step in range(2):
+            if step == 1:      # in-place update that does not bump _version
+                p = dict(net.named_parameters())[params.SPLINE_PREFIX + ".0.weight"]
+                p.data.mul_(1.25)
+                sdx[params.SPLINE_PREFIX + ".0.weight"] = p.detach().cpu().clone()
+            out = net({"fpm_batch": DeviceBatch.from_pairs(pairs, DEV), "gt_perm_mat": gt, "label": torch.ones(2)})
+            (train.permutation_loss(out["ds_mat"], gt, n1, n2) + out["ks_loss"]).backward()
+            ref = O.forward(pairs, sdx, regression=True, training=True, gt_perm=gt, labels=torch.ones(2))
+            assert (net.last_outputs["ss"].detach().cpu() - ref["ss"].detach()).abs().max() < 1e-4, (seed, step)
+        del net
