@@ -111,6 +111,7 @@ def parity_vs_oracle(pairs, ref, sd, dev, dtypes):
     at 1e-4, bf16 reported).  Checker only: runs after the timed region."""
     import torch
     import fpm
+    import oracle as O
     from fpm.batch import DeviceBatch
     out = {}
     for dt in dtypes:
@@ -125,9 +126,36 @@ def parity_vs_oracle(pairs, ref, sd, dev, dtypes):
         d["perm_pairs_identical"] = float(np.mean([torch.equal(P[b], R[b]) for b in range(P.shape[0])]))
         d["perm_pairs_tie_equivalent"] = float(np.mean([tie_equivalent(P[b], R[b], ref["ds_mat"][b])
                                                         for b in range(P.shape[0])]))
+        # pair-by-pair class of every perm_mat difference (oracle.compare: select / LSA near-tie,
+        # k* rounding crossing, or unexplained mismatch)
+        rep = O.compare.perm_report(res, ref, [p[0]["n"] for p in pairs], [p[1]["n"] for p in pairs])
+        d["perm_classes"] = rep["counts"]
         out[dt] = d
     out["pairs"] = len(pairs)
     return out
+
+
+def timed_batch_selfcheck(net, bt, res):
+    """The timed batch's own outputs against per-pair solo runs (the reference's forward loops
+    pair by pair, ngm.py:326-361, so a pair's row must not depend on the batch around it): pair 0,
+    the first pair of every pipeline chunk (incl. the halved tail chunks), the middle pair of the
+    last chunk and the last pair, each re-run alone (one chunk, the batch's padded sizes) after the
+    timed region and compared bit for bit with its row of the timed forward's outputs."""
+    import torch
+    K = net.pipeline_chunks(bt.B)
+    parts = bt.split(K, net.tail_splits if K > 1 else 0, net.head_splits if K > 1 else 0)
+    ranges = [p.pair_range if hasattr(p, "pair_range") else (0, bt.B) for p in parts]
+    idx = sorted({0, bt.B - 1, (ranges[-1][0] + ranges[-1][1] - 1) // 2} | {r[0] for r in ranges})
+    keys = ("s", "ss", "ds_mat", "perm_mat", "k_prob", "cls_prob")
+    bad = []
+    for b in idx:
+        solo = net.run(bt.split_range(b, b + 1), chunks=1)
+        for k in keys:
+            if not torch.equal(solo[k][0], res[k][b]):
+                bad.append((b, k))
+    torch.cuda.synchronize()
+    return {"identical": not bad, "pairs_checked": idx, "chunks": [list(r) for r in ranges],
+            "outputs": list(keys), "mismatches": bad[:16]}
 
 
 def bench_graph_build(kp, bt, dev, args):
@@ -177,8 +205,8 @@ T0 = time.perf_counter()
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1024, help="pairs per GPU")
     ap.add_argument("--n", type=int, default=256, help="keypoints per graph")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
@@ -270,6 +298,8 @@ def main():
     lib = _lib.load()
     import ctypes
 
+    last = {}       # each timed loop's final outputs (kept for the self-check after the timing)
+
     def timed(model, batch, steps, tag):
         """``steps`` forwards bracketed by barrier + synchronize -> (wall s, gpu-stage s, lsa s)."""
         g_s = l_s = 0.0
@@ -277,7 +307,7 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
-            model.run(batch)
+            last[tag] = model.run(batch)
             lt = model.last_timing
             g_s += lt["gpu_stage_s"]
             l_s += lt["lsa_s"]
@@ -313,6 +343,12 @@ def main():
     lib.fpm_profile_enable(0)
     net.n_streams = saved_streams
     _lib.call("fpm_profile_read", ctypes.byref(iso_ms), ctypes.byref(iso_fl), ctypes.byref(iso_cnt))
+    # the timed batch's rows against per-pair solo runs (after every timing of this rank)
+    selfcheck = timed_batch_selfcheck(net, bt, last[""])
+    log("timed-batch self-check: %s" % json.dumps(selfcheck))
+    if not selfcheck["identical"]:
+        raise SystemExit("bench: timed batch differs from per-pair solo runs: %s" % selfcheck["mismatches"])
+    del last[""]
     elapsed, gpu_s, lsa_s, elapsed_prof = reduce_max([elapsed, gpu_s, lsa_s, elapsed_prof], world)
     pairs_total = (args.gallery if args.config == "c4" else args.batch * world) * args.steps
     value = pairs_total / elapsed
@@ -415,6 +451,8 @@ def main():
             "value_profiled": pairs_total / elapsed_prof,
             "cpu_baseline": cpu,
             "parity_vs_oracle": parity,
+            "timed_batch_selfcheck": selfcheck["identical"],
+            "timed_batch_selfcheck_detail": {k: selfcheck[k] for k in ("pairs_checked", "chunks", "outputs")},
             "f32_line": f32_line,
             "strong_scaling": strong,
             "ranks_share_devices": shared_devices,

@@ -76,6 +76,7 @@ SIGNATURES = {
     "fpm_kron_pattern": (I, [P, P, L, P, P, L, I, I, I, I, P, P, P]),
     "fpm_feature_align_ws_floats": (L, [P, P]),
     "fpm_feature_align_fwd": (I, [P, P, P, P, P, P, P, P, I, F, F, P, P, L, P, P]),
+    "fpm_feature_align_bwd": (I, [P, P, P, P, P, P, P, P, I, F, F, P, P, L, P, P, P, P, P, P]),
     "fpm_sinkhorn_bwd_ws_floats": (L, [I, I, I, I]),
     "fpm_sinkhorn_log_bwd": (I, [P, L, L, L, P, L, L, L, P, P, P, I, I, I, I, F, I, P, L, P]),
     "fpm_soft_topk_bwd_ws_floats": (L, [I, I, I]),

@@ -146,6 +146,118 @@ __global__ void global_maxpool_kernel(Map m, int B, float* __restrict__ w) {
     w[t] = v;
 }
 
+// ---- backward (train.py stages 1 / 3 / 5 train the backbone through this stage) ----------------
+// Per map and image pixel, one workgroup: the keypoints whose bilinear corners hit the pixel are
+// found by recomputing every keypoint's corners exactly as the forward does (fixed keypoint order,
+// a pixel's weights of one keypoint summed over its corners q = a, b, c, d), then
+//   dy[c]  = sum_i w_i(pixel) * dX[i][off + c]                 (transpose of the gather)
+//   dx[c]  = (dy[c] - y[c] * sum_c' y[c'] dy[c']) / |x|        (y = x / |x|, normalize_over_channels)
+// written once per (image, channel, pixel) -- no atomics.  The global max-pool's gradient is added
+// afterwards by global_maxpool_bwd_kernel at each (image, channel)'s first maximum (torch's
+// AdaptiveMaxPool2d index rule, NaN last-wins like the forward).
+constexpr int FB_T = 256;
+
+__global__ __launch_bounds__(FB_T) void feature_align_bwd_kernel(Map m, Map g, const float* __restrict__ nrm,
+                                                                 const float* __restrict__ P,
+                                                                 const int* __restrict__ nv, int nmax, float ox,
+                                                                 float oy, const float* __restrict__ dX, long ldx,
+                                                                 int coff) {
+    extern __shared__ float wl[];                 // nmax weights, then the compact hit list
+    __shared__ float red[FB_T / 64];
+    __shared__ int nhit;
+    const int HW = m.H * m.W;
+    const long b = blockIdx.x / HW;
+    const int pix = (int)(blockIdx.x - b * HW);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int n = nv[b];
+    for (int i = tid; i < n; i += FB_T) {
+        float x, y;
+        to_map(P[(b * nmax + i) * 2], P[(b * nmax + i) * 2 + 1], ox, oy, m.H, m.W, x, y);
+        const Corner c = corners(x, y, m.H, m.W);
+        float w = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (c.off[q] == pix) w += c.w[q];
+        // hits are flagged by the corner test, not by w != 0 (a zero weight still indexes the pixel)
+        bool hit = c.off[0] == pix || c.off[1] == pix || c.off[2] == pix || c.off[3] == pix;
+        wl[i] = hit ? w : __int_as_float(0x7fc00001);   // a NaN payload marks "no hit"
+    }
+    __syncthreads();
+    // compact (keypoint, weight) pairs in ascending keypoint order (wave 0)
+    int* hid = (int*)(wl + nmax);
+    float* hw = (float*)(hid + nmax);
+    if (tid < 64) {
+        int cnt = 0;
+        for (int i0 = 0; i0 < n; i0 += 64) {
+            const int i = i0 + lane;
+            const float w = i < n ? wl[i] : 0.f;
+            const bool h = i < n && __float_as_int(w) != 0x7fc00001;
+            const unsigned long long bal = __ballot(h);
+            if (h) {
+                const int slot = cnt + __popcll(bal & ((1ull << lane) - 1ull));
+                hid[slot] = i;
+                hw[slot] = w;
+            }
+            cnt += __popcll(bal);
+        }
+        if (lane == 0) nhit = cnt;
+    }
+    __syncthreads();
+    const int nh = nhit;
+    const float inv = 1.f / nrm[b * HW + pix];
+    const int yy = pix / m.W, xx = pix - yy * m.W;
+    const float* xp = m.p + b * m.sb + (long)yy * m.sh + (long)xx * m.sw;
+    float* gp = (float*)g.p + b * g.sb + (long)yy * g.sh + (long)xx * g.sw;
+    constexpr int CPT = 2;                       // channels per thread (C <= 512)
+    float dy[CPT], yv[CPT];
+    float dot = 0.f;
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+        const int ch = tid + k * FB_T;
+        dy[k] = 0.f;
+        yv[k] = 0.f;
+        if (ch < m.C) {
+            float a = 0.f;
+            for (int h = 0; h < nh; ++h) a = fmaf(hw[h], dX[(b * nmax + hid[h]) * ldx + coff + ch], a);
+            dy[k] = a;
+            yv[k] = xp[(long)ch * m.sc] * inv;
+            dot = fmaf(yv[k], a, dot);
+        }
+    }
+    dot = fpm::warp_sum(dot);
+    if (lane == 0) red[tid >> 6] = dot;
+    __syncthreads();
+    dot = 0.f;
+#pragma unroll
+    for (int w = 0; w < FB_T / 64; ++w) dot += red[w];
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+        const int ch = tid + k * FB_T;
+        if (ch < m.C) gp[(long)ch * g.sc] = (dy[k] - yv[k] * dot) * inv;
+    }
+}
+
+__global__ void global_maxpool_bwd_kernel(Map m, Map g, int B, const float* __restrict__ dw) {
+    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (long)B * m.C) return;
+    const long b = t / m.C;
+    const int c = (int)(t - b * m.C);
+    const float* base = m.p + b * m.sb + (long)c * m.sc;
+    float v = -INFINITY;
+    int arg = 0, k = 0;
+    for (int y = 0; y < m.H; ++y)
+        for (int x = 0; x < m.W; ++x, ++k) {
+            const float u = base[(long)y * m.sh + (long)x * m.sw];
+            if (u > v || u != u) {
+                v = u;
+                arg = k;
+            }
+        }
+    const int y = arg / m.W, x = arg - (arg / m.W) * m.W;
+    float* gp = (float*)g.p + b * g.sb + (long)c * g.sc + (long)y * g.sh + (long)x * g.sw;
+    *gp += dw[t];
+}
+
 Map make_map(const float* p, const long* shape, const long* stride) {
     Map m;
     m.p = p;
@@ -190,4 +302,38 @@ extern "C" int fpm_feature_align_fwd(const float* nodes, const long* node_shape,
         hipLaunchKernelGGL(global_maxpool_kernel, dim3((unsigned)(((long)B * me.C + 255) / 256)), dim3(256), 0, st,
                            me, B, wglob);
     return fpm::check_launch("fpm_feature_align_fwd");
+}
+
+// Backward of fpm_feature_align_fwd: dX (B*nmax, ldx) and dwglob (B, C_edges, may be NULL) ->
+// dnodes / dedges, gradients w.r.t. the raw CNN maps (same shapes; own strides).  ws: the forward's
+// workspace (pixel norms, unchanged since the forward).  Every element of dnodes / dedges is written.
+extern "C" int fpm_feature_align_bwd(const float* nodes, const long* node_shape, const long* node_stride,
+                                     const float* edges, const long* edge_shape, const long* edge_stride,
+                                     const float* P, const int* n, int nmax, float ori_w, float ori_h,
+                                     const float* ws, const float* dX, long ldx, const float* dwglob, float* dnodes,
+                                     const long* dnode_stride, float* dedges, const long* dedge_stride,
+                                     void* stream) {
+    FPM_CHECK_ARG(node_shape[0] == edge_shape[0], "feature_align_bwd: node/edge maps disagree on the batch size");
+    FPM_CHECK_ARG(node_shape[1] <= 2 * FB_T && edge_shape[1] <= 2 * FB_T, "feature_align_bwd: at most %d channels",
+                  2 * FB_T);
+    FPM_CHECK_ARG(ldx >= node_shape[1] + edge_shape[1], "feature_align_bwd: ldx < C_nodes + C_edges");
+    FPM_CHECK_ARG(nmax >= 0 && nmax <= 4096, "feature_align_bwd: nmax must be <= 4096");
+    const int B = (int)node_shape[0];
+    if (B == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    const Map mn = make_map(nodes, node_shape, node_stride);
+    const Map me = make_map(edges, edge_shape, edge_stride);
+    const Map gn = make_map(dnodes, node_shape, dnode_stride);
+    const Map ge = make_map(dedges, edge_shape, dedge_stride);
+    const float* nn_ = ws;
+    const float* ne_ = ws + (long)B * mn.H * mn.W;
+    const size_t lds = (size_t)(nmax > 0 ? nmax : 1) * 3 * sizeof(float);
+    hipLaunchKernelGGL(feature_align_bwd_kernel, dim3((unsigned)((long)B * mn.H * mn.W)), dim3(FB_T), lds, st, mn, gn,
+                       nn_, P, n, nmax, ori_w, ori_h, dX, ldx, 0);
+    hipLaunchKernelGGL(feature_align_bwd_kernel, dim3((unsigned)((long)B * me.H * me.W)), dim3(FB_T), lds, st, me, ge,
+                       ne_, P, n, nmax, ori_w, ori_h, dX, ldx, mn.C);
+    if (dwglob)
+        hipLaunchKernelGGL(global_maxpool_bwd_kernel, dim3((unsigned)(((long)B * me.C + 255) / 256)), dim3(256), 0, st,
+                           me, ge, B, dwglob);
+    return fpm::check_launch("fpm_feature_align_bwd");
 }

@@ -741,17 +741,25 @@ class Net(nn.Module):
                 m.to(device=dev, memory_format=torch.channels_last)
             self._backbone_dev = dev
         xs, gs = [], []
+        # train mode with autograd on (train.py): the backbone runs under autograd and the align
+        # stage has its HIP backward (fpm.train.FeatureAlignFn); inference: no graph
+        grad = self.training and torch.is_grad_enabled()
         for img, pts, n in zip(images, Ps, ns):
             img = torch.as_tensor(img)
             if img.dim() == 3:
                 img = img.unsqueeze(0)
             img = img.to(device=dev, dtype=torch.float32).contiguous(memory_format=torch.channels_last)
-            with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.dtype_mode == "bf16"):
+            with torch.set_grad_enabled(grad), torch.autocast("cuda", dtype=torch.bfloat16,
+                                                               enabled=self.dtype_mode == "bf16"):
                 nodes = self.node_layers(img)
                 edges = self.edge_layers(nodes)
             pts = torch.as_tensor(pts).to(device=dev, dtype=torch.float32)
             n32 = torch.as_tensor(n).view(-1).to(device=dev, dtype=torch.int32)
-            x, g = ops.feature_align(nodes.float(), edges.float(), pts, n32, ori_size=C.RESCALE)
+            if grad:
+                from .train import FeatureAlignFn
+                x, g = FeatureAlignFn.apply(nodes.float(), edges.float(), pts.contiguous(), n32, C.RESCALE)
+            else:
+                x, g = ops.feature_align(nodes.float(), edges.float(), pts, n32, ori_size=C.RESCALE)
             xs.append(x)
             gs.append(g)
         return xs, gs

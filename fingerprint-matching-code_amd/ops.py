@@ -295,10 +295,11 @@ def match_cls(s, perm, w1, b1, bn1_sc, bn1_sh, w2, b2, bn2_sc, bn2_sh, fcw, fcb,
     return logits, prob
 
 
-def feature_align(nodes, edges, P, n, nmax=None, ori_size=(320.0, 240.0), out=None, wglob=None):
+def feature_align(nodes, edges, P, n, nmax=None, ori_size=(320.0, 240.0), out=None, wglob=None, keep_ws=False):
     """Normalise both CNN maps over channels, bilinear-gather them at the keypoints
     (utils/feature_align.py) and concatenate -> X (B*nmax, C_n + C_e) fp32 with zero padding rows;
-    also the global max-pooled edge feature (B, C_e).  Maps may be NCHW or channels_last."""
+    also the global max-pooled edge feature (B, C_e).  Maps may be NCHW or channels_last.
+    ``keep_ws``: also return the workspace (pixel norms) for feature_align_bwd."""
     _dev(nodes, edges, P, n)
     for t in (nodes, edges, P):
         if t.dtype != torch.float32:
@@ -321,7 +322,31 @@ def feature_align(nodes, edges, P, n, nmax=None, ori_size=(320.0, 240.0), out=No
     ws = torch.empty(int(lib.fpm_feature_align_ws_floats(ns_, es_)), dtype=torch.float32, device=nodes.device)
     _lib.call("fpm_feature_align_fwd", _p(nodes), ns_, nst, _p(edges), es_, est, _p(P), _p(n), nmax,
               float(ori_size[0]), float(ori_size[1]), _p(ws), _p(out), int(out.stride(0)), _p(wglob), _stream(nodes))
-    return out, wglob
+    return (out, wglob, ws) if keep_ws else (out, wglob)
+
+
+def feature_align_bwd(nodes, edges, P, n, ws, dX, dwglob=None, ori_size=(320.0, 240.0)):
+    """Backward of feature_align: gradients of X rows (and of the global feature) -> gradients of
+    the raw maps (dnodes, dedges), allocated with the maps' memory formats."""
+    _dev(nodes, edges, P, n, ws, dX)
+    B = int(nodes.shape[0])
+    nmax = int(P.shape[1])
+    Cn, Ce = int(nodes.shape[1]), int(edges.shape[1])
+    if dX.dtype != torch.float32 or dX.dim() != 2 or dX.shape[0] != B * nmax or dX.shape[1] < Cn + Ce or dX.stride(1) != 1:
+        raise _lib.FpmError("feature_align_bwd: dX must be (B*nmax, >= C_n + C_e) float32 rows")
+    if dwglob is not None:
+        _shape(dwglob, (B, Ce), "feature_align_bwd dwglob")
+        dwglob = dwglob.contiguous().float()
+    P = P.contiguous()
+    fmt = lambda t: torch.channels_last if t.is_contiguous(memory_format=torch.channels_last) and not t.is_contiguous() \
+        else torch.contiguous_format
+    dn = torch.empty_like(nodes, memory_format=fmt(nodes))
+    de = torch.empty_like(edges, memory_format=fmt(edges))
+    arr = lambda v: ctypes.cast((ctypes.c_long * 4)(*[int(x) for x in v]), ctypes.c_void_p)
+    _lib.call("fpm_feature_align_bwd", _p(nodes), arr(nodes.shape), arr(nodes.stride()), _p(edges), arr(edges.shape),
+              arr(edges.stride()), _p(P), _p(n), nmax, float(ori_size[0]), float(ori_size[1]), _p(ws), _p(dX),
+              int(dX.stride(0)), _p(dwglob), _p(dn), arr(dn.stride()), _p(de), arr(de.stride()), _stream(nodes))
+    return dn, de
 
 
 def lsa_batch_device(s, n1, n2, assign=None, status=None):
@@ -583,3 +608,4 @@ def memcpy_async(dst, src, kind=2):
         raise _lib.FpmError("memcpy_async: host destination must be pinned")
     _lib.call("fpm_memcpy_async", _p(dst), _p(src), src.numel() * src.element_size(), int(kind), _stream(src))
     return dst
+

@@ -21,7 +21,8 @@ same HIP forward kernels as inference and has a hand-written backward:
 The MatchClassifier runs as torch conv / batch-norm (MIOpen) in train mode (batch statistics,
 running buffers updated), like the reference module.  The Hungarian + greedy selection carry no
 gradient (``perm_mat`` is a constant mask of ``s``, ngm.py:444-453).  Gradients reach every
-parameter of the matcher and the node / global feature rows; the backbone is not trained here.
+parameter of the matcher and the node / global feature rows; with images in the data_dict the
+backbone (MIOpen convolutions under autograd) trains through ``FeatureAlignFn``'s HIP backward.
 """
 import os
 
@@ -514,6 +515,29 @@ def match_cls_train(m, P_, B_):
         x = F.max_pool2d(x, 2)
     x = F.adaptive_avg_pool2d(x, 1).view(x.shape[0], -1)
     return F.linear(x, P_("match_cls.fc.weight"), P_("match_cls.fc.bias")).squeeze(-1)
+
+
+class FeatureAlignFn(torch.autograd.Function):
+    """normalize_over_channels + feature_align + concat_features + the global max-pool
+    (ngm.py:235-248, utils/feature_align.py:5-126) on fpm_feature_align_fwd, with its hand-written
+    backward (fpm_feature_align_bwd) so the backbone trains through the node features and the
+    global weights (train.py stages 1, 3 and 5 update node_layers / edge_layers)."""
+
+    @staticmethod
+    def forward(ctx, nodes, edges, P, n, ori_size):
+        nc, ec = nodes.detach(), edges.detach()
+        X, wg, ws = ops.feature_align(nc, ec, P, n, ori_size=ori_size, keep_ws=True)
+        ctx.save_for_backward(nc, ec, P, n, ws)
+        ctx.ori_size = ori_size
+        return X, wg
+
+    @staticmethod
+    def backward(ctx, dX, dwg):
+        nodes, edges, P, n, ws = ctx.saved_tensors
+        if dX is None:
+            dX = torch.zeros(P.shape[0] * P.shape[1], nodes.shape[1] + edges.shape[1], device=nodes.device)
+        dn, de = ops.feature_align_bwd(nodes, edges, P, n, ws, dX.contiguous().float(), dwg, ori_size=ctx.ori_size)
+        return dn, de, None, None, None
 
 
 class _GnnCtx:

@@ -321,6 +321,17 @@ long fpm_feature_align_ws_floats(const long* node_shape, const long* edge_shape)
 int fpm_feature_align_fwd(const float* nodes, const long* node_shape, const long* node_stride, const float* edges,
                           const long* edge_shape, const long* edge_stride, const float* P, const int* n, int nmax,
                           float ori_w, float ori_h, float* ws, float* X, long ldx, float* wglob, void* stream);
+/* Its backward (train.py stages 1 / 3 / 5 train the backbone through this stage, ngm.py:235-251):
+ * dX (B*nmax, ldx) and dwglob (B, C_edges, may be NULL) -> dnodes / dedges (the maps' shapes, own
+ * element strides), every element written: transpose of the bilinear gather (keypoints found per
+ * pixel in a fixed order, no atomics), the channel-norm backward, and the global max-pool gradient
+ * at each (image, channel)'s first maximum.  ws: the forward's workspace (pixel norms); nmax <= 4096,
+ * C_nodes, C_edges <= 512. */
+int fpm_feature_align_bwd(const float* nodes, const long* node_shape, const long* node_stride, const float* edges,
+                          const long* edge_shape, const long* edge_stride, const float* P, const int* n, int nmax,
+                          float ori_w, float ori_h, const float* ws, const float* dX, long ldx, const float* dwglob,
+                          float* dnodes, const long* dnode_stride, float* dedges, const long* dedge_stride,
+                          void* stream);
 
 /* ---- profiling hooks: HIP-event timing of the dominant kernel (edge-message GEMM) ------------ */
 int fpm_profile_enable(int on);

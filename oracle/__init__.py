@@ -19,3 +19,4 @@ factorised SAGE-mean vs the reference's explicit Kronecker pattern).
 from .ngm_oracle import *  # noqa: F401,F403
 from . import graphs_oracle  # noqa: F401,E402
 from . import frontend_oracle  # noqa: F401,E402
+from . import compare  # noqa: F401,E402

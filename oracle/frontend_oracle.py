@@ -45,12 +45,14 @@ def feature_align(raw_feature, P, ns, ori_size=(320, 240)):
     """feature_align.py:5-68 -> (b, c, n_max), zeros past ns[b]."""
     b, c = raw_feature.shape[:2]
     n_max = P.shape[1]
-    ori = torch.tensor(ori_size, dtype=torch.float32)
-    F = torch.zeros(b, c, n_max, dtype=torch.float32)
+    dev = raw_feature.device               # feature_align.py:23-24: output on the input's device
+    ori = torch.tensor(ori_size, dtype=torch.float32, device=dev)
+    F = torch.zeros(b, c, n_max, dtype=raw_feature.dtype, device=dev)
+    P = P.to(dev)
     for idx in range(b):
         n = int(ns[idx])
         feat = raw_feature[idx]
-        fs = torch.as_tensor(feat.shape[1:3], dtype=torch.float32)
+        fs = torch.as_tensor(feat.shape[1:3], dtype=torch.float32, device=dev)
         step = ori / fs
         p = (P[idx, :n].float() - step / 2) / ori * fs
         F[idx, :, :n] = bilinear_points(feat, p[:, 0], p[:, 1])

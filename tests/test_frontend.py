@@ -55,6 +55,13 @@ def test_backbone_layout_and_shapes():
 DEV = torch.device("cuda", 0)
 
 
+@pytest.fixture
+def deterministic_convs():
+    """Ask the library convolutions for deterministic algorithms where they have them."""
+    with torch.backends.cudnn.flags(enabled=True, benchmark=False, deterministic=True):
+        yield
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("channels_last", [False, True])
 def test_feature_align_kernel_golden(channels_last):
@@ -158,3 +165,159 @@ def test_images_to_match_forward():
     for r in (ref, out):
         assert (r["ds_mat"].cpu() - orc["ds_mat"]).abs().max() < 1e-4
         assert (r["k_prob"].cpu() - orc["k_prob"]).abs().max() < 2e-4
+
+
+def _align_case(seed, B, n, Cn=256, Ce=512, hn=(15, 20), he=(8, 10)):
+    """Random maps + keypoints incl. the frame's borders (the clamped-corner branch)."""
+    g = torch.Generator().manual_seed(seed)
+    nodes = torch.randn(B, Cn, *hn, generator=g, dtype=torch.float64)
+    edges = torch.relu(torch.randn(B, Ce, *he, generator=g, dtype=torch.float64))
+    P = torch.zeros(B, n, 2, dtype=torch.float32)
+    ns = []
+    for b in range(B):
+        m = n - 3 * b
+        P[b, :m, 0] = torch.rand(m, generator=g) * 320
+        P[b, :m, 1] = torch.rand(m, generator=g) * 240
+        P[b, 0] = torch.tensor([0.0, 0.0])          # corners / edges of the frame
+        P[b, 1] = torch.tensor([319.9, 239.9])
+        P[b, 2] = torch.tensor([3.0, 120.0])
+        ns.append(m)
+    return nodes, edges, P, torch.tensor(ns)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("channels_last", [False, True])
+@pytest.mark.parametrize("case", ["golden", "c3"])
+def test_feature_align_bwd_vs_autograd(channels_last, case):
+    """fpm_feature_align_bwd (transpose of the bilinear gather, channel-norm backward, global
+    max-pool gradient) against float64 autograd through the oracle front end (frontend_oracle,
+    pinned by feature_align.npz) on the same fp32 maps: dnodes / dedges within 1e-5 of their scale."""
+    from fpm import ops
+    if case == "golden":
+        z = _golden()
+        nodes, edges, P, ns = z["nodes"].double(), z["edges"].double(), z["P"].float(), z["ns"]
+    else:
+        nodes, edges, P, ns = _align_case(4, 3, 48)
+    nodes, edges = nodes.float().double(), edges.float().double()
+    B, nmax = P.shape[:2]
+    C = nodes.shape[1] + edges.shape[1]
+    g = torch.Generator().manual_seed(77)
+    dX = torch.randn(B, nmax, C, generator=g, dtype=torch.float64)
+    dG = torch.randn(B, edges.shape[1], generator=g, dtype=torch.float64)
+    nl, el = nodes.clone().requires_grad_(True), edges.clone().requires_grad_(True)
+    X, G = FO.image_features(nl, el, P, ns)
+    ((X * dX).sum() + (G * dG).sum()).backward()
+    mf = torch.channels_last if channels_last else torch.contiguous_format
+    nd = nodes.float().to(DEV).contiguous(memory_format=mf)
+    ed = edges.float().to(DEV).contiguous(memory_format=mf)
+    n32 = ns.to(torch.int32).to(DEV)
+    Xd, Gd, ws = ops.feature_align(nd, ed, P.to(DEV), n32, keep_ws=True)
+    dn, de = ops.feature_align_bwd(nd, ed, P.to(DEV), n32, ws, dX.float().reshape(B * nmax, C).to(DEV),
+                                   dG.float().to(DEV))
+    assert dn.is_contiguous(memory_format=mf) and de.is_contiguous(memory_format=mf)
+    for got, ref in ((dn, nl.grad), (de, el.grad)):
+        err = float((got.cpu().double() - ref).abs().max() / ref.abs().max())
+        assert err < 1e-5, err
+
+
+@pytest.mark.gpu
+def test_backbone_gradient_through_align_vs_oracle_front_end(deterministic_convs):
+    """The backbone's parameter gradients through FeatureAlignFn (HIP forward + backward) against
+    the same MIOpen backbone through the oracle's torch front end under autograd, for the same
+    upstream gradients of the node rows and the global feature: within 1e-4 of each tensor's
+    gradient scale (the two differ in the align stage's backward only)."""
+    import fpm
+    from fpm import train
+    net = fpm.Net(regression=True, backbone=True)
+    net.to(DEV).train()
+    B, n = 2, 40
+    imgs, Ps, ns = _image_batch(B, n, 13)
+    img = imgs[0].to(DEV).contiguous(memory_format=torch.channels_last)
+    g = torch.Generator().manual_seed(3)
+    dX = torch.randn(B, n, 768, generator=g).to(DEV)
+    dG = torch.randn(B, 512, generator=g).to(DEV)
+    bb = [(k, p) for k, p in net.named_parameters() if k.startswith(("node_layers", "edge_layers"))]
+    state = {k: v.clone() for k, v in net.state_dict().items()}
+    grads = []
+    for path in ("hip", "oracle", "hip"):
+        net.load_state_dict(state)
+        net.zero_grad(set_to_none=True)
+        nodes = net.node_layers(img)
+        edges = net.edge_layers(nodes)
+        if path == "hip":
+            X, G = train.FeatureAlignFn.apply(nodes, edges, Ps[0].to(DEV), ns[0].to(torch.int32).to(DEV), (320.0, 240.0))
+            X = X.view(B, n, -1)
+        else:
+            X, G = FO.image_features(nodes, edges, Ps[0].to(DEV), ns[0])
+        ((X * dX).sum() + (G * dG).sum()).backward()
+        grads.append({k: p.grad.clone() for k, p in bb})
+    # the library convolutions' weight-gradient reductions are not bitwise reproducible: two runs
+    # of the same path spread by `noise`; the HIP and oracle paths must agree within that (or 1e-4)
+    for k, _ in bb:
+        ref = grads[1][k]
+        scale = ref.abs().max().clamp(min=1e-30)
+        err = float((grads[0][k] - ref).abs().max() / scale)
+        noise = float((grads[0][k] - grads[2][k]).abs().max() / scale)
+        assert err < max(1e-4, 3.0 * noise), (k, err, noise)
+
+
+@pytest.mark.gpu
+def test_train_backbone_gradient_end_to_end(deterministic_convs):
+    """train.py stages 1 / 3 / 5: Net.forward in train mode on images (backbone under autograd,
+    FeatureAlignFn, the matcher's HIP backward) gives every node_layers / edge_layers parameter a
+    finite, non-zero gradient equal (1e-4 of each tensor's scale) to the run whose node rows are
+    differentiated through the oracle's torch front end instead.  Run 2 feeds the matcher the HIP
+    rows' values with the oracle rows' gradient path (x_hip + (x_oracle - x_oracle.detach())), so
+    both runs see bit-identical matcher inputs: the tau = 0.01 Sinkhorn backwards would otherwise
+    amplify the ~1e-7 difference of the two front ends' forward values to ~1e-2."""
+    import fpm
+    from fpm import params, train
+    net = fpm.Net(regression=True, backbone=True)
+    net.load_state_dict({**net.state_dict(), **params.init_params(5)})
+    net.to(DEV).train()
+    B, n = 2, 32
+    imgs, Ps, ns = _image_batch(B, n, 11)
+    gt = torch.zeros(B, n, n)
+    for b in range(B):
+        m = min(int(ns[0][b]), int(ns[1][b]))
+        gt[b, torch.arange(m), torch.arange(m)] = 1.0
+    n1, n2 = ns[0].tolist(), ns[1].tolist()
+
+    def loss_of(out):
+        # PermutationLoss + ks_loss (the classifier's perm mask is discrete: left out so both runs
+        # see exactly the same differentiable graph)
+        return train.permutation_loss(out["ds_mat"], gt, n1, n2) + out["ks_loss"]
+
+    bb = [(k, p) for k, p in net.named_parameters() if k.startswith(("node_layers", "edge_layers"))]
+    state = {k: v.clone() for k, v in net.state_dict().items()}
+    runs = []
+    for _ in range(2):          # twice: the library convolutions' run-to-run spread (`noise`)
+        net.zero_grad(set_to_none=True)
+        net.load_state_dict(state)
+        out = net({"images": imgs, "Ps": Ps, "ns": ns, "gt_perm_mat": gt})
+        loss_of(out).backward()
+        runs.append({k: p.grad.clone() for k, p in bb})
+    got = runs[0]
+    for k, gr in got.items():
+        assert torch.isfinite(gr).all() and gr.abs().max() > 0, k
+    net.zero_grad(set_to_none=True)
+    net.load_state_dict(state)                     # same BatchNorm running buffers as run 1
+    xs, gs = [], []
+    for side in range(2):
+        img = imgs[side].to(DEV).contiguous(memory_format=torch.channels_last)
+        nodes = net.node_layers(img)
+        edges = net.edge_layers(nodes)
+        X, G = FO.image_features(nodes.float(), edges.float(), Ps[side].to(DEV), ns[side])
+        with torch.no_grad():
+            Xh, Gh = net.image_features([imgs[side]], [Ps[side]], [ns[side]], DEV)
+        xs.append(Xh[0].view_as(X) + (X - X.detach()))
+        gs.append(Gh[0] + (G - G.detach()))
+    out2 = net({"node_features": xs, "global_features": gs, "Ps": Ps, "ns": ns, "gt_perm_mat": gt})
+    print("ds_mat run1 vs run2", float((out2["ds_mat"] - out["ds_mat"]).abs().max()))
+    assert (out2["ds_mat"] - out["ds_mat"]).abs().max() < 1e-6
+    loss_of(out2).backward()
+    for k, p in bb:
+        scale = p.grad.abs().max().clamp(min=1e-30)
+        err = float((got[k] - p.grad).abs().max() / scale)
+        noise = float((got[k] - runs[1][k]).abs().max() / scale)
+        assert err < max(1e-4, 3.0 * noise), (k, err, noise)

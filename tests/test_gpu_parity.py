@@ -254,11 +254,77 @@ def test_forward_no_regression_parity(sd):
     assert d["perm_equal"], d
 
 
+def _run_and_ref(pairs, sd, dtypes=("f32",), regression=True, bt=None):
+    """The device forward in each compute mode and the oracle on the same pairs."""
+    ref = O.forward(pairs, sd, regression=regression)
+    outs = {}
+    for dt in dtypes:
+        net = fpm.Net(regression=regression, backbone=False, dtype=dt)
+        net.load_state_dict(sd)
+        outs[dt] = net.run(bt if bt is not None else DeviceBatch.from_pairs(pairs, DEV))
+    return outs, ref
+
+
+def _perm_gate(res, ref, pairs, name):
+    """perm_mat against the oracle, pair by pair (oracle.compare): every pair identical or differing
+    only by a (near-)tie or a k* rounding-boundary crossing; the classes are recorded."""
+    n1 = [p[0]["n"] for p in pairs]
+    n2 = [p[1]["n"] for p in pairs]
+    rep = O.compare.perm_report(res, ref, n1, n2)
+    _record(name, {k: v for k, v in rep.items()})
+    assert rep["counts"]["mismatch"] == 0, rep
+    return rep
+
+
 def test_forward_n256_parity(sd):
-    """Benchmark graph size (C3's n=256) at a batch the CPU oracle finishes in seconds."""
-    d = _compare_forward(synth.make_batch(5, 2, 256), sd)
-    assert d["ss"] < 1e-4 and d["ds_mat"] < 1e-4 and d["k_prob"] < 1e-4, d
-    assert d["perm_equal"], d
+    """Benchmark graph size (C3's n=256), 16 pairs, fp32 mode vs the oracle: ss / ds_mat / k_prob
+    within 1e-4 and every pair's perm_mat identical or explained (tie / k* rounding; the identical
+    fraction is recorded).  The bf16 headline mode on the same pairs gets the bf16 gates."""
+    pairs = synth.make_batch(5, 16, 256)
+    outs, ref = _run_and_ref(pairs, sd, ("f32", "bf16"))
+    res = outs["f32"]
+    d = {k: float((res[k].float().cpu() - ref[k]).abs().max()) for k in ("ss", "ds_mat", "k_prob", "cls_prob")}
+    assert d["ss"] < 1e-4 and d["ds_mat"] < 1e-4 and d["k_prob"] < 1e-4 and d["cls_prob"] < 1e-4, d
+    _perm_gate(res, ref, pairs, "perm_report_n256_f32")
+    db = fidelity_stats(outs["bf16"], ref)
+    _record("bf16_fidelity_c3_16", db)
+    _bf16_gate(db)
+    _perm_gate(outs["bf16"], ref, pairs, "perm_report_n256_bf16")
+
+
+def test_forward_c2_parity(sd):
+    """SURVEY config C2 (n = 128, fp32 mode) vs the oracle: 1e-4 on ss / ds_mat / k_prob and
+    cls_prob, perm_mat explained pair by pair (ngm.py:479-487)."""
+    pairs = synth.make_batch(13, 6, 128)
+    outs, ref = _run_and_ref(pairs, sd, ("f32",))
+    res = outs["f32"]
+    d = {k: float((res[k].float().cpu() - ref[k]).abs().max()) for k in ("Kp", "ss", "ds_mat", "k_prob", "cls_prob")}
+    _record("c2_parity", d)
+    assert d["Kp"] < 1e-5 and d["ss"] < 1e-4 and d["ds_mat"] < 1e-4 and d["k_prob"] < 1e-4, d
+    assert d["cls_prob"] < 1e-4, d
+    _perm_gate(res, ref, pairs, "perm_report_c2")
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_forward_c4_probe_gallery_vs_oracle(sd, dtype):
+    """SURVEY config C4 (1 probe x gallery, n = 128; evaluate_binary_classifier.py:97): the
+    probe-shared batch (the probe's SplineConv computed once and broadcast) against the oracle
+    run on the expanded (probe, gallery_g) pairs: fp32 at 1e-4, bf16 under the bf16 gates."""
+    probe = synth.make_graph(17, 0, 0, 128)
+    gallery = [synth.make_graph(17, 1 + g, 1, 128 - (g % 3) * 5) for g in range(6)]
+    pairs = [(probe, g) for g in gallery]
+    bt = DeviceBatch.from_probe_gallery(probe, gallery, DEV)
+    outs, ref = _run_and_ref(pairs, sd, (dtype,), bt=bt)
+    res = outs[dtype]
+    if dtype == "f32":
+        d = {k: float((res[k].float().cpu() - ref[k]).abs().max()) for k in ("ss", "ds_mat", "k_prob", "cls_prob")}
+        _record("c4_parity_f32", d)
+        assert d["ss"] < 1e-4 and d["ds_mat"] < 1e-4 and d["k_prob"] < 1e-4 and d["cls_prob"] < 1e-4, d
+    else:
+        d = fidelity_stats(res, ref)
+        _record("c4_fidelity_bf16", d)
+        _bf16_gate(d)
+    _perm_gate(res, ref, pairs, "perm_report_c4_" + dtype)
 
 
 def _fidelity(pairs, sd, dtype="bf16"):
@@ -268,7 +334,7 @@ def _fidelity(pairs, sd, dtype="bf16"):
     net.load_state_dict(sd)
     res = net.run(DeviceBatch.from_pairs(pairs, DEV))
     ref = O.forward(pairs, sd, regression=True)
-    return fidelity_stats(res, ref)
+    return fidelity_stats(res, ref), res, ref
 
 
 def fidelity_stats(res, ref):
@@ -295,38 +361,48 @@ def _record(name, d):
     print(name, d)
 
 
+# bf16 mode vs the fp32 oracle: the largest deviations measured on the box by the fidelity tests
+# (round 2: n = 128 / 256 / 512 -> gpurun_out/bf16_fidelity_*.json) and the bench's 8-pair C3 sample
+BF16_MEASURED = {"Kp": 1.3e-5, "ss": 1.3e-6, "ds_mat": 3.6e-6, "k_prob": 8.7e-4, "cls_prob": 2.7e-5}
+
+
 def _bf16_gate(d):
     """Bounds for the bf16 throughput mode against the fp32 oracle (reported, with
-    these gates).  Measured on the box (round 2): Kp <= 1.3e-5, ss <= 1.3e-6, ds_mat
-    <= 3.3e-6, k_prob <= 7.8e-4, cls_prob <= 2.7e-5, perm_mat tie-equivalent on 7-8 of 8 pairs.
-    The gates leave ~5-10x room; a pair's perm_mat may differ from the oracle's only by picks
-    among (near-)tied soft top-k entries or by a k* that moved across a rounding boundary."""
-    assert d["Kp"] < 1e-4 and d["ss"] < 1e-5 and d["ds_mat"] < 5e-5, d
-    assert d["k_prob"] < 5e-3 and d["cls_prob"] < 2e-4, d
-    assert d["perm_matches_kept"] >= 0.97 and d["perm_pairs_tie_equivalent"] >= 0.5, d
+    these gates): 2x the largest deviation measured (BF16_MEASURED), and every pair's perm_mat
+    identical or tie-equivalent (a different pick among (near-)tied soft top-k entries) -- a k*
+    rounding crossing is judged by _perm_gate, which classifies pair by pair."""
+    for k, v in BF16_MEASURED.items():
+        assert d[k] < 2.0 * v, (k, d[k], 2.0 * v, d)
+    assert d["perm_matches_kept"] >= 0.98, d
 
 
 def test_forward_bf16_fidelity_n128(sd):
     """bf16 MFMA mode vs the fp32 oracle at n=128 (C2 size)."""
-    d = _fidelity(synth.make_batch(6, 2, 128), sd)
+    pairs = synth.make_batch(6, 2, 128)
+    d, res, ref = _fidelity(pairs, sd)
     _record("bf16_fidelity_n128", d)
     _bf16_gate(d)
+    _perm_gate(res, ref, pairs, "perm_report_bf16_n128")
 
 
 def test_forward_bf16_fidelity_c3(sd):
     """SURVEY §8(d) parity gate for the headline mode: bf16 at C3's graph size (n=256, B=4) vs the
     fp32 oracle, max|d| on ss / ds_mat / k_prob / cls_prob and perm_mat agreement, recorded and bounded."""
-    d = _fidelity(synth.make_batch(61, 4, 256), sd)
+    pairs = synth.make_batch(61, 4, 256)
+    d, res, ref = _fidelity(pairs, sd)
     _record("bf16_fidelity_c3", d)
     _bf16_gate(d)
+    _perm_gate(res, ref, pairs, "perm_report_bf16_c3")
 
 
 @pytest.mark.slow
 def test_forward_bf16_fidelity_c5(sd):
     """The same gate at C5's graph size (n=512, B=1)."""
-    d = _fidelity(synth.make_batch(62, 1, 512), sd)
+    pairs = synth.make_batch(62, 1, 512)
+    d, res, ref = _fidelity(pairs, sd)
     _record("bf16_fidelity_c5", d)
     _bf16_gate(d)
+    _perm_gate(res, ref, pairs, "perm_report_bf16_c5")
 
 
 def test_forward_data_dict_surface(sd):
@@ -855,3 +931,4 @@ def test_afau_head_and_nodecls_variants_bit_identical(sd):
         ops.set_tuning("nodecls_t", prev)
     for k in ("k_prob", "s", "ss", "ds_mat", "perm_mat"):
         assert torch.equal(r8[k], r1[k]), k
+
