@@ -107,12 +107,6 @@ int& gemm_phase_flag() {
 }
 }  // namespace fpm
 
-int& gnn_packed_flag();
-int& gnn_unroll_flag();
-int& gnn_group_flag();
-int& gnn_group1_flag();
-int& gnn_wide_flag();
-int& gnn_il_flag();
 int& nodecls_t_flag();
 int& plan_graph_flag();
 int& combine_npb_flag();
@@ -128,12 +122,6 @@ extern "C" int fpm_set_tuning(const char* key, int value) {
     if (key && !strcmp(key, "gemm_phase")) f = &fpm::gemm_phase_flag();
     else if (key && !strcmp(key, "gemm_persist")) f = &fpm::gemm_persist_flag();
     else if (key && !strcmp(key, "gemm_aff_big")) f = &fpm::gemm_aff_big_flag();
-    else if (key && !strcmp(key, "gnn_packed")) f = &gnn_packed_flag();
-    else if (key && !strcmp(key, "gnn_unroll")) f = &gnn_unroll_flag();
-    else if (key && !strcmp(key, "gnn_group")) f = &gnn_group_flag();
-    else if (key && !strcmp(key, "gnn_group1")) f = &gnn_group1_flag();
-    else if (key && !strcmp(key, "gnn_wide")) f = &gnn_wide_flag();
-    else if (key && !strcmp(key, "gnn_il")) f = &gnn_il_flag();
     else if (key && !strcmp(key, "nodecls_t")) f = &nodecls_t_flag();
     else if (key && !strcmp(key, "plan_graph")) f = &plan_graph_flag();
     else if (key && !strcmp(key, "combine_npb")) f = &combine_npb_flag();

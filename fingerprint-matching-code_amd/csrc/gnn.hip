@@ -2,17 +2,21 @@
 // sparse Kronecker pattern built at ngm.py:326-344) without materialising the pattern.
 //
 // torch_sparse mean aggregation over {Kronecker edge pairs} U {diagonal} factorises exactly:
-//   agg[c][d][i] = ( sum_{a in N1(i)} sum_{b in N2(d)} X[c][b][a] + D[d][i] X[c][d][i] )
+//   agg[c][d][i] = ( sum_{a in N1(i)} sum_{e in N2(d)} X[c][e][a] + D[d][i] X[c][d][i] )
 //                  / ( deg1(i) deg2(d) + D[d][i] ),   D = [d*n1max + i < n1b*n2b]  (quirk A.10(ii))
-// One workgroup per (graph-2 node d, pair), one thread per graph-1 node i: the rows X[c][b][:] of
-// d's neighbours are summed (coalesced) into LDS, then each thread gathers its i's graph-1
-// neighbours from LDS and runs the node MLPs: x1 = lin_l(agg) + lin_r(x) + relu(W2 relu(W1 x + b1)
-// + b2), z = classifier(x1).  (An fp32-MFMA variant of the MLPs measured slower: the layer is bound
-// by the neighbour-row gathers, not the MLP arithmetic.)
 // Layout: X[b][c][d][i] (channel-major, i = graph-1 node fastest), p(i,d) = d*n1max + i.
-// Block order: all (d) blocks of a pair run on ONE XCD (workgroups are dealt to the 8 XCDs
-// round-robin by linear id), so the pair's 17-channel slab (4.4 MB at n = 256) is re-read from
-// that XCD's L2 by the ~6 neighbour blocks instead of from the fabric.
+//
+// Work split.  One workgroup per (pair, graph-2 node d), one thread per graph-1 node i.  Phase 1
+// sums the rows X[c][e][:] of d's graph-2 neighbours e (coalesced along i, two rows' loads in
+// flight, the neighbour ids read with scalar loads straight from the CSR) into LDS, node-major;
+// phase 2 gathers i's graph-1 neighbours from there and runs the node MLPs on packed fp32 FMAs:
+//   x1 = lin_l(agg) + lin_r(x) + relu(W2 relu(W1 x + b1) + b2),  z = classifier(x1).
+// (An fp32-MFMA variant of the MLPs measured slower: fp32 MFMA has the packed-FMA rate on CDNA4.)
+// Block order: all blocks of a pair run on ONE XCD (workgroups are dealt to the 8 XCDs round-robin
+// by linear id), so the pair's slab is re-read from that XCD's L2.  (Measured and dropped: a
+// breadth-first block order of graph 2, -2 % per layer for a 0.1 ms order kernel per chunk, and
+// workgroups of 2-4 BFS-consecutive nodes loading their neighbour-row union once: the larger
+// workgroups lost more to occupancy than the shared loads saved.)
 #include "fpm_common.h"
 #include <cstdlib>
 
@@ -45,142 +49,18 @@ __device__ __forceinline__ void pk_fma_bcast(f2_t& acc, f2_t w, f2_t v, bool hi)
     else asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1]" : "+v"(acc) : "s"(w), "v"(v));
 }
 
-// WIDE (C = 17, n1max % 4 == 0): phase 1 with 16-B loads -- each thread sums one quad of graph-1
-// positions (4 consecutive i) for a group of <= 5 channels, so a graph-2 neighbour row costs
-// 17 / 4 times fewer vector-memory instructions; the per-position sums (same order, same
-// values) land in the same LDS layout, so phase 2 and the outputs are bit-identical.
-template <int C, bool PACKED, int U = 1, int G = 1, bool WIDE = false, bool IL = false>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(PACKED ? 5 : 6, 8))) void gnn_layer_kernel(const float* __restrict__ X, int n1max, int n2max,
-                                                         const int* __restrict__ ptr1, const int* __restrict__ nbr1,
-                                                         const int* __restrict__ ptr2, const int* __restrict__ nbr2,
-                                                         const int* __restrict__ n1, const int* __restrict__ n2,
-                                                         const float* __restrict__ W, float* __restrict__ Xo,
-                                                         float* __restrict__ zbuf, float* __restrict__ vpart,
-                                                         const float* __restrict__ cls_w, int B) {
-    // one thread per graph-1 node i (blockDim >= n1max): no loop, so the uniform weight loads
-    // stay scalar (s_load, SGPR operands of the FMAs) instead of being hoisted into VGPRs.
+// Phase 2 of one association node p = (d, i): agg from the graph-2 sums in LDS (Tg, node-major,
+// TS floats per graph-1 node) gathered over i's graph-1 neighbours, the mean, the node MLPs and
+// classifier (output channels in pairs (o, o+1) on v_pk_fma_f32: the same fma chain per channel as
+// scalar FMAs, half the VALU instructions; the weight pair is one 64-bit scalar operand, the input
+// broadcast from one half of a VGPR pair by op_sel), then the stores.
+template <int C, int TS>
+__device__ __forceinline__ void gnn_point(const float* Tg, __amdgpu_buffer_rsrc_t xr, int N4, long N, int n1max,
+                                          int b, int d, int i, int nn2, const int* __restrict__ ptr1,
+                                          const int* __restrict__ nbr1, int n1b, int n2b, const float* __restrict__ W,
+                                          float* __restrict__ Xo, float* __restrict__ zbuf, float* __restrict__ vpart,
+                                          const float* __restrict__ cls_w) {
     using P = GnnPack<C>;
-    // T[a][TS]: sum of graph-2 neighbour rows, node-major with 80-B rows (C = 17) so phase 2
-    // reads a neighbour's 17 channels with 4 ds_read_b128 + 1 ds_read_b32
-    constexpr int TS = C == 1 ? 1 : 20;
-    extern __shared__ __attribute__((aligned(16))) float T[];
-    __shared__ int nb2_[G][64];
-    __shared__ int nnb2_[G], beg2_[G];
-
-    // G > 1: G graph-2 nodes per workgroup, one thread group of blockDim / G each
-    const int subw = G > 1 ? (int)blockDim.x / G : (int)blockDim.x;
-    const int sub = G > 1 ? (int)threadIdx.x / subw : 0;
-    const int i = G > 1 ? (int)threadIdx.x - sub * subw : (int)threadIdx.x;
-    int dg, b;
-    if (!pair_block((n2max + G - 1) / G, B, b, dg)) return;
-    const int d = dg * G + sub;
-    const bool active = d < n2max;
-    int* nb2 = nb2_[sub];
-    float* Tg = T + (long)sub * n1max * TS;
-    const long N = (long)n1max * n2max;
-    const float* Xb = X + (long)b * C * N;
-    // the pair's C channels as one buffer resource (host check: C * N * 4 < 2^31)
-    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)Xb, (short)0, (int)(C * N * 4), 0x00020000);
-    const int N4 = (int)(N * 4);
-    if (i == 0 && active) {
-        const int beg = ptr2[(long)b * n2max + d], end = ptr2[(long)b * n2max + d + 1];
-        nnb2_[sub] = end - beg;
-        beg2_[sub] = beg;
-        for (int k = 0; k < end - beg && k < 64; ++k) nb2[k] = nbr2[beg + k];
-    }
-    __syncthreads();
-    const int nn2 = active ? nnb2_[sub] : 0;
-    const int beg2 = active ? beg2_[sub] : 0;
-    if constexpr (WIDE) {
-        static_assert(C == 17, "WIDE phase 1 is the 17-channel layer's");
-        constexpr int CPG = 5;                               // ceil(17 / 4); ng >= 4 channel groups
-        const int nq = n1max >> 2;
-        const int ng = subw / nq;
-        const int q = i % nq, g = i / nq;
-        const int c0 = g * ((C + ng - 1) / ng);
-        const int cn = min(C - c0, (C + ng - 1) / ng);
-        if (active && g < ng && cn > 0) {
-            float4 acc[CPG];
-#pragma unroll
-            for (int cc = 0; cc < CPG; ++cc) acc[cc] = make_float4(0.f, 0.f, 0.f, 0.f);
-            const float* base = Xb + (long)c0 * N + 4 * q;
-            auto add_row = [&](int nb) {
-                const float* row = base + (long)nb * n1max;
-                float4 v[CPG];
-#pragma unroll
-                for (int cc = 0; cc < CPG; ++cc)
-                    if (cc < cn) v[cc] = *(const float4*)(row + (long)cc * N);
-#pragma unroll
-                for (int cc = 0; cc < CPG; ++cc)
-                    if (cc < cn) {
-                        acc[cc].x += v[cc].x;
-                        acc[cc].y += v[cc].y;
-                        acc[cc].z += v[cc].z;
-                        acc[cc].w += v[cc].w;
-                    }
-            };
-            const int nl = nn2 < 64 ? nn2 : 64;
-            for (int k = 0; k < nl; ++k) add_row(nb2[k]);
-            for (int k = 64; k < nn2; ++k) add_row(nbr2[beg2 + k]);
-            float* Tq = Tg + 4 * q * TS + c0;
-#pragma unroll
-            for (int cc = 0; cc < CPG; ++cc)
-                if (cc < cn) {
-                    Tq[cc] = acc[cc].x;
-                    Tq[TS + cc] = acc[cc].y;
-                    Tq[2 * TS + cc] = acc[cc].z;
-                    Tq[3 * TS + cc] = acc[cc].w;
-                }
-        }
-    } else if (i < n1max && active) {
-        // neighbour-outer, channel-inner: C independent loads in flight per neighbour row
-        float acc[C];
-#pragma unroll
-        for (int c = 0; c < C; ++c) acc[c] = 0.f;
-        // buffer loads: one 32-bit VGPR row offset + the channel as an SGPR offset, instead of
-        // 64-bit per-channel address math per load (~100 VALU per wave)
-        auto add_row = [&](int nb) {
-            const int off = (nb * n1max + i) * 4;
-            float v[C];
-#pragma unroll
-            for (int c = 0; c < C; ++c) v[c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, off, c * N4, 0));
-#pragma unroll
-            for (int c = 0; c < C; ++c) acc[c] += v[c];
-        };
-        const int nl = nn2 < 64 ? nn2 : 64;
-        int k0 = 0;
-        if constexpr (U > 1) {
-            // U neighbour rows' loads issued together (U x C in flight), summed in the same order
-            for (; k0 + U <= nl; k0 += U) {
-                float v[U][C];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const float* row = Xb + (long)nb2[k0 + u] * n1max + i;
-#pragma unroll
-                    for (int c = 0; c < C; ++c) v[u][c] = row[(long)c * N];
-                }
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-#pragma unroll
-                    for (int c = 0; c < C; ++c) acc[c] += v[u][c];
-            }
-        }
-        for (int k = k0; k < nl; ++k) add_row(nb2[k]);                 // LDS copy of the first 64
-        for (int k = 64; k < nn2; ++k) add_row(nbr2[beg2 + k]);
-
-        float* Ti = Tg + i * TS;
-        if constexpr (C == 17) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                *(float4*)(Ti + 4 * q) = make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
-            Ti[16] = acc[16];
-        } else {
-            Ti[0] = acc[0];
-        }
-    }
-    __syncthreads();
-    if (i >= n1max || !active) return;
-    const int n1b = n1[b], n2b = n2[b];
     const long p = (long)d * n1max + i;
     // the pair's 17 output channels as one buffer resource: channel o at SGPR offset o * N4
     const __amdgpu_buffer_rsrc_t orr = __builtin_amdgcn_make_buffer_rsrc((void*)(Xo + (long)b * 17 * N), (short)0,
@@ -199,6 +79,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(PACKED ? 5
     for (int e = beg; e < end; ++e) {
         const float* Ta = Tg + nbr1[e] * TS;
         if constexpr (C == 17) {
+            static_assert(TS % 4 == 0, "16-B aligned node rows");
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const float4 t4 = *(const float4*)(Ta + 4 * q);
@@ -221,38 +102,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(PACKED ? 5
         float v = self ? agg[c] + x[c] : agg[c];
         agg[c] = v * rc;
     }
-    if (!PACKED) {
-        float h[16];
-#pragma unroll
-        for (int m = 0; m < 16; ++m) {
-            float s = W[P::b1 + m];
-#pragma unroll
-            for (int c = 0; c < C; ++c) s += W[P::W1 + c * 16 + m] * x[c];
-            h[m] = fmaxf(s, 0.f);
-        }
-        float z = 0.f, vp = 0.f;
-#pragma unroll
-        for (int o = 0; o < 16; ++o) {
-            float l = 0.f, r = 0.f, t = 0.f;
-#pragma unroll
-            for (int c = 0; c < C; ++c) {
-                l += W[P::Wl + c * 16 + o] * agg[c];
-                r += W[P::Wr + c * 16 + o] * x[c];
-            }
-#pragma unroll
-            for (int m = 0; m < 16; ++m) t += W[P::W2 + m * 16 + o] * h[m];
-            float x1 = ((l + W[P::bl + o]) + r) + fmaxf(t + W[P::b2 + o], 0.f);
-            if (vpart) vp = fmaf(cls_w[o], x1, vp);      // last layer: only w[0:16] . x1 is consumed
-            else store_o(o, x1);
-            z += W[P::wc + o] * x1;
-        }
-        if (vpart) vpart[(long)b * N + p] = vp;
-        zbuf[(long)b * N + p] = z + W[P::bc];
-        return;
-    }
-    // packed: output channels in pairs (o, o+1) on v_pk_fma_f32 -- the same fma chain per channel
-    // as the scalar path (bit-identical), half the VALU instructions.  The weight pair is one
-    // 64-bit scalar operand; the input value is broadcast from one half of a VGPR pair by op_sel.
     constexpr int CP = (C + 1) / 2;
     f2_t x2[CP], a2[CP];
 #pragma unroll
@@ -261,59 +110,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(PACKED ? 5
         a2[k] = (f2_t){agg[2 * k], 2 * k + 1 < C ? agg[2 * k + 1] : 0.f};
     }
     const f2_t* W2p = (const f2_t*)W;                     // pair view (all block offsets even)
-    if constexpr (IL) {
-        // input-channel-outer order: a weight row W[c][0..15] is contiguous, so the scalar loads
-        // merge into wide s_load_dwordx8/x16 (the per-(c, pair) order issued one s_load_dwordx2
-        // per FMA: ~470 scalar-memory instructions per wave).  Every accumulator keeps its fma
-        // chain order, so the outputs are bit-identical to the loop above.
-        f2_t h[8];
-#pragma unroll
-        for (int m = 0; m < 8; ++m) h[m] = W2p[(P::b1 >> 1) + m];
-#pragma unroll
-        for (int c = 0; c < C; ++c)
-#pragma unroll
-            for (int m = 0; m < 8; ++m) pk_fma_bcast(h[m], W2p[((P::W1 + c * 16) >> 1) + m], x2[c >> 1], c & 1);
-#pragma unroll
-        for (int m = 0; m < 8; ++m) h[m] = (f2_t){fmaxf(h[m].x, 0.f), fmaxf(h[m].y, 0.f)};
-        float z = 0.f, vp = 0.f;
-        constexpr int OPB = 4;                            // output pairs per block (register budget)
-#pragma unroll
-        for (int ob = 0; ob < 8; ob += OPB) {
-            f2_t l[OPB], r[OPB], t[OPB];
-#pragma unroll
-            for (int k = 0; k < OPB; ++k) l[k] = r[k] = t[k] = (f2_t){0.f, 0.f};
-#pragma unroll
-            for (int c = 0; c < C; ++c)
-#pragma unroll
-                for (int k = 0; k < OPB; ++k) {
-                    pk_fma_bcast(l[k], W2p[((P::Wl + c * 16) >> 1) + ob + k], a2[c >> 1], c & 1);
-                    pk_fma_bcast(r[k], W2p[((P::Wr + c * 16) >> 1) + ob + k], x2[c >> 1], c & 1);
-                }
-#pragma unroll
-            for (int m = 0; m < 16; ++m)
-#pragma unroll
-                for (int k = 0; k < OPB; ++k)
-                    pk_fma_bcast(t[k], W2p[((P::W2 + m * 16) >> 1) + ob + k], h[m >> 1], m & 1);
-#pragma unroll
-            for (int k = 0; k < OPB; ++k) {
-                const int op = ob + k, o = 2 * op;
-                const f2_t tb = t[k] + W2p[(P::b2 >> 1) + op];
-                const f2_t x1 = ((l[k] + W2p[(P::bl >> 1) + op]) + r[k]) + (f2_t){fmaxf(tb.x, 0.f), fmaxf(tb.y, 0.f)};
-                if (vpart) {
-                    vp = fmaf(cls_w[o], x1.x, vp);
-                    vp = fmaf(cls_w[o + 1], x1.y, vp);
-                } else {
-                    store_o(o, x1.x);
-                    store_o(o + 1, x1.y);
-                }
-                z = fmaf(W[P::wc + o], x1.x, z);
-                z = fmaf(W[P::wc + o + 1], x1.y, z);
-            }
-        }
-        if (vpart) vpart[(long)b * N + p] = vp;
-        zbuf[(long)b * N + p] = z + W[P::bc];
-        return;
-    }
     f2_t h[8];
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
@@ -348,6 +144,70 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(PACKED ? 5
     }
     if (vpart) vpart[(long)b * N + p] = vp;
     zbuf[(long)b * N + p] = z + W[P::bc];
+}
+
+template <int C>
+__global__ __launch_bounds__(1024) void gnn_layer_kernel(const float* __restrict__ X, int n1max, int n2max,
+                                                         const int* __restrict__ ptr1, const int* __restrict__ nbr1,
+                                                         const int* __restrict__ ptr2, const int* __restrict__ nbr2,
+                                                         const int* __restrict__ n1,
+                                                         const int* __restrict__ n2, const float* __restrict__ W,
+                                                         float* __restrict__ Xo, float* __restrict__ zbuf,
+                                                         float* __restrict__ vpart, const float* __restrict__ cls_w,
+                                                         int B) {
+    // T[i][TS]: sum of graph-2 neighbour rows, node-major with 80-B rows (C = 17) so phase 2
+    // reads a neighbour's 17 channels with 4 ds_read_b128 + 1 ds_read_b32
+    constexpr int TS = C == 1 ? 1 : 20;
+    extern __shared__ __attribute__((aligned(16))) float T[];
+    int b, d;
+    if (!pair_block(n2max, B, b, d)) return;
+    const int i = threadIdx.x;
+    const long N = (long)n1max * n2max;
+    const float* Xb = X + (long)b * C * N;
+    // the pair's C channels as one buffer resource (host check: 17 * N * 4 < 2^31)
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)Xb, (short)0, (int)(C * N * 4), 0x00020000);
+    const int N4 = (int)(N * 4);
+    const int beg2 = ptr2[(long)b * n2max + d], end2 = ptr2[(long)b * n2max + d + 1];
+    if (i < n1max) {
+        float acc[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[c] = 0.f;
+        // buffer loads: one 32-bit VGPR row offset + the channel as an SGPR offset; the neighbour
+        // ids are uniform (scalar loads)
+        auto load_row = [&](int r, float (&v)[C]) {
+#pragma unroll
+            for (int c = 0; c < C; ++c)
+                v[c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, (r * n1max + i) * 4, c * N4, 0));
+        };
+        int k = beg2;
+        for (; k + 1 < end2; k += 2) {          // two rows' loads in flight, summed in list order
+            float va[C], vb[C];
+            load_row(nbr2[k], va);
+            load_row(nbr2[k + 1], vb);
+#pragma unroll
+            for (int c = 0; c < C; ++c) acc[c] += va[c];
+#pragma unroll
+            for (int c = 0; c < C; ++c) acc[c] += vb[c];
+        }
+        if (k < end2) {
+            float va[C];
+            load_row(nbr2[k], va);
+#pragma unroll
+            for (int c = 0; c < C; ++c) acc[c] += va[c];
+        }
+        float* Ti = T + i * TS;
+        if constexpr (C == 17) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                *(float4*)(Ti + 4 * q) = make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
+            Ti[16] = acc[16];
+        } else {
+            Ti[0] = acc[0];
+        }
+    }
+    __syncthreads();
+    if (i >= n1max) return;
+    gnn_point<C, TS>(T, xr, N4, N, n1max, b, d, i, end2 - beg2, ptr1, nbr1, n1[b], n2[b], W, Xo, zbuf, vpart, cls_w);
 }
 
 // v[p] = classifier(emb[p]) (ngm.py:368), written as s[b][i][j] = v[b][j*n1max + i] (ngm.py:369).
@@ -424,117 +284,23 @@ int& nodecls_t_flag() {
     return on;
 }
 
-// MLP on packed fp32 FMAs (default) or scalar FMAs (bit-identical); env FPM_GNN_PACKED or
-// fpm_set_tuning("gnn_packed", v)
-int& gnn_packed_flag() {
-    static int on = [] {
-        const char* e = getenv("FPM_GNN_PACKED");
-        return e ? atoi(e) : 1;
-    }();
-    return on;
-}
-
-// graph-2 nodes per workgroup, processed by parallel 256-thread groups (1, 2, 4; bit-identical);
-// env FPM_GNN_GROUP or fpm_set_tuning("gnn_group", v)
-int& gnn_group_flag() {
-    static int u = [] {
-        const char* e = getenv("FPM_GNN_GROUP");
-        return e ? atoi(e) : 2;
-    }();
-    return u;
-}
-
-// the grouping for the first (1-channel) layer as well: env FPM_GNN_GROUP1 / "gnn_group1"
-int& gnn_group1_flag() {
-    static int u = [] {
-        const char* e = getenv("FPM_GNN_GROUP1");
-        return e ? atoi(e) : 0;
-    }();
-    return u;
-}
-
-// 16-B phase-1 loads for the 17-channel layer (bit-identical); env FPM_GNN_WIDE or
-// fpm_set_tuning("gnn_wide", v)
-int& gnn_wide_flag() {
-    static int u = [] {
-        const char* e = getenv("FPM_GNN_WIDE");
-        return e ? atoi(e) : 0;
-    }();
-    return u;
-}
-
-// input-channel-outer MLP order (wide scalar weight loads, bit-identical); env FPM_GNN_IL or
-// fpm_set_tuning("gnn_il", v)
-int& gnn_il_flag() {
-    static int u = [] {
-        const char* e = getenv("FPM_GNN_IL");
-        return e ? atoi(e) : 0;
-    }();
-    return u;
-}
-
-// graph-2 neighbour rows loaded U at a time (1, 2 or 3; bit-identical); env FPM_GNN_UNROLL or
-// fpm_set_tuning("gnn_unroll", v)
-int& gnn_unroll_flag() {
-    static int u = [] {
-        const char* e = getenv("FPM_GNN_UNROLL");
-        return e ? atoi(e) : 1;
-    }();
-    return u;
-}
-
 extern "C" int fpm_kron_gnn_layer_fwd(const float* X, int C, int B, int n1max, int n2max, const int* ptr1,
-                                      const int* nbr1, const int* ptr2, const int* nbr2, const int* n1, const int* n2,
-                                      const float* params, float* Xout, float* zbuf, float* vpart, const float* cls_w,
-                                      void* stream) {
+                                      const int* nbr1, const int* ptr2, const int* nbr2, const int* n1,
+                                      const int* n2, const float* params, float* Xout, float* zbuf,
+                                      float* vpart, const float* cls_w, void* stream) {
     FPM_CHECK_ARG(C == 1 || C == 17, "gnn_layer: C must be 1 or 17 (got %d)", C);
     FPM_CHECK_ARG(!vpart || cls_w, "gnn_layer: vpart needs cls_w");
     if (B == 0) return 0;
-    FPM_CHECK_ARG(n1max <= 1024, "gnn_layer: n1max must be <= 1024");
-    FPM_CHECK_ARG((long)C * n1max * n2max * 4 < (1L << 31), "gnn_layer: a pair's state must be < 2 GiB");
-    dim3 grid(pair_grid(n2max, B));
-    hipStream_t st = (hipStream_t)stream;
+    FPM_CHECK_ARG(n1max >= 1 && n1max <= 1024, "gnn_layer: n1max must be in [1, 1024]");
+    FPM_CHECK_ARG((long)17 * n1max * n2max * 4 < (1L << 31), "gnn_layer: a pair's state must be < 2 GiB");
     const size_t sh = (size_t)(C == 1 ? 1 : 20) * n1max * 4;
     const int threads = (n1max + 63) / 64 * 64;
-    const bool packed = gnn_packed_flag() != 0;
-    const int un = gnn_unroll_flag();
-    // default 2 (21% faster at n = 256, 13% at n = 100; slower as a 1024-thread workgroup at n = 512)
-    const int grp = gnn_group_flag() * threads <= 512 ? gnn_group_flag() : 1;
-    const bool wide = gnn_wide_flag() != 0 && (n1max & 3) == 0;
-    const bool il = gnn_il_flag() != 0;
-#define FPM_GNN_WI(C_, P_, U_, G_, W_, I_)                                                                       \
-    do {                                                                                                         \
-        const size_t sh_ = sh * G_;                                                                              \
-        if (sh_ > 65536)                                                                                         \
-            (void)hipFuncSetAttribute((const void*)gnn_layer_kernel<C_, P_, U_, G_, W_, I_>,                     \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh_);                     \
-        const dim3 g_(pair_grid((n2max + G_ - 1) / G_, B));                                                      \
-        const dim3 t_(threads * G_);                                                                             \
-        hipLaunchKernelGGL((gnn_layer_kernel<C_, P_, U_, G_, W_, I_>), g_, t_, sh_, st, X, n1max, n2max, ptr1,   \
-                           nbr1, ptr2, nbr2, n1, n2, params, Xout, zbuf, vpart, cls_w, B);                       \
-    } while (0)
-#define FPM_GNN_W(C_, P_, U_, G_, W_)                                                                            \
-    do {                                                                                                         \
-        if (il) FPM_GNN_WI(C_, P_, U_, G_, W_, true);                                                            \
-        else FPM_GNN_WI(C_, P_, U_, G_, W_, false);                                                              \
-    } while (0)
-#define FPM_GNN(C_, P_, U_, G_) FPM_GNN_W(C_, P_, U_, G_, false)
-    if (C == 1) {
-        if (!packed) FPM_GNN(1, false, 1, 1);
-        else if (grp == 2 && gnn_group1_flag()) FPM_GNN(1, true, 1, 2);
-        else FPM_GNN(1, true, 1, 1);
-    }
-    else if (!packed) FPM_GNN(17, false, 1, 1);
-    else if (wide && grp == 2) FPM_GNN_W(17, true, 1, 2, true);
-    else if (wide) FPM_GNN_W(17, true, 1, 1, true);
-    else if (grp == 2) FPM_GNN(17, true, 1, 2);
-    else if (grp == 4) FPM_GNN(17, true, 1, 4);
-    else if (un == 2) FPM_GNN(17, true, 2, 1);
-    else if (un == 3) FPM_GNN(17, true, 3, 1);
-    else FPM_GNN(17, true, 1, 1);
-#undef FPM_GNN
-#undef FPM_GNN_W
-#undef FPM_GNN_WI
+    void (*k)(const float*, int, int, const int*, const int*, const int*, const int*, const int*, const int*,
+              const float*, float*, float*, float*, const float*, int) =
+        C == 1 ? gnn_layer_kernel<1> : gnn_layer_kernel<17>;
+    if (sh > 65536) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
+    hipLaunchKernelGGL(k, dim3(pair_grid(n2max, B)), dim3(threads), sh, (hipStream_t)stream, X, n1max, n2max, ptr1,
+                       nbr1, ptr2, nbr2, n1, n2, params, Xout, zbuf, vpart, cls_w, B);
     return fpm::check_launch("fpm_kron_gnn_layer_fwd");
 }
 

@@ -136,6 +136,8 @@ class Net(nn.Module):
         # later (same compute stream) has run: that latency-bound kernel otherwise runs beside the
         # copy's blit kernel and stalls ~25x
         self.copy_defer = int(os.environ.get("FPM_COPY_DEFER", "1"))
+        if self.copy_defer not in (0, 1):
+            raise ValueError("FPM_COPY_DEFER must be 0 or 1")
         self._plan_events = None
         # FPM_OFFSET=1: the second stream starts its first chunk after the first chunk's SplineConv,
         # so the streams' phases interleave (MFMA-heavy SplineConv beside the VALU / memory-bound GNN,
@@ -251,28 +253,25 @@ class Net(nn.Module):
         return d
 
     # ------------------------------------------------------------------------------------------
-    def _spline_side(self, wp, bt, side, cscale):
-        """SiameseSConvOnNodes over one side's batch (spline_conv.py:28-57) -> operand rows."""
+    def _spline_side(self, wp, bt, side, cscale, x_op=None):
+        """SiameseSConvOnNodes over one side's batch (spline_conv.py:28-57) -> operand rows.
+        ``x_op``: this side's bf16 operand rows when the caller cast the whole batch up front."""
         dev = bt.device
         op = torch.bfloat16 if self.dtype_mode == "bf16" else torch.float32
         nn_ = bt.B * bt.nmax[side]
         E = bt.E[side]
         plan = ops.spline_plan(bt.src[side], bt.dst[side], bt.pseudo[side], nn_, bt.nmax[side],
                                bt.max_graph_edges(side))
-        # FPM_COPY_DEFER=1: the previous-but-one chunk's D2H starts after this side-0 plan;
-        # 2: after the side-0 bf16 cast too (the product GEMM then runs beside the copy's blit)
-        if side == 0 and self._plan_events is not None and (self.copy_defer == 1 or bt.shared0):
+        # copy deferral: the previous-but-one chunk's D2H starts after this side-0 plan
+        if side == 0 and self._plan_events is not None:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(dev))
             self._plan_events.append(ev)
         if side == 0 and bt.shared0 and bt.B > 1:
             return (plan,) + self._spline_shared(wp, bt, cscale)
         x0 = bt.x[side]
-        x_op = ops.cast_bf16(x0) if op == torch.bfloat16 else x0
-        if side == 0 and self._plan_events is not None and self.copy_defer == 2 and not bt.shared0:
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(dev))
-            self._plan_events.append(ev)
+        if x_op is None:
+            x_op = ops.cast_bf16(x0) if op == torch.bfloat16 else x0
         yws = ops.spline_y_ws(ops.BF16 if op == torch.bfloat16 else ops.F32, E, nn_, dev)
         h = torch.empty(nn_, C.NODE_FEATURE_DIM, device=dev, dtype=op)
         ops.spline_conv(x_op, plan, E, nn_, bt.nmax[side], bt.n[side], wp["W0"], wp["bias0"], yws, 0, out_t=h)
@@ -440,9 +439,10 @@ class Net(nn.Module):
                  C.GLOBAL_STATE_DIM, epi=ops.EPI_TANH, bias=wp["aff_b"], out_f=coef)
         return gw, coef
 
-    def run_gpu_stage(self, bt, keep_feats=False, s_out=None, ss_out=None, gc=None):
+    def run_gpu_stage(self, bt, keep_feats=False, s_out=None, ss_out=None, gc=None, x_ops=(None, None)):
         """Everything up to ds_mat on the GPU.  Returns a dict of device tensors.  ``gc``: this
-        batch's rows of global_coef() when computed for a parent batch."""
+        batch's rows of global_coef() when computed for a parent batch; ``x_ops``: its rows of the
+        parent's bf16 operand copies of the node features (cast once per forward)."""
         keep_feats = keep_feats or self.compute_ke
         self._keep_feats = keep_feats
         if self._stage_timing:
@@ -454,8 +454,8 @@ class Net(nn.Module):
         N = n1max * n2max
         gw, coef = gc if gc is not None else self.global_coef(bt)
         self._mark("coef")
-        plan0, x1c, f1 = self._spline_side(wp, bt, 0, coef)
-        plan1, x2, f2 = self._spline_side(wp, bt, 1, None)
+        plan0, x1c, f1 = self._spline_side(wp, bt, 0, coef, x_ops[0])
+        plan1, x2, f2 = self._spline_side(wp, bt, 1, None, x_ops[1])
         self._mark("splineconv")
         if self._offset_events is not None:
             ev = torch.cuda.Event()
@@ -537,11 +537,13 @@ class Net(nn.Module):
         ev.record(cs)
         return ev
 
-    def _stage_a(self, part, b0, b1, o, keep_feats, gt_ks, min_pt, st, gc, col=None, defer=None):
+    def _stage_a(self, part, b0, b1, o, keep_feats, gt_ks, min_pt, st, gc, col=None, defer=None, xop=None):
         """GPU stage of one chunk (on its stream): everything up to ds_mat, then its D2H copy."""
         dev = part.device
+        x_ops = tuple(None if t is None else t[b0 * part.nmax[s]:b1 * part.nmax[s]]
+                      for s, t in enumerate(xop or (None, None)))
         r = self.run_gpu_stage(part, keep_feats, s_out=o["s"][b0:b1], ss_out=o["ss"][b0:b1],
-                               gc=(gc[0][b0:b1], gc[1][b0:b1]))
+                               gc=(gc[0][b0:b1], gc[1][b0:b1]), x_ops=x_ops)
         ks = o["k_prob"][b0:b1]
         if self.regression:
             ks.copy_(self._afau(self.packed(dev), o["ss"][b0:b1], part, col=col))
@@ -648,6 +650,12 @@ class Net(nn.Module):
         ev_start = torch.cuda.Event(enable_timing=True)
         ev_start.record(main)
         gc = self.global_coef(bt)
+        # bf16 operand rows of both sides' node features in one launch each, before any chunk's
+        # ds_mat D2H is in flight (cast per chunk, they ran beside the copy's blit kernel and
+        # stalled ~14x; a shared probe side is cast inside its chunk's one-graph SplineConv)
+        xop = None
+        if self.dtype_mode == "bf16" and len(parts) > 1:
+            xop = tuple(None if (s == 0 and bt.shared0) else ops.cast_bf16(bt.x[s]) for s in range(2))
         # the AFA-U column block once for the whole batch (per distinct n2), before the chunks
         col = (self._afau_col(self.packed(dev), bt)
                if self.regression and os.environ.get("FPM_AFAU_COLDEDUP", "1") == "1"
@@ -672,7 +680,8 @@ class Net(nn.Module):
                     st.wait_event(self._offset_events[0])
                     self._offset_events = None
                 with torch.cuda.stream(st):
-                    r, ev = self._stage_a(part, b0, b1, o, keep_feats, gt_ks, min_pt, st, gc, col=col, defer=pending)
+                    r, ev = self._stage_a(part, b0, b1, o, keep_feats, gt_ks, min_pt, st, gc, col=col, defer=pending,
+                                          xop=xop)
                 outs.append(r)
                 events.append(ev)
                 if lag and c >= lag:

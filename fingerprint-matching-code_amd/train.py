@@ -56,6 +56,7 @@ class _Side:
         self.csr = ops.plan_csr(self.plan, self.E, self.num_nodes)
         self._rplan = None
 
+
     def out_csr(self):
         if self._rplan is None:
             bt = self.bt

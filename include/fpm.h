@@ -98,10 +98,6 @@ int fpm_memcpy_async(void* dst, const void* src, long bytes, int kind, void* str
  *                kernel (one workgroup per CU over the plan's real tiles, next tile's DMA prologue under
  *                the current epilogue; bit-identical; +9 % alone, -1.5 % inside the two-stream forward);
  *                env FPM_GEMM_PERSIST_GRID caps its workgroup count
- *   "gnn_packed" (env FPM_GNN_PACKED, default 1): GNN-layer MLPs on packed (1) or scalar (0) FMAs
- *   "gnn_group"  (FPM_GNN_GROUP, default 2): graph-2 nodes per GNN workgroup (1, 2, 4; n1max <= 256)
- *   "gnn_group1" (FPM_GNN_GROUP1, default 0): the same for the 1-channel first layer
- *   "gnn_unroll" (FPM_GNN_UNROLL, default 1): graph-2 neighbour rows loaded 1, 2 or 3 at a time
  *   "combine_npb" (FPM_COMBINE_NPB, default 4): destination nodes per SplineConv combine workgroup
  * Switches whose variants round differently (results within fp32 rounding, not bit-identical):
  *   "sinkhorn_fast" (FPM_SINKHORN_FAST, default 1): shifted single-pass lse after the first step
@@ -166,7 +162,8 @@ int fpm_edge_diff_padded(const float* x, const int* src, const int* dst, const i
  * is written instead of Xout channels 0..15 (fpm_node_classifier then reads vpart + channel 16).
  * params: fpm_gnn_param_count(C) floats = lin_l.weight^T [C][16], lin_l.bias [16],
  * lin_r.weight^T [C][16], n_self_func.0.weight^T [C][16], n_self_func.0.bias [16],
- * n_self_func.2.weight^T [16][16], n_self_func.2.bias [16], classifier.weight [16], classifier.bias. */
+ * n_self_func.2.weight^T [16][16], n_self_func.2.bias [16], classifier.weight [16], classifier.bias.
+ * n1max <= 1024; neighbour lists ascending (the plan CSR). */
 int fpm_kron_gnn_layer_fwd(const float* X, int C, int B, int n1max, int n2max, const int* ptr1, const int* nbr1,
                            const int* ptr2, const int* nbr2, const int* n1, const int* n2, const float* params,
                            float* Xout, float* zbuf, float* vpart, const float* cls_w, void* stream);

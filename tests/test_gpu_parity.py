@@ -270,7 +270,10 @@ def _perm_gate(res, ref, pairs, name):
     only by a (near-)tie or a k* rounding-boundary crossing; the classes are recorded."""
     n1 = [p[0]["n"] for p in pairs]
     n2 = [p[1]["n"] for p in pairs]
-    rep = O.compare.perm_report(res, ref, n1, n2)
+    bf16 = "bf16" in name
+    # k* rounding crossings are judged against the mode's own k_prob tolerance
+    rep = O.compare.perm_report(res, ref, n1, n2, reduced_precision=bf16,
+                                k_tol=2.0 * BF16_MEASURED["k_prob"] if bf16 else 1e-4)
     _record(name, {k: v for k, v in rep.items()})
     assert rep["counts"]["mismatch"] == 0, rep
     return rep
@@ -496,8 +499,7 @@ def test_gconv_golden():
 @pytest.mark.parametrize("C,layer", [(1, 0), (17, 1)])
 def test_gnn_layer_vs_oracle(sd, C, layer):
     """Kronecker GNN layer (gnn.hip) on a ragged batch: x1 (Xout channels 0..15) and the
-    classifier logit z against the oracle's factorised aggregation + MLPs; the packed-FMA and
-    scalar-FMA MLPs bit-identical."""
+    classifier logit z against the oracle's factorised aggregation + MLPs."""
     import torch.nn.functional as F
     from fpm import synth
     n1s, n2s = [40, 33, 25], [40, 38, 20]
@@ -510,19 +512,11 @@ def test_gnn_layer_vs_oracle(sd, C, layer):
     wp = net.packed(DEV)
     g = torch.Generator().manual_seed(C)
     X = torch.randn(B, C, nm, nm, generator=g)                 # [b][c][j (graph 2)][i (graph 1)]
-    outs = []
-    for packed in (1, 0):
-        prev = ops.set_tuning("gnn_packed", packed)
-        try:
-            Xn = torch.full((B, 17, nm, nm), 5.0, device=DEV)
-            z = torch.full((B, nm, nm), 5.0, device=DEV)
-            ops.gnn_layer(X.to(DEV), C, B, nm, nm, csr[0], csr[1], bt.n1, bt.n2, wp["gnn%d" % layer], Xn, z)
-            torch.cuda.synchronize()
-        finally:
-            ops.set_tuning("gnn_packed", prev)
-        outs.append((Xn.cpu(), z.cpu()))
-    assert torch.equal(outs[0][0][:, :16], outs[1][0][:, :16]) and torch.equal(outs[0][1], outs[1][1])
-    Xn, z = outs[0]
+    Xn = torch.full((B, 17, nm, nm), 5.0, device=DEV)
+    z = torch.full((B, nm, nm), 5.0, device=DEV)
+    ops.gnn_layer(X.to(DEV), C, B, nm, nm, csr[0], csr[1], bt.n1, bt.n2, wp["gnn%d" % layer], Xn, z)
+    torch.cuda.synchronize()
+    Xn, z = Xn.cpu(), z.cpu()
     pre = "gnn_layer_%d" % layer
     w = lambda k: sd[pre + k].float()
     for b in range(B):
@@ -721,7 +715,7 @@ def test_gnn_kernel_variants_bit_identical(sd):
     net.load_state_dict(sd)
     bt = DeviceBatch.from_pairs(pairs, DEV)
     outs = []
-    for key, val in (("gnn_group", 1), ("gnn_group", 2), ("gnn_unroll", 3), ("combine_npb", 16), ("gnn_wide", 1), ("gnn_il", 1),
+    for key, val in (("combine_npb", 4), ("combine_npb", 16),
                      ("plan_graph", 0), ("combine_pf", 0), ("combine_pf", 1), ("gemm_persist", 1), ("nodecls_t", 0)):
         prev = ops.set_tuning(key, val)
         try:

@@ -26,6 +26,9 @@ variants = [tuple((k, int(v)) for k, v in (kv.split("=") for kv in a.split(","))
 ROUNDS = int(os.environ.get("ROUNDS", 5))
 
 
+ORD = {}
+
+
 def time_layer(C, key, Xc, reps=20):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
