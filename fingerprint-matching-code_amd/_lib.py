@@ -27,8 +27,6 @@ SIGNATURES = {
     "fpm_cast_bf16": (I, [P, P, L, P]),
     "fpm_global_weights": (I, [P, L, P, L, I, I, I, P, L, P]),
     "fpm_split_bf16x3": (I, [P, L, L, I, I, P, L, P]),
-    "fpm_copy_async": (I, [P, P, L, I, P]),
-    "fpm_memcpy_async": (I, [P, P, L, I, P]),
     "fpm_set_tuning": (I, [ctypes.c_char_p, I]),
     "fpm_spline_plan_bytes": (L, [L, L]),
     "fpm_spline_plan": (I, [P, P, P, L, L, I, P, L, P]),
@@ -88,6 +86,7 @@ SIGNATURES = {
     "fpm_kron_agg": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, I, P, P]),
     "fpm_kron_gnn_layer_bwd_point": (I, [P, I, I, I, I, P, P, P, P, P, P, P]),
     "fpm_profile_enable": (I, [I]),
+    "fpm_profile_enabled": (I, []),
     "fpm_profile_read": (I, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(I)]),
 }

@@ -32,13 +32,13 @@ class DeviceBatch:
         self.edge_off = edge_off
         self._splits = {}
 
-    def split(self, k, tail=0, head=0):
+    def split(self, k, tail=0):
         """k contiguous sub-batches of pairs (views of x/w, renumbered edge copies); cached.
         ``tail`` > 0 halves the last chunk ``tail`` times (a short final chunk shortens the host
         Hungarian that runs after the GPU has finished)."""
         if k <= 1 or self.B < 2:
             return [self]
-        key = (k, tail, head)
+        key = (k, tail)
         if key in self._splits:
             return self._splits[key]
         if self.edge_off is None:
@@ -48,10 +48,6 @@ class DeviceBatch:
             a, b = bounds[-2], bounds[-1]
             if b - a >= 2:
                 bounds.insert(-1, (a + b) // 2)
-        for _ in range(head):      # a short first chunk starts the host Hungarian earlier
-            a, b = bounds[0], bounds[1]
-            if b - a >= 2:
-                bounds.insert(1, (a + b) // 2)
         parts = [self.split_range(bounds[c], bounds[c + 1]) for c in range(len(bounds) - 1)
                  if bounds[c + 1] > bounds[c]]
         self._splits[key] = parts

@@ -554,35 +554,9 @@ __global__ __launch_bounds__(1024) void instnorm_kernel(const float* __restrict_
     }
 }
 
-// ks = sigmoid((final_row(gr) + final_col(gc)) / 2)   (ngm.py:406-412, mean_k = True)
-__global__ __launch_bounds__(64) void afau_head_kernel(const float* __restrict__ gr, const float* __restrict__ gc,
-                                                       int E, const float* __restrict__ r0w, const float* __restrict__ r0b,
-                                                       const float* __restrict__ r2w, const float* __restrict__ r2b,
-                                                       const float* __restrict__ c0w, const float* __restrict__ c0b,
-                                                       const float* __restrict__ c2w, const float* __restrict__ c2b,
-                                                       float* __restrict__ ks) {
-    const int b = blockIdx.x, lane = threadIdx.x;
-    float kr = 0.f, kc = 0.f;
-    for (int m = 0; m < 8; ++m) {
-        float sr = 0.f, sc = 0.f;
-        for (int k = lane; k < E; k += 64) {
-            sr += r0w[m * E + k] * gr[(long)b * E + k];
-            sc += c0w[m * E + k] * gc[(long)b * E + k];
-        }
-        sr = fpm::warp_sum(sr) + r0b[m];
-        sc = fpm::warp_sum(sc) + c0b[m];
-        kr += r2w[m] * fmaxf(sr, 0.f);
-        kc += c2w[m] * fmaxf(sc, 0.f);
-    }
-    kr += r2b[0];
-    kc += c2b[0];
-    if (lane == 0) ks[b] = 1.f / (1.f + expf(-((kr + kc) / 2.f)));
-}
-
-// The same with the 8 hidden units on 8 waves (the one-wave form ran the 16 dot products of length
-// E back to back: ~60 us per launch, latency-bound on 1 wave per pair).  Each unit's dot product and
-// lane-0 sum are those of afau_head_kernel; the units are then combined in the same order:
-// bit-identical.
+// ks = sigmoid((final_row(gr) + final_col(gc)) / 2)   (ngm.py:406-412, mean_k = True): the 8
+// hidden units on 8 waves (a one-wave form ran the 16 dot products of length E back to back:
+// ~60 us per launch, latency-bound on 1 wave per pair); the units combined in order by thread 0.
 __global__ __launch_bounds__(512) void afau_head8_kernel(const float* __restrict__ gr, const float* __restrict__ gc,
                                                          int E, const float* __restrict__ r0w, const float* __restrict__ r0b,
                                                          const float* __restrict__ r2w, const float* __restrict__ r2b,
@@ -617,19 +591,10 @@ __global__ __launch_bounds__(512) void afau_head8_kernel(const float* __restrict
 
 }  // namespace
 
+// the LDS-staged-V kernel where it applies (1) or always the gather kernel (0): kernel-vs-kernel
+// tests only, fpm_set_tuning("afau_attn_v", v)
 int& afau_attn_v_flag() {
-    static int v = [] {
-        const char* e = getenv("FPM_AFAU_ATTN_V");
-        return e ? atoi(e) : 1;
-    }();
-    return v;
-}
-
-int& afau_lut_flag() {
-    static int v = [] {
-        const char* e = getenv("FPM_AFAU_LUT");
-        return e ? atoi(e) : 2;      // 2 = by dtype
-    }();
+    static int v = 1;
     return v;
 }
 
@@ -641,15 +606,15 @@ extern "C" int fpm_crossset_attn_fwd(int dtype, const float* cost, long c_sb, lo
     dim3 grid(B, (n1max + 15) / 16);
     hipStream_t st = (hipStream_t)stream;
     FPM_CHECK_ARG(n2max <= 640, "crossset_attn: n2max %d > 640", n2max);
-    // fp32 (parity) mode scores with the 16-term sum (the reference's operation order); the LUT is
-    // the bf16 throughput mode's (env FPM_AFAU_LUT / fpm_set_tuning("afau_lut") override)
-    const bool v_ok = n2max <= 512 && emb >= n2max && emb % 4 == 0 && ((uintptr_t)Wv & 15) == 0 && afau_attn_v_flag() != 0;
-    const int lut = afau_lut_flag() != 2 ? afau_lut_flag() : (dtype != 0 && !v_ok);
+    // the LDS-staged-V kernel where it applies (n2max <= 512); beyond, the gather kernel, whose
+    // bf16 throughput modes score through a lookup table (fp32 parity mode: the 16-term sum, the
+    // reference's operation order)
+    const bool v_ok = n2max <= 512 && emb >= n2max && emb % 4 == 0 && ((uintptr_t)Wv & 15) == 0 && afau_attn_v_flag();
+    const int lut = dtype != 0 && !v_ok;
 #define FPM_ATT(TT, TJ_, SP_)                                                                                    \
     hipLaunchKernelGGL((afau_row_attn_kernel<TT, TJ_, SP_>), grid, dim3(256), 0, st, cost, c_sb, c_ld, n1max, n2max, \
                        n2, Wv, emb, mix1w, mix1b, mix2w, mix2b, (TT*)out, lut, (float2*)stats)
-    // the LDS-staged-V kernel (16-term scores) where it applies; env FPM_AFAU_ATTN_V=0 keeps the other
-    const bool vpath = !lut && v_ok;
+    const bool vpath = v_ok;
 #define FPM_ATTV(TT, SP_)                                                                                        \
     do {                                                                                                         \
         if (n2max <= 256)                                                                                        \
@@ -698,11 +663,7 @@ extern "C" int fpm_afau_head(const float* gr, const float* gc, int B, int E, con
                              const float* r2w, const float* r2b, const float* c0w, const float* c0b, const float* c2w,
                              const float* c2b, float* ks, void* stream) {
     if (B == 0) return 0;
-    if (getenv("FPM_AFAU_HEAD1") == nullptr)
-        hipLaunchKernelGGL(afau_head8_kernel, dim3(B), dim3(512), 0, (hipStream_t)stream, gr, gc, E, r0w, r0b, r2w, r2b,
-                           c0w, c0b, c2w, c2b, ks);
-    else
-        hipLaunchKernelGGL(afau_head_kernel, dim3(B), dim3(64), 0, (hipStream_t)stream, gr, gc, E, r0w, r0b, r2w, r2b,
-                           c0w, c0b, c2w, c2b, ks);
+    hipLaunchKernelGGL(afau_head8_kernel, dim3(B), dim3(512), 0, (hipStream_t)stream, gr, gc, E, r0w, r0b, r2w, r2b,
+                       c0w, c0b, c2w, c2b, ks);
     return fpm::check_launch("fpm_afau_head");
 }

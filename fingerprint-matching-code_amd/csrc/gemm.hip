@@ -6,7 +6,6 @@
 #include <cstring>
 
 namespace fpm {
-int& gemm_aff_big_flag();
 }
 
 extern "C" int fpm_gemm(int dtype, const void* A, long lda, long sA, const int* a_rows, const void* B, long ldb,
@@ -31,7 +30,7 @@ extern "C" int fpm_gemm(int dtype, const void* A, long lda, long sA, const int* 
     hipStream_t st = (hipStream_t)stream;
     // bf16 with a large M: the 256-row LDS-DMA tiles (gemm_big.h)
     const int mt = (M + G2_BM - 1) / G2_BM;
-    const bool epi_ok = epi == EPI_STORE || epi == EPI_RELU || (epi == EPI_AFFINITY && Cf && !Ct && gemm_aff_big_flag());
+    const bool epi_ok = epi == EPI_STORE || epi == EPI_RELU || (epi == EPI_AFFINITY && Cf && !Ct);
     const bool big = dtype == 1 && M >= G2_BM && K % G2_BK == 0 && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
                      !(Cf && Ct) && (Cf ? ldc % 4 == 0 : ldc % 8 == 0) && epi_ok &&
                      (long)mt * ((N + 127) / 128) * batch >= 128;
@@ -66,38 +65,6 @@ extern "C" int fpm_gemm(int dtype, const void* A, long lda, long sA, const int* 
 }
 
 namespace fpm {
-// the vertex-affinity epilogue on the 256-row LDS-DMA tiles (1) or the 128x128 tiles (0);
-// env FPM_GEMM_AFF_BIG or fpm_set_tuning("gemm_aff_big", v)
-int& gemm_aff_big_flag() {
-    static int on = [] {
-        const char* e = getenv("FPM_GEMM_AFF_BIG");
-        return e ? atoi(e) : 1;
-    }();
-    return on;
-}
-
-int& gemm_persist_flag() {
-    static int on = [] {
-        const char* e = getenv("FPM_GEMM_PERSIST");
-        return e ? atoi(e) : 0;
-    }();
-    return on;
-}
-
-// one persistent workgroup per CU (whole rounds of the 8 XCDs)
-int gemm_persist_grid() {
-    static int g = [] {
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 8)
-            cus = 256;
-        const char* e = getenv("FPM_GEMM_PERSIST_GRID");   // A/B: fewer workgroups than CUs
-        if (e && atoi(e) >= 8 && atoi(e) < cus) cus = atoi(e);
-        return cus / 8 * 8;
-    }();
-    return g;
-}
-
 int& gemm_phase_flag() {
     static int on = [] {
         const char* e = getenv("FPM_GEMM_PHASE");
@@ -107,30 +74,22 @@ int& gemm_phase_flag() {
 }
 }  // namespace fpm
 
-int& nodecls_t_flag();
 int& plan_graph_flag();
 int& combine_npb_flag();
-int& combine_pf_flag();
 int& sinkhorn_bwd_reg_flag();
-int& afau_lut_flag();
-int& afau_attn_v_flag();
 int& sinkhorn_fast_flag();
 int& soft_topk_fast_flag();
+int& afau_attn_v_flag();
 
 extern "C" int fpm_set_tuning(const char* key, int value) {
     int* f = nullptr;
     if (key && !strcmp(key, "gemm_phase")) f = &fpm::gemm_phase_flag();
-    else if (key && !strcmp(key, "gemm_persist")) f = &fpm::gemm_persist_flag();
-    else if (key && !strcmp(key, "gemm_aff_big")) f = &fpm::gemm_aff_big_flag();
-    else if (key && !strcmp(key, "nodecls_t")) f = &nodecls_t_flag();
     else if (key && !strcmp(key, "plan_graph")) f = &plan_graph_flag();
     else if (key && !strcmp(key, "combine_npb")) f = &combine_npb_flag();
-    else if (key && !strcmp(key, "combine_pf")) f = &combine_pf_flag();
     else if (key && !strcmp(key, "sinkhorn_bwd_reg")) f = &sinkhorn_bwd_reg_flag();
-    else if (key && !strcmp(key, "afau_lut")) f = &afau_lut_flag();
-    else if (key && !strcmp(key, "afau_attn_v")) f = &afau_attn_v_flag();
     else if (key && !strcmp(key, "sinkhorn_fast")) f = &sinkhorn_fast_flag();
     else if (key && !strcmp(key, "topk_fast")) f = &soft_topk_fast_flag();
+    else if (key && !strcmp(key, "afau_attn_v")) f = &afau_attn_v_flag();
     if (!f) {
         fpm::set_error("fpm_set_tuning: unknown key '%s'", key ? key : "(null)");
         return -1;
@@ -246,38 +205,3 @@ extern "C" int fpm_split_bf16x3(const float* src, long lds, long rows, int K, in
     return fpm::check_launch("fpm_split_bf16x3");
 }
 
-// Device -> pinned-host copy on a few workgroups.  The runtime's blit copy for this direction
-// launches one 512-thread workgroup per CU for the whole (PCIe-bound) transfer; the transfer needs
-// only enough 16-B stores in flight, so a handful of workgroups keep the CUs for the compute
-// streams.  dst must be device-accessible (pinned host memory); 16-B aligned, bytes % 16 == 0.
-namespace {
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-__global__ __launch_bounds__(1024) void copy16_kernel(const u32x4_t* __restrict__ src, u32x4_t* __restrict__ dst, long n) {
-    for (long k = (long)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (long)gridDim.x * blockDim.x)
-        __builtin_nontemporal_store(src[k], dst + k);
-}
-}  // namespace
-
-extern "C" int fpm_copy_async(const void* src, void* dst, long bytes, int nblocks, void* stream) {
-    FPM_CHECK_ARG(((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0 && bytes % 16 == 0,
-                  "copy_async: 16-B aligned pointers and sizes required");
-    if (bytes == 0) return 0;
-    if (nblocks <= 0) nblocks = 16;
-    hipLaunchKernelGGL(copy16_kernel, dim3(nblocks), dim3(1024), 0, (hipStream_t)stream, (const u32x4_t*)src, (u32x4_t*)dst,
-                       bytes / 16);
-    return fpm::check_launch("fpm_copy_async");
-}
-
-// hipMemcpyAsync with an explicit copy kind (2 = device -> host, 1024 = hipMemcpyDeviceToDeviceNoCU:
-// a copy engine instead of a blit kernel, for a pinned host destination the device can address).
-// Used for the ds_mat hand-off to the host Hungarian pool (model.py, FPM_COPY_KIND).
-extern "C" int fpm_memcpy_async(void* dst, const void* src, long bytes, int kind, void* stream) {
-    FPM_CHECK_ARG(bytes >= 0, "memcpy_async: negative size");
-    if (bytes == 0) return 0;
-    const hipError_t e = hipMemcpyAsync(dst, src, (size_t)bytes, (hipMemcpyKind)kind, (hipStream_t)stream);
-    if (e != hipSuccess) {
-        fpm::set_error("fpm_memcpy_async(kind %d): %s", kind, hipGetErrorString(e));
-        return 1;
-    }
-    return 0;
-}

@@ -277,330 +277,11 @@ __global__ __launch_bounds__(G2_THREADS, 1) void gemm_phase_kernel(GemmParams p)
     }
 }
 
-// ---- persistent form (the SplineConv product GEMM) -------------------------------------------
-// The same tiles, K loop and per-element accumulation order as gemm_phase_kernel<EPI_STORE, bf16>
-// (bit-identical outputs), with one workgroup per CU walking the XCD-chunked tile order
-// v = blockIdx.x, + gridDim.x, ... over the real tiles only (their count read from the plan).
-// A one-shot tile pays its prologue DMA latency, its LDS-staged epilogue and a workgroup launch
-// with nothing to overlap them (measured: ~40 % of a 768-deep tile's time).  Here the NEXT tile's
-// prologue (half-tiles 0..5) is issued BEFORE the current tile's epilogue, which stages one
-// 128 x 128 quadrant at a time through the two half-tile slots that prologue leaves free (buffer 1's
-// A1 and B1; 16-B chunks XOR-swizzled by row, no padding) and writes with buffer stores whose rows
-// past the group's end fall outside the buffer range (dropped).  The next tile starts with a full
-// vmcnt(0): counting the DMA past the epilogue's stores is unsafe (measured: stores, dropped ones
-// in particular, retire ahead of older LDS-DMA, and K-tile 0 then read stale half-tiles).  The
-// next tile's gather indices are loaded during K-tile 0.  Epilogue LDS accesses are inline asm
-// (the compiler would wait for the in-flight prologue DMA before them) behind raw s_barrier +
-// lgkmcnt(0) (__syncthreads() would drain it too).
-typedef unsigned int gp_u32x4_t __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ int remap_tile_v(int v, int nt, int mtiles) {
-    if (mtiles < REMAP_MIN) return v;
-    const int chunk = 4 * nt;
-    const int i = v >> 3;
-    return ((i / chunk) * 8 + (v & 7)) * chunk + (i % chunk);
-}
-__device__ __forceinline__ int remap_count(int nt, int mtiles) {
-    const int chunk = 4 * nt, t = nt * mtiles;
-    if (mtiles < REMAP_MIN) return t;
-    return (t + 8 * chunk - 1) / (8 * chunk) * (8 * chunk);
-}
-
-template <int N>
-__device__ __forceinline__ void gp_vmcnt() {
-    if constexpr (N == 0) FPM_VMCNT(0);
-    else if constexpr (N == 2) FPM_VMCNT(2);
-    else if constexpr (N == 4) FPM_VMCNT(4);
-    else if constexpr (N == 6) FPM_VMCNT(6);
-    else if constexpr (N == 8) FPM_VMCNT(8);
-    else static_assert(N < 0, "unsupported vmcnt");
-}
-
-template <int EPI>   // EPI_STORE only (a template so the header can be included by several units)
-__global__ __launch_bounds__(G2_THREADS, 1) void gemm_phase_persist_kernel(GemmParams p, const int* __restrict__ p_ntiles) {
-    static_assert(EPI == EPI_STORE, "the persistent kernel stores bf16 without an epilogue op");
-    constexpr int BN = 256;
-    __shared__ __attribute__((aligned(16))) unsigned char smem[8 * GP_HALF];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wr = wave >> 2, wc = wave & 3;
-    const int nt = (p.N + BN - 1) / BN;
-    const int mtiles = p_ntiles ? *p_ntiles : p.remap_mtiles;
-    const int nvirt = remap_count(nt, mtiles);
-    const bf16_t* A = (const bf16_t*)p.A;
-    // buffer descriptor of C (base, stride 0, num_records = bytes, the word-3 flags of
-    // __builtin_amdgcn_make_buffer_rsrc(..., 0x00020000)); an SGPR quad for the asm stores
-    typedef int gp_i32x4_t __attribute__((ext_vector_type(4)));
-    const unsigned long long cbase = (unsigned long long)(uintptr_t)p.Ct;
-    const gp_i32x4_t crs4 = {(int)(unsigned)cbase, (int)(unsigned)((cbase >> 32) & 0xffffu),
-                             (int)((long)p.M * p.ldc * 2), 0x00020000};
-
-    // wave-uniform tile description (only the first *p_ntiles table entries are walked, all real
-    // tiles); the table is read through the constant address space (scalar loads: it is not
-    // written while the kernel runs)
-    typedef const __attribute__((address_space(4))) int* cint_ptr;
-    const cint_ptr tinfo = (cint_ptr)(uintptr_t)p.tile_info;
-    const cint_ptr goff = (cint_ptr)(uintptr_t)p.group_off;
-    auto meta = [&](int v, int& group, int& row0, int& row_end, int& n0) -> bool {
-        const int q = remap_tile_v(v, nt, mtiles);
-        const int mtile = q / nt, ntile = q - mtile * nt;
-        if (mtile >= mtiles) return false;
-        group = tinfo[2 * mtile];
-        row0 = tinfo[2 * mtile + 1];
-        row_end = goff[group + 1];
-        n0 = ntile * BN;
-        return true;
-    };
-    auto next_tile = [&](int v, int& group, int& row0, int& row_end, int& n0) -> int {
-        while (v < nvirt && !meta(v, group, row0, row_end, n0)) v += gridDim.x;
-        return v;
-    };
-    // DMA sources: half-tile piece i of wave w = rows 8*(2w+i) + (lane>>3) of the half,
-    // K-chunk (lane&7) ^ ((row>>1)&7); 32-bit element offsets (the 64-bit pointers of the one-shot
-    // kernel cost 16 VGPRs the epilogue needs); the gathered row ids are loaded one tile ahead
-    int arow[2][2];                                       // [h][piece]
-    auto load_rows = [&](int row0, int row_end) {
-        int ltid = tid;                                   // opaque: row offsets not kept live
-        asm volatile("" : "+v"(ltid));
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                int gr = row0 + h * 128 + ((ltid >> 6) * 2 + i) * 8 + ((ltid & 63) >> 3);
-                gr = gr < row_end ? gr : row0;            // clamp: rows past the end are never stored
-                arow[h][i] = p.a_rows[gr];                // gathered rows (the launcher requires a_rows)
-            }
-    };
-    int aoff[2][2], boff[2];                              // [h][piece], [piece]
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int r = (wave * 2 + i) * 8 + (lane >> 3);
-        boff[i] = r * (int)p.ldb + ((lane & 7) ^ ((r >> 1) & 7)) * 8;
-    }
-    const bf16_t* Bt = (const bf16_t*)p.B;                // this tile's B rows n0.. (uniform)
-    auto set_src = [&](int group, int n0) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int r = (wave * 2 + i) * 8 + (lane >> 3);
-            const int kc = (lane & 7) ^ ((r >> 1) & 7);
-#pragma unroll
-            for (int h = 0; h < 2; ++h) aoff[h][i] = arow[h][i] * (int)p.lda + kc * 8;
-        }
-        Bt = (const bf16_t*)p.B + (long)group * p.sB_seg + (long)n0 * p.ldb;
-    };
-    auto issue = [&](int j, int slot) {
-        const int t = j >> 2;
-        unsigned char* dst = smem + ((t & 1) * 4 + slot) * GP_HALF + wave * 2048;
-        const int k0 = t * G2_BK;
-        // opaque copies of the offsets: no 64-bit induction pointers hoisted out of the K loop
-        // (LLVM's strength reduction kept 8 of them live and spilled)
-        int o0 = slot < 2 ? aoff[slot][0] : boff[0], o1 = slot < 2 ? aoff[slot][1] : boff[1];
-        asm volatile("" : "+v"(o0), "+v"(o1));
-        const bf16_t* base = slot < 2 ? A + k0 : Bt + (long)(slot - 2) * 128 * p.ldb + k0;
-        const bf16_t* s0p = base + o0;
-        const bf16_t* s1p = base + o1;
-        __builtin_amdgcn_global_load_lds((gbl_ptr_t)s0p, (lds_ptr_t)dst, 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((gbl_ptr_t)s1p, (lds_ptr_t)(dst + 1024), 16, 0, 0);
-    };
-    constexpr int SLOT[4] = {0, 2, 3, 1};
-    auto prologue = [&] {
-#pragma unroll
-        for (int j = 0; j < 6; ++j) issue(j, SLOT[j & 3]);
-    };
-
-    const int xr = (lane >> 1) & 7;
-    const int a_off = (wr * 64 + (lane & 15)) * 128;
-    const int b_off = (wc * 32 + (lane & 15)) * 128;
-    const int s0 = ((lane >> 4) ^ xr) * 16, s1 = ((4 + (lane >> 4)) ^ xr) * 16;
-    f32x4_t acc[2][2][4][2];
-    bf16x8_t a[2][4], b0[2][2], b1[2][2];
-    auto read_a = [&](int t, int h) {
-        const unsigned char* base = smem + ((t & 1) * 4 + h) * GP_HALF + a_off;
-#pragma unroll
-        for (int f = 0; f < 4; ++f) {
-            a[0][f] = *(const bf16x8_t*)(base + f * 2048 + s0);
-            a[1][f] = *(const bf16x8_t*)(base + f * 2048 + s1);
-        }
-    };
-    auto read_b = [&](int t, int g, bf16x8_t (&bb)[2][2]) {
-        const unsigned char* base = smem + ((t & 1) * 4 + 2 + g) * GP_HALF + b_off;
-#pragma unroll
-        for (int f = 0; f < 2; ++f) {
-            bb[0][f] = *(const bf16x8_t*)(base + f * 2048 + s0);
-            bb[1][f] = *(const bf16x8_t*)(base + f * 2048 + s1);
-        }
-    };
-    auto mfma = [&](f32x4_t (&c)[4][2], bf16x8_t (&bb)[2][2]) {
-        __builtin_amdgcn_s_barrier();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (GP_PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-            for (int fm = 0; fm < 4; ++fm)
-#pragma unroll
-                for (int fn = 0; fn < 2; ++fn)
-                    c[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kk][fm], bb[kk][fn], c[fm][fn], 0, 0, 0);
-        if (GP_PRIO) __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_s_barrier();
-    };
-    auto ktile = [&](int t, auto VM0, auto VM1, auto VM2, auto VM3, bool iss0, bool iss1, bool iss2, bool iss3) {
-        const int phi = 4 * t;
-        gp_vmcnt<decltype(VM0)::value>();
-        if (iss0) issue(phi + 6, SLOT[(0 + 6) & 3]);
-        read_a(t, 0);
-        read_b(t, 0, b0);
-        mfma(acc[0][0], b0);
-        gp_vmcnt<decltype(VM1)::value>();
-        if (iss1) issue(phi + 7, SLOT[(1 + 6) & 3]);
-        read_b(t, 1, b1);
-        mfma(acc[0][1], b1);
-        gp_vmcnt<decltype(VM2)::value>();
-        if (iss2) issue(phi + 8, SLOT[(2 + 6) & 3]);
-        read_a(t, 1);
-        mfma(acc[1][1], b1);
-        gp_vmcnt<decltype(VM3)::value>();
-        if (iss3) issue(phi + 9, SLOT[(3 + 6) & 3]);
-        mfma(acc[1][0], b0);
-    };
-    using V6 = std::integral_constant<int, 6>;
-    using V4 = std::integral_constant<int, 4>;
-    using V2 = std::integral_constant<int, 2>;
-    using V0 = std::integral_constant<int, 0>;
-    using VN = std::integral_constant<int, -1>;
-
-    // epilogue of one tile: quadrant (h, g) staged into slots 5 (rows 0-63) and 7 (rows 64-127),
-    // row r at (r & 63) * 256, 16-B chunk c8 at slot c8 ^ (r & 15).  A lane writes rows
-    // wr*64 + fm*16 + rg*4 + j (rg = lane >> 4) of column c = wc*32 + fn*16 + (lane & 15):
-    // chunk (wc*4 + fn*2 + b3) ^ (rg*4 + j) = ((wc ^ rg) << 2) + ((fn*2 + b3) ^ j), b3 = (lane >> 3) & 1,
-    // so every write is one of two per-lane bases (j even / odd) plus an immediate.
-    auto epilogue = [&](int row0, int row_end, int n0) {
-        // lane-derived bases recomputed here from an opaque copy of tid (not kept live through
-        // the K loop by loop-invariant hoisting)
-        int ltid = tid;
-        asm volatile("" : "+v"(ltid));
-        const int llane = ltid & 63, lwave = ltid >> 6;
-        const int rg = llane >> 4, b3 = (llane >> 3) & 1;
-        const unsigned lds_base = (unsigned)(uintptr_t)(lds_ptr_t)smem;
-        const int wbase = ((lwave >> 2) ? 7 : 5) * GP_HALF + rg * 4 * 256 + (((lwave & 3) ^ rg) << 6) + (llane & 7) * 2;
-        const int wb_even = wbase + b3 * 16, wb_odd = wbase + (b3 ^ 1) * 16;
-        // reads: r = it*32 + (tid >> 4), chunk tid & 15 -> one base plus an immediate per it
-        const int rbase = (ltid >> 4) * 256 + (((ltid & 15) ^ ((ltid >> 4) & 15)) << 4);
-        const int srow = ltid >> 4, scol = (ltid & 15) * 8;
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int g = 0; g < 2; ++g) {
-#pragma unroll
-                for (int fm = 0; fm < 4; ++fm)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-#pragma unroll
-                        for (int fn = 0; fn < 2; ++fn) {
-                            const int imm = fm * 16 * 256 + j * 256 + (((fn * 2) ^ (j & 2)) << 4);
-                            // inline asm: the compiler would put vmcnt(0) in front of an LDS
-                            // write it cannot tell apart from the in-flight prologue DMA
-                            asm volatile("ds_write_b16 %0, %1 offset:%2"
-                                         :: "v"(lds_base + (j & 1 ? wb_odd : wb_even)),
-                                            "v"((unsigned)f2bf(acc[h][g][fm][fn][j])), "i"(imm) : "memory");
-                        }
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                __builtin_amdgcn_s_barrier();
-                asm volatile("" ::: "memory");
-                gp_u32x4_t val[4];
-                asm volatile("ds_read_b128 %0, %4\n\t"
-                             "ds_read_b128 %1, %4 offset:%6\n\t"
-                             "ds_read_b128 %2, %5\n\t"
-                             "ds_read_b128 %3, %5 offset:%6\n\t"
-                             "s_waitcnt lgkmcnt(0)"
-                             : "=&v"(val[0]), "=&v"(val[1]), "=&v"(val[2]), "=&v"(val[3])
-                             : "v"(lds_base + 5 * GP_HALF + rbase), "v"(lds_base + 7 * GP_HALF + rbase),
-                               "i"(32 * 256)
-                             : "memory");
-                int voff[4], soff[4];
-#pragma unroll
-                for (int it = 0; it < 4; ++it) {
-                    const int rr = h * 128 + it * 32;                         // uniform part of the row
-                    const int gr = row0 + rr + srow;
-                    voff[it] = gr < row_end ? (srow * (int)p.ldc + scol) * 2 : (int)0x80000000u;
-                    soff[it] = (int)((((long)(row0 + rr)) * p.ldc + n0 + g * 128) * 2);
-                }
-                // inline asm with trailing wait states: a 16-B store reads its data VGPRs after
-                // issue, and the compiler let a VALU overwrite them right behind the builtin form
-                // (measured: the first dword of lanes 12-15 of each 16 took the next row index)
-                asm volatile("buffer_store_dwordx4 %0, %4, %8, %9 offen\n\t"
-                             "buffer_store_dwordx4 %1, %5, %8, %10 offen\n\t"
-                             "buffer_store_dwordx4 %2, %6, %8, %11 offen\n\t"
-                             "buffer_store_dwordx4 %3, %7, %8, %12 offen\n\t"
-                             "s_nop 4"
-                             :: "v"(val[0]), "v"(val[1]), "v"(val[2]), "v"(val[3]), "v"(voff[0]), "v"(voff[1]),
-                                "v"(voff[2]), "v"(voff[3]), "s"(crs4), "s"(soff[0]), "s"(soff[1]), "s"(soff[2]),
-                                "s"(soff[3])
-                             : "memory");
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                __builtin_amdgcn_s_barrier();
-                asm volatile("" ::: "memory");
-            }
-    };
-    auto zero_acc = [&] {
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int g = 0; g < 2; ++g)
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) acc[h][g][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    };
-
-    const int ktiles = p.K / G2_BK;                       // >= 3 (checked by the launcher)
-    int gc, r0c, rec, n0c;                                // current tile
-    int v = next_tile(blockIdx.x, gc, r0c, rec, n0c);
-    if (v >= nvirt) return;
-    int gn = 0, r0n = 0, ren = 0, n0n = 0;                // next tile
-    int vn = next_tile(v + gridDim.x, gn, r0n, ren, n0n);
-    load_rows(r0c, rec);
-    set_src(gc, n0c);
-    prologue();
-    zero_acc();
-    for (;;) {
-        // everything older is retired here: the prologue (issued before the previous epilogue, so
-        // landed by now) and the previous epilogue's stores (stores may retire out of order with
-        // the LDS-DMA, so K-tile 0 cannot count past them)
-        FPM_VMCNT(0);
-        __builtin_amdgcn_s_barrier();
-        if (GP_STAGGER && wr == 1) __builtin_amdgcn_s_barrier();
-        if (vn < nvirt) load_rows(r0n, ren);              // the next tile's gather rows, used at its prologue
-        int t = 0;
-        for (; t < ktiles - 2; ++t) ktile(t, V6{}, V6{}, V6{}, V6{}, true, true, true, true);
-        ktile(t, V6{}, V6{}, V6{}, V4{}, true, true, false, false);
-        ktile(t + 1, V2{}, V0{}, VN{}, VN{}, false, false, false, false);
-        if (GP_STAGGER && wr == 0) __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_s_barrier();                     // every wave is past its last LDS read
-        const bool more = vn < nvirt;
-        int g2 = 0, r02 = 0, re2 = 0, n02 = 0, v2 = nvirt;
-        if (more) {
-            set_src(gn, n0n);
-            v2 = next_tile(vn + gridDim.x, g2, r02, re2, n02);
-            prologue();                                   // lands under the epilogue below
-        }
-        epilogue(r0c, rec, n0c);
-        if (!more) break;
-        gc = gn; r0c = r0n; rec = ren; n0c = n0n;
-        gn = g2; r0n = r02; ren = re2; n0n = n02;
-        vn = v2;
-        zero_acc();
-    }
-}
-
 #undef FPM_VMCNT
 
 // launch policy: the phase kernel for 256-wide tiles with >= 2 K-tiles; FPM_GEMM_PHASE=0 (or
 // fpm_set_gemm_phase(0)) keeps gemm_big_kernel<256> -- an A/B switch, both are bit-identical
 int& gemm_phase_flag();
 inline bool use_gemm_phase(int K) { return gemm_phase_flag() != 0 && K / G2_BK >= GP_MIN_KTILES; }
-// the persistent product GEMM (bf16, no bias / epilogue op): env FPM_GEMM_PERSIST or
-// fpm_set_tuning("gemm_persist", v)
-int& gemm_persist_flag();
-int gemm_persist_grid();
 
 }  // namespace fpm

@@ -212,30 +212,8 @@ __global__ __launch_bounds__(1024) void gnn_layer_kernel(const float* __restrict
 
 // v[p] = classifier(emb[p]) (ngm.py:368), written as s[b][i][j] = v[b][j*n1max + i] (ngm.py:369).
 // With vpart (the last GNN layer's w[0:16] . x1, fused there) only channel 16 (its Sinkhorn) is read.
-__global__ __launch_bounds__(256) void node_classifier_kernel(const float* __restrict__ X, int n1max, int n2max,
-                                                              const float* __restrict__ w, const float* __restrict__ bias,
-                                                              const float* __restrict__ vpart, float* __restrict__ s,
-                                                              int B) {
-    int d, b;
-    if (!pair_block(n2max, B, b, d)) return;
-    const long N = (long)n1max * n2max;
-    for (int i = threadIdx.x; i < n1max; i += 256) {
-        const long p = (long)d * n1max + i;
-        float acc;
-        if (vpart) {
-            acc = fmaf(w[16], X[(long)b * 17 * N + 16L * N + p], vpart[(long)b * N + p]);
-        } else {
-            acc = 0.f;
-#pragma unroll
-            for (int c = 0; c < 17; ++c) acc += w[c] * X[(long)b * 17 * N + (long)c * N + p];
-        }
-        s[(long)b * N + (long)i * n2max + d] = acc + bias[0];
-    }
-}
-
-// The same on 64 x 64 (d, i) tiles transposed through LDS: reads along i and writes s along d are
-// both coalesced (the per-(pair, d) form wrote each value to its own cache line, 4 B per lane at
-// a 4 n2max-byte stride).  Same arithmetic per element, bit-identical.
+// 64 x 64 (d, i) tiles transposed through LDS: reads along i and writes s along d are both
+// coalesced (a per-(pair, d) form wrote each value to its own cache line).
 __global__ __launch_bounds__(256) void node_classifier_t_kernel(const float* __restrict__ X, int n1max, int n2max,
                                                                 const float* __restrict__ w,
                                                                 const float* __restrict__ bias,
@@ -274,16 +252,6 @@ __global__ __launch_bounds__(256) void node_classifier_t_kernel(const float* __r
 
 }  // namespace
 
-// node classifier through the LDS transpose (1, default) or the per-(pair, d) form (0);
-// env FPM_NODECLS_T or fpm_set_tuning("nodecls_t", v)
-int& nodecls_t_flag() {
-    static int on = [] {
-        const char* e = getenv("FPM_NODECLS_T");
-        return e ? atoi(e) : 1;
-    }();
-    return on;
-}
-
 extern "C" int fpm_kron_gnn_layer_fwd(const float* X, int C, int B, int n1max, int n2max, const int* ptr1,
                                       const int* nbr1, const int* ptr2, const int* nbr2, const int* n1,
                                       const int* n2, const float* params, float* Xout, float* zbuf,
@@ -309,14 +277,10 @@ extern "C" int fpm_gnn_param_count(int C) { return C == 1 ? GnnPack<1>::total : 
 extern "C" int fpm_node_classifier(const float* X, int B, int n1max, int n2max, const float* w, const float* bias,
                                    const float* vpart, float* s, void* stream) {
     if (B == 0) return 0;
-    if (nodecls_t_flag() && B <= 65535) {
-        const dim3 grid((unsigned)((n1max + 63) / 64), (unsigned)((n2max + 63) / 64), (unsigned)B);
-        hipLaunchKernelGGL(node_classifier_t_kernel, grid, dim3(256), 0, (hipStream_t)stream, X, n1max, n2max, w, bias,
-                           vpart, s);
-        return fpm::check_launch("fpm_node_classifier");
-    }
-    hipLaunchKernelGGL(node_classifier_kernel, dim3(pair_grid(n2max, B)), dim3(256), 0, (hipStream_t)stream, X, n1max,
-                       n2max, w, bias, vpart, s, B);
+    FPM_CHECK_ARG(B <= 65535, "node_classifier: B must be <= 65535");
+    const dim3 grid((unsigned)((n1max + 63) / 64), (unsigned)((n2max + 63) / 64), (unsigned)B);
+    hipLaunchKernelGGL(node_classifier_t_kernel, grid, dim3(256), 0, (hipStream_t)stream, X, n1max, n2max, w, bias,
+                       vpart, s);
     return fpm::check_launch("fpm_node_classifier");
 }
 

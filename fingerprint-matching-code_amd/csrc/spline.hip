@@ -143,7 +143,7 @@ __global__ __launch_bounds__(256) void plan_blkcount_kernel(const int* __restric
 // one block: per-cell exclusive scan over blocks (in place), cell offsets, GEMM tile table, and the
 // exclusive scan of in-degrees -> dst CSR pointers.
 // The number of real tiles is also stored at *count (cell_off[27] for 128-row tiles, [28] for
-// 256-row tiles): the persistent product GEMM walks only those.
+// 256-row tiles).
 __device__ void build_tile_table(const int* coff, const int* cell_tot, int* tile_off, int tb, int* tile_info,
                                  int max_tiles, int* count) {
     const int tid = threadIdx.x;
@@ -573,13 +573,11 @@ __global__ __launch_bounds__(PG_THREADS) void plan_graph_rank_kernel(const int* 
 
 // out[v] = max_{in-edges e} sum_s basis[e,s] * Y[row(src_e, cell_s)] + Y[root row v] + bias
 //   mode 0: relu(.) ; mode 1: xres[v] + 0.1 * (.)   (+ optional per-pair column scale on out_t)
-// One wave per node, 12 channels per lane (3 x 4 contiguous).
-// PF: the node's in-edge row ids / basis weights are loaded once into lanes (one per edge) and
-// read back with v_readlane, and two in-edges' 8 product rows are loaded together (24 loads in
-// flight per lane instead of 12 behind a scalar rows4 load); same fma / max order, bit-identical.
+// One wave per node, 12 channels per lane (3 x 4 contiguous).  (An in-edge prefetch variant --
+// row ids in lanes, two edges' 8 product rows in flight -- measured neutral and was dropped.)
 // ARG (training forward): also record, per (node, channel), the CSR slot of the in-edge attaining
 // the max (the first one in CSR order, -1 without in-edges) for the scatter backward.
-template <typename T, int NPB = 4, bool PF = false, bool ARG = false>
+template <typename T, int NPB = 4, bool ARG = false>
 __global__ __launch_bounds__(64 * NPB) void combine_kernel(const T* __restrict__ Y, const int* __restrict__ cell_off,
                                                       const float* __restrict__ bias,
                                                       const int* __restrict__ dst_ptr, const int4* __restrict__ rows4,
@@ -610,82 +608,6 @@ __global__ __launch_bounds__(64 * NPB) void combine_kernel(const T* __restrict__
             am[t][j] = -1;
         }
     (void)am;
-    if constexpr (PF) {
-        const int deg = end - beg;
-        int4 rl = make_int4(0, 0, 0, 0);
-        float4 bl = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (lane < deg) {
-            rl = rows4[beg + lane];
-            bl = basis4[beg + lane];
-        }
-        auto rd = [](int v, int k) { return __builtin_amdgcn_readlane(v, k); };
-        auto rdf = [](float v, int k) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k)); };
-        // edge k of the node: product-row pointers and basis weights (wave-uniform)
-        auto edge = [&](int k, const T* (&y)[4], float (&bs)[4]) {
-            int4 r;
-            float4 b4;
-            if (k < 64) {
-                r = make_int4(rd(rl.x, k), rd(rl.y, k), rd(rl.z, k), rd(rl.w, k));
-                b4 = make_float4(rdf(bl.x, k), rdf(bl.y, k), rdf(bl.z, k), rdf(bl.w, k));
-            } else {
-                r = rows4[beg + k];
-                b4 = basis4[beg + k];
-            }
-            y[0] = Y + (long)r.x * 768; y[1] = Y + (long)r.y * 768;
-            y[2] = Y + (long)r.z * 768; y[3] = Y + (long)r.w * 768;
-            bs[0] = b4.x; bs[1] = b4.y; bs[2] = b4.z; bs[3] = b4.w;
-        };
-        int k = 0;
-        for (; k + 2 <= deg; k += 2) {
-            const T* ya[4];
-            const T* yb[4];
-            float ba[4], bb[4];
-            edge(k, ya, ba);
-            edge(k + 1, yb, bb);
-            float a[3][4][4], c[3][4][4];
-#pragma unroll
-            for (int t = 0; t < 3; ++t)
-#pragma unroll
-                for (int s4 = 0; s4 < 4; ++s4) {
-                    fpm::load4(ya[s4] + 4 * lane + 256 * t, a[t][s4]);
-                    fpm::load4(yb[s4] + 4 * lane + 256 * t, c[t][s4]);
-                }
-#pragma unroll
-            for (int t = 0; t < 3; ++t)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    float msg = ba[0] * a[t][0][j];
-                    msg = fmaf(ba[1], a[t][1][j], msg);
-                    msg = fmaf(ba[2], a[t][2][j], msg);
-                    msg = fmaf(ba[3], a[t][3][j], msg);
-                    m[t][j] = fmaxf(m[t][j], msg);
-                    float msg2 = bb[0] * c[t][0][j];
-                    msg2 = fmaf(bb[1], c[t][1][j], msg2);
-                    msg2 = fmaf(bb[2], c[t][2][j], msg2);
-                    msg2 = fmaf(bb[3], c[t][3][j], msg2);
-                    m[t][j] = fmaxf(m[t][j], msg2);
-                }
-        }
-        if (k < deg) {
-            const T* ya[4];
-            float ba[4];
-            edge(k, ya, ba);
-#pragma unroll
-            for (int t = 0; t < 3; ++t) {
-                float a[4][4];
-#pragma unroll
-                for (int s4 = 0; s4 < 4; ++s4) fpm::load4(ya[s4] + 4 * lane + 256 * t, a[s4]);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    float msg = ba[0] * a[0][j];
-                    msg = fmaf(ba[1], a[1][j], msg);
-                    msg = fmaf(ba[2], a[2][j], msg);
-                    msg = fmaf(ba[3], a[3][j], msg);
-                    m[t][j] = fmaxf(m[t][j], msg);
-                }
-            }
-        }
-    } else
     for (int e = beg; e < end; ++e) {
         const int4 r = rows4[e];
         const float4 bs = basis4[e];
@@ -974,17 +896,6 @@ int& combine_npb_flag() {
     return u;
 }
 
-// combine in-edge prefetch + 2-edge loads (1) or the per-edge loop (0, default); bit-identical,
-// measured neutral at C3 (26.3 K vs 26.3 K pairs/s, interleaved A/B).  Env FPM_COMBINE_PF or
-// fpm_set_tuning("combine_pf", v)
-int& combine_pf_flag() {
-    static int u = [] {
-        const char* e = getenv("FPM_COMBINE_PF");
-        return e ? atoi(e) : 0;
-    }();
-    return u;
-}
-
 extern "C" long fpm_spline_plan_bytes(long E, long num_nodes) {
     return plan_layout(E, num_nodes).total;
 }
@@ -1154,10 +1065,6 @@ extern "C" int fpm_spline_conv_fwd_argmax(int dtype, const void* x_op, const voi
             (void)hipEventRecord(rec.a, st);
         }
         if (dtype == 0) hipLaunchKernelGGL((gemm_kernel<float, false>), grid, dim3(GTHREADS), 0, st, p);
-        else if (use_gemm_phase(D) && gemm_persist_flag() && D / G2_BK >= 3 && D % 256 == 0 &&
-                 (long)p.M * p.ldc * 2 < (1L << 31))
-            hipLaunchKernelGGL(gemm_phase_persist_kernel<EPI_STORE>, dim3(gemm_persist_grid()), dim3(G2_THREADS), 0, st, p,
-                               (const int*)(w + L.cell_off) + NCELL + 2);
         else if (use_gemm_phase(D)) hipLaunchKernelGGL((gemm_phase_kernel<EPI_STORE, false>), grid, dim3(G2_THREADS), 0, st, p);
         else hipLaunchKernelGGL((gemm_big_kernel<256, EPI_STORE, false>), grid, dim3(G2_THREADS), 0, st, p);
         if (g_prof_on && g_prof_rows && rec.slot < PROF_MAX) {
@@ -1168,16 +1075,14 @@ extern "C" int fpm_spline_conv_fwd_argmax(int dtype, const void* x_op, const voi
     {
         const long graphs = (num_nodes + nmax - 1) / nmax;
         const int npb = combine_npb_flag();
-        const bool pf = combine_pf_flag() != 0;
-#define FPM_COMB1(T_, N_, P_)                                                                                    \
-    hipLaunchKernelGGL((combine_kernel<T_, N_, P_>), dim3((unsigned)(((graphs + 7) / 8) * 8 * ((nmax + N_ - 1) / N_))), \
+#define FPM_COMB(T_, N_)                                                                                         \
+    hipLaunchKernelGGL((combine_kernel<T_, N_>), dim3((unsigned)(((graphs + 7) / 8) * 8 * ((nmax + N_ - 1) / N_))), \
                        dim3(64 * N_), 0, st, (const T_*)y_ws, (const int*)(w + L.cell_off), bias,                \
                        (const int*)(w + L.dst_ptr), (const int4*)(w + L.rows4), (const float4*)(w + L.basis4),   \
                        num_nodes, nmax, nvalid, mode, xres, cscale, out_f, (T_*)out_t)
-#define FPM_COMB(T_, N_) do { if (pf) FPM_COMB1(T_, N_, true); else FPM_COMB1(T_, N_, false); } while (0)
         if (argmax) {
 #define FPM_COMBA(T_)                                                                                            \
-    hipLaunchKernelGGL((combine_kernel<T_, 4, false, true>), dim3((unsigned)(((graphs + 7) / 8) * 8 * ((nmax + 3) / 4))), \
+    hipLaunchKernelGGL((combine_kernel<T_, 4, true>), dim3((unsigned)(((graphs + 7) / 8) * 8 * ((nmax + 3) / 4))), \
                        dim3(256), 0, st, (const T_*)y_ws, (const int*)(w + L.cell_off), bias,                    \
                        (const int*)(w + L.dst_ptr), (const int4*)(w + L.rows4), (const float4*)(w + L.basis4),   \
                        num_nodes, nmax, nvalid, mode, xres, cscale, out_f, (T_*)out_t, argmax)
@@ -1189,7 +1094,6 @@ extern "C" int fpm_spline_conv_fwd_argmax(int dtype, const void* x_op, const voi
             if (npb == 16) FPM_COMB(bf16_t, 16); else if (npb == 8) FPM_COMB(bf16_t, 8); else FPM_COMB(bf16_t, 4);
         }
 #undef FPM_COMB
-#undef FPM_COMB1
     }
     return check_launch("fpm_spline_conv_fwd");
 }
@@ -1276,6 +1180,8 @@ extern "C" int fpm_profile_enable(int on) {
     g_prof_on = on != 0;
     return 0;
 }
+
+extern "C" int fpm_profile_enabled(void) { return g_prof_on ? 1 : 0; }
 
 // Sum of the recorded edge-GEMM durations (ms) and algorithmic FLOPs since the last read.
 extern "C" int fpm_profile_read(double* ms_total, double* flops_total, int* count) {

@@ -117,36 +117,25 @@ class Net(nn.Module):
         self.compute_ke = compute_ke
         self._pack = None
         self._pack_key = None
+        self._pack_gen = 0
         self._pinned = None
         self._stream_cache = {}
+        # FPM_STREAMS: compute streams of the chunk pipeline (1 = single-stream profiling runs)
         self.n_streams = max(1, int(os.environ.get("FPM_STREAMS", "2")))
+        # the last chunk halved this many times: the two streams' last chunks land together, so the
+        # host Hungarian's tail after the GPU is their (short) LSA
         self.tail_splits = int(os.environ.get("FPM_TAIL", "2"))
-        self.head_splits = int(os.environ.get("FPM_HEAD", "0"))
-        # FPM_ZERO_COPY=1: soft_topk writes ds_mat straight into pinned host memory instead of a
-        # stream copy.  Measured slower (21.2K -> 19.7K pairs/s: the kernel stalls on PCIe writes
-        # on the critical path), so off by default.
-        self.zero_copy = os.environ.get("FPM_ZERO_COPY", "0") == "1"
-        self.copy_stream = os.environ.get("FPM_COPY_STREAM", "1") == "1"
-        # > 0: ds_mat D2H on this many workgroups (fpm_copy_async) instead of the runtime's blit
-        self.copy_blocks = int(os.environ.get("FPM_COPY_BLOCKS", "0"))
-        # > 0: ds_mat D2H through hipMemcpyAsync with this copy kind (fpm_memcpy_async; 1024 = the
-        # no-compute-unit device-to-device kind, i.e. a copy engine instead of the blit kernel)
-        self.copy_kind = int(os.environ.get("FPM_COPY_KIND", "0"))
-        # defer each chunk's ds_mat D2H until the side-0 spline plan of the chunk queued two places
-        # later (same compute stream) has run: that latency-bound kernel otherwise runs beside the
-        # copy's blit kernel and stalls ~25x
+        # defer each chunk's ds_mat D2H until the spline plans of the chunk queued two places later
+        # (same compute stream) have run: those latency-bound kernels otherwise run beside the
+        # copy's blit kernel and stall ~10x
         self.copy_defer = int(os.environ.get("FPM_COPY_DEFER", "1"))
         if self.copy_defer not in (0, 1):
             raise ValueError("FPM_COPY_DEFER must be 0 or 1")
-        self._plan_events = None
-        # FPM_OFFSET=1: the second stream starts its first chunk after the first chunk's SplineConv,
-        # so the streams' phases interleave (MFMA-heavy SplineConv beside the VALU / memory-bound GNN,
-        # Sinkhorn and soft top-k) instead of running the same stages side by side
-        self.stream_offset = int(os.environ.get("FPM_OFFSET", "0"))
-        self._offset_events = None
-        # the host thread waits for each chunk's ds_mat with a sleeping (not spinning) event wait,
-        # leaving its core to the Hungarian pool
-        self.blocking_wait = os.environ.get("FPM_BLOCKING_WAIT", "1") == "1"
+        # FPM_GRAPHS=1: multi-chunk inference forwards replay HIP graphs captured per (batch, chunk)
+        # (host enqueue 8 -> 1 ms per 1024 pairs; the GPU stage measured 4 % slower than eager
+        # launches, so off by default; fpm.parallel.ShardedNet turns it on); see run()
+        self.use_graphs = os.environ.get("FPM_GRAPHS", "0") == "1"
+        self._gstate = None
         self._keep_feats = False
         self._stage_timing = os.environ.get("FPM_STAGE_TIMING", "0") == "1"
         self.stage_times = {}
@@ -250,23 +239,26 @@ class Net(nn.Module):
         d["mc_fcw"] = g("match_cls.fc.weight").reshape(-1).contiguous()
         d["mc_fcb"] = g("match_cls.fc.bias")
         self._pack, self._pack_key = d, key
+        self._pack_gen += 1
         return d
 
     # ------------------------------------------------------------------------------------------
-    def _spline_side(self, wp, bt, side, cscale, x_op=None):
+    def plans(self, bt):
+        """Spline plans of both sides of ``bt`` (cell masks, product-row tables, dst CSR): shared by
+        the two SplineConv layers and the GNN layers of a forward."""
+        return [ops.spline_plan(bt.src[s], bt.dst[s], bt.pseudo[s], bt.B * bt.nmax[s], bt.nmax[s],
+                                bt.max_graph_edges(s)) for s in range(2)]
+
+    def _spline_side(self, wp, bt, side, cscale, x_op=None, plan=None):
         """SiameseSConvOnNodes over one side's batch (spline_conv.py:28-57) -> operand rows.
         ``x_op``: this side's bf16 operand rows when the caller cast the whole batch up front."""
         dev = bt.device
         op = torch.bfloat16 if self.dtype_mode == "bf16" else torch.float32
         nn_ = bt.B * bt.nmax[side]
         E = bt.E[side]
-        plan = ops.spline_plan(bt.src[side], bt.dst[side], bt.pseudo[side], nn_, bt.nmax[side],
-                               bt.max_graph_edges(side))
-        # copy deferral: the previous-but-one chunk's D2H starts after this side-0 plan
-        if side == 0 and self._plan_events is not None:
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(dev))
-            self._plan_events.append(ev)
+        if plan is None:
+            plan = ops.spline_plan(bt.src[side], bt.dst[side], bt.pseudo[side], nn_, bt.nmax[side],
+                                   bt.max_graph_edges(side))
         if side == 0 and bt.shared0 and bt.B > 1:
             return (plan,) + self._spline_shared(wp, bt, cscale)
         x0 = bt.x[side]
@@ -311,8 +303,6 @@ class Net(nn.Module):
         op = torch.bfloat16 if self.afau_mode in ("bf16", "bf16s") else torch.float32
         E, FF = C.AFAU_EMB, C.AFAU_FF
         x3 = self.afau_mode == "bf16x3"
-        mask = int(os.environ.get("FPM_AFAU_X3_MASK", "7"))
-        kx = lambda bit, kp: 3 * kp if mask & bit else kp
         rows = nb_ * P_
         o1f = torch.empty(rows, E, device=dev, dtype=torch.float32)
         KE = E if op == torch.float32 else C.AFAU_EMB_PAD      # bf16 operand copy: zero-padded K
@@ -327,10 +317,10 @@ class Net(nn.Module):
         if x3:
             o13 = ops.split_bf16x3(o1f, C.AFAU_EMB_PAD)
             hf = torch.empty(rows, FF, device=dev, dtype=torch.float32)
-            ops.gemm(o13, wp[blk + "_W1"], rows, FF, kx(2, C.AFAU_EMB_PAD), o13.shape[1], o13.shape[1],
+            ops.gemm(o13, wp[blk + "_W1"], rows, FF, 3 * C.AFAU_EMB_PAD, o13.shape[1], o13.shape[1],
                      epi=ops.EPI_RELU, bias=wp[blk + "_b1"], out_f=hf, ldc=FF)
             h3 = ops.split_bf16x3(hf, FF)
-            ops.gemm(h3, wp[blk + "_W2"], rows, E, kx(4, FF), h3.shape[1], h3.shape[1], bias=wp[blk + "_b2"],
+            ops.gemm(h3, wp[blk + "_W2"], rows, E, 3 * FF, h3.shape[1], h3.shape[1], bias=wp[blk + "_b2"],
                      out_f=ff, ldc=E)
         else:
             hbuf = torch.empty(rows, FF, device=dev, dtype=op)
@@ -342,23 +332,31 @@ class Net(nn.Module):
         ops.instnorm(o1f, nb_, P_, E, wp[blk + "_n2w"], wp[blk + "_n2b"], in2=ff, gmax=gm)
         return gm
 
-    def _afau_col(self, wp, bt):
-        """The AFA-U column block for every distinct n2 of a batch: (n2u, gmax per n2u, n2max).
-        The column block sees a = one-hot rows and b = zero rows, so k = v = 0 and its attention
-        output is exactly the combine bias (afau.py:99-142): its result depends on n2 and the batch's
-        n2max only, not on ss.  A forward computes it once per distinct n2 and gathers it for every
-        pair and pipeline chunk -- the same arithmetic on the same inputs, bit-identical to the
-        per-pair evaluation."""
-        if os.environ.get("FPM_AFAU_COLDEDUP", "1") == "1":
-            n2u = np.unique(bt.n_host[1].numpy())
-        else:
-            n2u = bt.n_host[1].numpy()
+    @staticmethod
+    def _afau_col_index(bt):
+        """(distinct n2 values, their device copy, per-pair gather index or None) of a batch."""
+        n2u = np.unique(bt.n_host[1].numpy())
         n2u_d = torch.as_tensor(n2u, dtype=torch.int32).to(bt.device, non_blocking=True)
-        return n2u, self._afau_block(wp, "col", len(n2u), bt.n2max, n2u_d=n2u_d), bt.n2max
+        n2c = bt.n_host[1].numpy()
+        inv = None
+        if len(n2u) != len(n2c) or not np.array_equal(n2u, n2c):
+            inv = torch.as_tensor(np.searchsorted(n2u, n2c), dtype=torch.long).to(bt.device, non_blocking=True)
+        return n2u, n2u_d, inv
 
-    def _afau(self, wp, ss, bt, col=None):
-        """AFA-U k regression (ngm.py:386-412) -> ks (B,).  ``col``: the forward's _afau_col result
-        (computed here for this batch when None)."""
+    def _afau_col(self, wp, bt, idx=None):
+        """The AFA-U column block for every distinct n2 of a batch: (n2u, gmax per n2u, n2max, gather
+        index or None).  The column block sees a = one-hot rows and b = zero rows, so k = v = 0 and
+        its attention output is exactly the combine bias (afau.py:99-142): its result depends on n2
+        and the batch's n2max only, not on ss.  A forward computes it once per distinct n2 and
+        gathers it for every pair and pipeline chunk -- the same arithmetic on the same inputs,
+        bit-identical to the per-pair evaluation.  The host-to-device index copies happen here, once
+        per batch (``idx`` = _afau_col_index(bt), computed before a graph capture)."""
+        n2u, n2u_d, inv = idx if idx is not None else self._afau_col_index(bt)
+        return n2u, self._afau_block(wp, "col", len(n2u), bt.n2max, n2u_d=n2u_d), bt.n2max, inv
+
+    def _afau(self, wp, ss, bt, col=None, b0=0):
+        """AFA-U k regression (ngm.py:386-412) -> ks (B,).  ``col``: the _afau_col result of the
+        forward's batch, whose pairs [b0, b0 + B) this (sub-)batch is (computed here when None)."""
         dev = ss.device
         B, n1max, n2max = bt.B, bt.n1max, bt.n2max
         # f32 / bf16x3: fp32 activations; bf16 / bf16s: bf16 FFN operands
@@ -373,23 +371,16 @@ class Net(nn.Module):
         ops.crossset_attn(ss, bt.n2, wp["row_Wv"], wp["row_mix1w"], wp["row_mix1b"], wp["row_mix2w"],
                           wp["row_mix2b"], att, split=split)
         mh = torch.empty(B * n1max, E, device=dev, dtype=torch.float32)
-        # diagnostic: FPM_AFAU_X3_MASK selects which of (combine, W1, W2) use the three split terms;
-        # the others multiply the hi parts only (plain bf16 products)
-        mask = int(os.environ.get("FPM_AFAU_X3_MASK", "7"))
-        kx = lambda bit, kp: 3 * kp if mask & bit else kp
         if x3:
             att = ops.split_bf16x3(att, HD)
         # bf16s: hi*W_hi + lo*W_hi (2 terms; the W_lo term changed nothing measurable, +0.7 % time)
-        kc = int(os.environ.get("FPM_AFAU_SPLIT_TERMS", "2")) * HD if split else (kx(1, HD) if x3 else HD)
+        kc = 2 * HD if split else (3 * HD if x3 else HD)
         ops.gemm(att, wp["row_Wc"], B * n1max, E, kc, att.shape[1], att.shape[1], bias=wp["row_bc"], out_f=mh, ldc=E)
         g_row = self._afau_block(wp, "row", B, n1max, mh=mh)
         if col is None or col[2] != n2max:
-            col = self._afau_col(wp, bt)
-        n2u, gm_u, _ = col
-        n2c = bt.n_host[1].numpy()
-        inv = np.searchsorted(n2u, n2c) if len(n2u) != len(n2c) or not np.array_equal(n2u, n2c) else None
-        g_col = gm_u if inv is None else gm_u.index_select(0, torch.as_tensor(inv, dtype=torch.long).to(
-            dev, non_blocking=True))
+            col, b0 = self._afau_col(wp, bt), 0
+        n2u, gm_u, _, inv = col
+        g_col = gm_u if inv is None else gm_u.index_select(0, inv[b0:b0 + B])
         ks = torch.empty(B, device=dev, dtype=torch.float32)
         ops.afau_head(g_row, g_col, B, E, wp["final_row0w"], wp["final_row0b"], wp["final_row2w"],
                       wp["final_row2b"], wp["final_col0w"], wp["final_col0b"], wp["final_col2w"], wp["final_col2b"], ks)
@@ -439,10 +430,11 @@ class Net(nn.Module):
                  C.GLOBAL_STATE_DIM, epi=ops.EPI_TANH, bias=wp["aff_b"], out_f=coef)
         return gw, coef
 
-    def run_gpu_stage(self, bt, keep_feats=False, s_out=None, ss_out=None, gc=None, x_ops=(None, None)):
-        """Everything up to ds_mat on the GPU.  Returns a dict of device tensors.  ``gc``: this
+    def run_gpu_stage(self, bt, keep_feats=False, s_out=None, ss_out=None, gc=None, x_ops=(None, None), plans=None):
+        """Everything up to ss on the GPU.  Returns a dict of device tensors.  ``gc``: this
         batch's rows of global_coef() when computed for a parent batch; ``x_ops``: its rows of the
-        parent's bf16 operand copies of the node features (cast once per forward)."""
+        parent's bf16 operand copies of the node features (cast once per forward); ``plans``:
+        plans(bt) when already computed."""
         keep_feats = keep_feats or self.compute_ke
         self._keep_feats = keep_feats
         if self._stage_timing:
@@ -454,13 +446,11 @@ class Net(nn.Module):
         N = n1max * n2max
         gw, coef = gc if gc is not None else self.global_coef(bt)
         self._mark("coef")
-        plan0, x1c, f1 = self._spline_side(wp, bt, 0, coef, x_ops[0])
-        plan1, x2, f2 = self._spline_side(wp, bt, 1, None, x_ops[1])
+        pl = plans if plans is not None else self.plans(bt)
+        plan0, x1c, f1 = self._spline_side(wp, bt, 0, coef, x_ops[0], pl[0])
+        self._mark("splineconv0")
+        plan1, x2, f2 = self._spline_side(wp, bt, 1, None, x_ops[1], pl[1])
         self._mark("splineconv")
-        if self._offset_events is not None:
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(dev))
-            self._offset_events.append(ev)
         # Kp^T per pair: emb0[b][j][i] = softplus((x1_i o c) . x2_j) - 0.5 on the valid block (ngm.py:277-321)
         X = torch.empty(B, 1, n2max, n1max, device=dev, dtype=torch.float32)
         ops.gemm(x2, x1c, n2max, n1max, C.NODE_FEATURE_DIM, C.NODE_FEATURE_DIM, C.NODE_FEATURE_DIM, batch=B,
@@ -499,16 +489,19 @@ class Net(nn.Module):
     def _streams(self, dev):
         key = str(dev)
         if key not in self._stream_cache:
-            # FPM_STREAM_PRIO=1: compute streams at high priority (the ds_mat copy stream stays at
-            # the default) -- A/B switch for the copy blit's interference
-            prio = -1 if os.environ.get("FPM_STREAM_PRIO", "0") == "1" else 0
-            self._stream_cache[key] = [torch.cuda.Stream(dev, priority=prio) for _ in range(self.n_streams)]
+            self._stream_cache[key] = [torch.cuda.Stream(dev) for _ in range(self.n_streams)]
         return self._stream_cache[key]
 
     def _lsa_streams(self, dev):
         key = "lsa:" + str(dev)
         if key not in self._stream_cache:
             self._stream_cache[key] = [torch.cuda.Stream(dev) for _ in range(2)]
+        return self._stream_cache[key]
+
+    def _copy_stream(self, dev):
+        key = "copy:" + str(dev)
+        if key not in self._stream_cache:
+            self._stream_cache[key] = torch.cuda.Stream(dev)
         return self._stream_cache[key]
 
     def pipeline_chunks(self, B):
@@ -520,73 +513,41 @@ class Net(nn.Module):
         return max(1, min(8, B // 128))
 
     def _enqueue_copy(self, dev, b0, b1, o, done, after=None):
-        """ds_mat[b0:b1] -> pinned host memory on the copy stream once ``done`` (and ``after``, if
-        given) have fired; returns the copy's completion event."""
+        """ds_mat[b0:b1] -> pinned host memory on the copy stream (the copy is a blit kernel: on a
+        stream of its own it does not hold back the next chunk queued on a compute stream) once
+        ``done`` (and ``after``, if given) have fired; returns the copy's completion event, which
+        the host thread waits on with a sleeping (not spinning) wait, leaving its core to the
+        Hungarian pool."""
         cs = self._copy_stream(dev)
         cs.wait_event(done)
         if after is not None:
             cs.wait_event(after)
         with torch.cuda.stream(cs):
-            if self.copy_kind > 0:
-                ops.memcpy_async(self._pinned[b0:b1], o["ds_mat"][b0:b1], self.copy_kind)
-            elif self.copy_blocks > 0:
-                ops.copy_async(self._pinned[b0:b1], o["ds_mat"][b0:b1], self.copy_blocks)
-            else:
-                self._pinned[b0:b1].copy_(o["ds_mat"][b0:b1], non_blocking=True)
-        ev = torch.cuda.Event(enable_timing=True, blocking=self.blocking_wait)
+            self._pinned[b0:b1].copy_(o["ds_mat"][b0:b1], non_blocking=True)
+        ev = torch.cuda.Event(enable_timing=True, blocking=True)
         ev.record(cs)
         return ev
 
-    def _stage_a(self, part, b0, b1, o, keep_feats, gt_ks, min_pt, st, gc, col=None, defer=None, xop=None):
-        """GPU stage of one chunk (on its stream): everything up to ds_mat, then its D2H copy."""
+    def _stage_a(self, part, b0, b1, o, keep_feats, gt_ks, min_pt, gc, col=None, xop=None, plans=None):
+        """GPU stage of one chunk (on the current stream): everything up to ds_mat.  Only device
+        work on tensors that outlive the call (capturable into a HIP graph)."""
         dev = part.device
         x_ops = tuple(None if t is None else t[b0 * part.nmax[s]:b1 * part.nmax[s]]
                       for s, t in enumerate(xop or (None, None)))
         r = self.run_gpu_stage(part, keep_feats, s_out=o["s"][b0:b1], ss_out=o["ss"][b0:b1],
-                               gc=(gc[0][b0:b1], gc[1][b0:b1]), x_ops=x_ops)
+                               gc=(gc[0][b0:b1], gc[1][b0:b1]), x_ops=x_ops, plans=plans)
         ks = o["k_prob"][b0:b1]
         if self.regression:
-            ks.copy_(self._afau(self.packed(dev), o["ss"][b0:b1], part, col=col))
+            ks.copy_(self._afau(self.packed(dev), o["ss"][b0:b1], part, col=col, b0=b0))
         else:
             ks.copy_(gt_ks[b0:b1] / min_pt[b0:b1])
         self._mark("afau")
         k_used = gt_ks[b0:b1] if self.training else ks * min_pt[b0:b1]
         ops.soft_topk_fwd(o["ss"][b0:b1], part.n1, part.n2, k_used.contiguous(), C.SK_ITER_NUM, self.tau,
-                      out=o["ds_mat"][b0:b1], steps=o["sk_steps"][b0:b1],
-                      out_host=self._pinned[b0:b1] if self.zero_copy else None)
+                          out=o["ds_mat"][b0:b1], steps=o["sk_steps"][b0:b1])
         o["_kk"][b0:b1].copy_(ks * min_pt[b0:b1])
         self._mark("soft_topk")
-        if self.lsa_mode == "device":
-            # the Hungarian kernel is latency-bound (one wave per pair): run it and the selection /
-            # classifier on a side stream so the next chunks' GPU stages are not queued behind it
-            ev = torch.cuda.Event(enable_timing=True)
-            ev.record(st)
-            self._lsa_rr = getattr(self, "_lsa_rr", 0) + 1
-            side = self._lsa_streams(dev)[self._lsa_rr % 2]
-            side.wait_event(ev)
-            with torch.cuda.stream(side):
-                self._stage_c_device(part, b0, b1, o)
-            return r, ev
-        if not self.zero_copy and self.copy_stream:
-            # the D2H copy is a blit kernel: on a stream of its own it does not hold back the next
-            # chunk queued on this compute stream
-            done = torch.cuda.Event()
-            done.record(st)
-            if defer is not None:
-                defer.append((b0, b1, done))
-                return r, None
-            return r, self._enqueue_copy(dev, b0, b1, o, done)
-        if not self.zero_copy:
-            self._pinned[b0:b1].copy_(o["ds_mat"][b0:b1], non_blocking=True)
-        ev = torch.cuda.Event(enable_timing=True, blocking=self.blocking_wait)
-        ev.record(st)
-        return r, ev
-
-    def _copy_stream(self, dev):
-        key = "copy:" + str(dev)
-        if key not in self._stream_cache:
-            self._stream_cache[key] = torch.cuda.Stream(dev)
-        return self._stream_cache[key]
+        return r
 
     def _stage_c_device(self, part, b0, b1, o):
         """Device Hungarian + greedy selection + MatchClassifier of one chunk, queued on the
@@ -620,87 +581,190 @@ class Net(nn.Module):
         self._mark("match_cls")
         return dt
 
-    def run(self, bt, gt_perm=None, label=None, keep_feats=False, chunks=None):
-        """Full forward, pipelined over sub-batches ("chunks").  Every chunk's GPU stage is queued
-        at once, alternating over two streams (per-pair kernels of neighbouring chunks -- Sinkhorn,
-        soft top-k, AFA-U, one workgroup per pair -- then fill the 256 CUs together); the host LSA
-        of chunk c starts as soon as its ds_mat lands in pinned memory while the GPU continues;
-        chunk c's selection + classifier follow its LSA on its stream."""
-        dev = bt.device
-        B, n1max, n2max = bt.B, bt.n1max, bt.n2max
-        K = chunks if chunks is not None else self.pipeline_chunks(B)
-        if self.compute_ke:
-            K = 1          # Ke blocks are padded to per-chunk edge maxima: keep one chunk
-        parts = bt.split(K, self.tail_splits if K > 1 else 0, self.head_splits if K > 1 else 0)
-        t0 = time.perf_counter()
-        min_pt = torch.minimum(bt.n1, bt.n2).to(torch.float32)
-        if gt_perm is None:
-            gt_ks = min_pt.clone()     # synthetic pairs: identity ground truth
-        else:
-            gt_ks = torch.as_tensor(gt_perm).to(dev).reshape(B, -1).sum(-1).to(torch.float32)
+    @staticmethod
+    def _alloc_outputs(B, n1max, n2max, dev):
         f32 = dict(device=dev, dtype=torch.float32)
         o = {k: torch.empty(B, n1max, n2max, **f32) for k in ("s", "ss", "ds_mat", "perm_mat", "lsa")}
         o.update({k: torch.empty(B, **f32) for k in ("k_prob", "cls_logits", "cls_prob", "_kk")})
         o["sk_steps"] = torch.empty(B, device=dev, dtype=torch.int32)
         o["_lsa_status"] = torch.zeros(B, device=dev, dtype=torch.int32)
+        return o
+
+    def _prologue(self, bt, cast=True, col_idx=None):
+        """Per-forward work before the chunks (main stream): global weights + affinity
+        coefficients, the bf16 operand rows of both sides' node features in one launch each (before
+        any chunk's ds_mat D2H is in flight: cast per chunk, they ran beside the copy's blit kernel
+        and stalled ~14x; a shared probe side is cast inside its chunk's one-graph SplineConv), and
+        the AFA-U column block once per distinct n2."""
+        gc = self.global_coef(bt)
+        xop = None
+        if self.dtype_mode == "bf16" and cast:
+            xop = tuple(None if (s == 0 and bt.shared0) else ops.cast_bf16(bt.x[s]) for s in range(2))
+        col = self._afau_col(self.packed(bt.device), bt, col_idx) if self.regression else None
+        return gc, xop, col
+
+    def _graph_state(self, bt, parts, dev):
+        """HIP graphs of one batch's forward, captured on first use and replayed while the batch,
+        the chunking and the packed weights stay the same: the prologue on the main stream, then per
+        chunk its spline plans and the rest of its GPU stage (two graphs, so the copy deferral can
+        wait between them) on the chunk's stream.  Chunks of one stream share a memory pool (they
+        run in order); the two streams and the prologue have their own.  Every tensor a graph reads
+        or writes outside its pool is a static buffer of the state."""
+        wp = self.packed(dev)
+        rng = [(0, bt.B) if p is bt else p.pair_range for p in parts]
+        key = (len(parts), tuple(rng), self.dtype_mode, self.afau_mode, self.regression,
+               self.n_streams, self._pack_gen, str(dev))
+        g = self._gstate
+        if g is not None and g["bt"]() is bt and g["key"] == key:
+            return g
+        self._gstate = None
+        torch.cuda.synchronize(dev)
+        import weakref
+        B, n1max, n2max = bt.B, bt.n1max, bt.n2max
+        g = {"bt": weakref.ref(bt), "key": key}
+        o = self._alloc_outputs(B, n1max, n2max, dev)
+        g["o"] = o
+        g["min_pt"] = torch.minimum(bt.n1, bt.n2).to(torch.float32)
+        g["gt_ks"] = g["min_pt"].clone()
+        streams = self._streams(dev)
+        pools = [torch.cuda.graph_pool_handle() for _ in range(len(streams) + 1)]
+        g["col_idx"] = self._afau_col_index(bt) if self.regression else None
+        torch.cuda.synchronize(dev)
+        gp = torch.cuda.CUDAGraph()
+        # captured on a side stream (capture needs a non-default stream), replayed on the main one
+        with torch.cuda.graph(gp, pool=pools[-1], stream=self._copy_stream(dev)):
+            gc, xop, col = self._prologue(bt, col_idx=g["col_idx"])
+        g["prologue"], g["pro_out"] = gp, (gc, xop, col)
+        g["chunks"] = []
+        for c, part in enumerate(parts):
+            st = streams[c % len(streams)]
+            b0, b1 = rng[c]
+            gpl, gst = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gpl, pool=pools[c % len(streams)], stream=st):
+                pl = self.plans(part)
+            with torch.cuda.graph(gst, pool=pools[c % len(streams)], stream=st):
+                self._stage_a(part, b0, b1, o, False, g["gt_ks"], g["min_pt"], gc, col=col, xop=xop, plans=pl)
+            g["chunks"].append((gpl, gst, pl))
+        torch.cuda.synchronize(dev)
+        self._gstate = g
+        return g
+
+    def _parts(self, bt, chunks=None):
+        K = chunks if chunks is not None else self.pipeline_chunks(bt.B)
+        if self.compute_ke:
+            K = 1          # Ke blocks are padded to per-chunk edge maxima: keep one chunk
+        return bt.split(K, self.tail_splits if K > 1 else 0)
+
+    def _graphed(self, parts, keep_feats=False):
+        return (self.use_graphs and not keep_feats and self.lsa_mode != "device" and not self.compute_ke
+                and not self.training and not self._stage_timing and not ops.profiling())
+
+    def prepare(self, bt, chunks=None):
+        """Capture ``bt``'s HIP graphs now if its forward will replay them (graph mode, multi-chunk),
+        so the first run() only replays -- e.g. before several host threads drive their devices."""
+        parts = self._parts(bt, chunks)
+        if self._graphed(parts):
+            with torch.cuda.device(bt.device):
+                self._graph_state(bt, parts, bt.device)
+
+    def run(self, bt, gt_perm=None, label=None, keep_feats=False, chunks=None):
+        """Full forward, pipelined over sub-batches ("chunks").  Every chunk's GPU stage is queued
+        at once, alternating over two streams (per-pair kernels of neighbouring chunks -- Sinkhorn,
+        soft top-k, AFA-U, one workgroup per pair -- then fill the 256 CUs together); the host LSA
+        of chunk c starts as soon as its ds_mat lands in pinned memory while the GPU continues;
+        chunk c's selection + classifier follow its LSA on its stream.
+
+        With ``use_graphs`` (FPM_GRAPHS=1, ShardedNet's replicas), inference forwards replay HIP
+        graphs of the prologue and of every chunk's GPU stage (captured on the batch's first
+        forward, _graph_state): ~100 kernel launches per chunk become two graph launches.  Graph
+        mode returns fresh copies of the
+        reference outputs (ds_mat, perm_mat, k_prob, cls_prob); s / ss / lsa are views of the
+        batch's static buffers, valid until its next forward."""
+        dev = bt.device
+        B, n1max, n2max = bt.B, bt.n1max, bt.n2max
+        parts = self._parts(bt, chunks)
+        t0, t0c = time.perf_counter(), time.thread_time()
         device_lsa = self.lsa_mode == "device"
-        if not device_lsa and (self._pinned is None or self._pinned.shape != o["ds_mat"].shape):
-            self._pinned = torch.empty(o["ds_mat"].shape, dtype=torch.float32, pin_memory=True)
+        graphed = self._graphed(parts, keep_feats)
+        if not device_lsa and (self._pinned is None or self._pinned.shape != (B, n1max, n2max)):
+            self._pinned = torch.empty((B, n1max, n2max), dtype=torch.float32, pin_memory=True)
         main = torch.cuda.current_stream(dev)
+        if graphed:
+            gs = self._graph_state(bt, parts, dev)
+            o, min_pt, gt_ks = gs["o"], gs["min_pt"], gs["gt_ks"]
+        else:
+            o = self._alloc_outputs(B, n1max, n2max, dev)
+            min_pt = torch.minimum(bt.n1, bt.n2).to(torch.float32)
+            gt_ks = min_pt.clone()
+        if gt_perm is not None:
+            gt_ks.copy_(torch.as_tensor(gt_perm).to(dev).reshape(B, -1).sum(-1).to(torch.float32))
+        elif graphed:
+            gt_ks.copy_(min_pt)        # synthetic pairs: identity ground truth
         ev_start = torch.cuda.Event(enable_timing=True)
         ev_start.record(main)
-        gc = self.global_coef(bt)
-        # bf16 operand rows of both sides' node features in one launch each, before any chunk's
-        # ds_mat D2H is in flight (cast per chunk, they ran beside the copy's blit kernel and
-        # stalled ~14x; a shared probe side is cast inside its chunk's one-graph SplineConv)
-        xop = None
-        if self.dtype_mode == "bf16" and len(parts) > 1:
-            xop = tuple(None if (s == 0 and bt.shared0) else ops.cast_bf16(bt.x[s]) for s in range(2))
-        # the AFA-U column block once for the whole batch (per distinct n2), before the chunks
-        col = (self._afau_col(self.packed(dev), bt)
-               if self.regression and os.environ.get("FPM_AFAU_COLDEDUP", "1") == "1"
-               and os.environ.get("FPM_AFAU_COLFWD", "1") == "1" else None)
+        if graphed:
+            gs["prologue"].replay()
+            gc, xop, col = gs["pro_out"]
+        else:
+            gc, xop, col = self._prologue(bt, cast=len(parts) > 1)
         ev_coef = torch.cuda.Event()
         ev_coef.record(main)
         streams = self._streams(dev) if (len(parts) > 1 and self.n_streams > 1) else [main]
         for st in streams:
             if st is not main:
                 st.wait_event(ev_coef)
-        outs, events = [], []
-        lag = 2 if (self.copy_defer and len(parts) > 2 and len(streams) == 2 and self.copy_stream
-                    and not self.zero_copy and not device_lsa) else 0
-        pending = [] if lag else None
-        self._plan_events = [] if lag else None
-        self._offset_events = [] if (self.stream_offset and len(streams) == 2 and len(parts) > 1) else None
-        try:
-            for c, part in enumerate(parts):
-                st = streams[c % len(streams)]
-                b0, b1 = (0, B) if part is bt else part.pair_range     # a chunk's range inside bt
-                if c == 1 and self._offset_events:
-                    st.wait_event(self._offset_events[0])
-                    self._offset_events = None
-                with torch.cuda.stream(st):
-                    r, ev = self._stage_a(part, b0, b1, o, keep_feats, gt_ks, min_pt, st, gc, col=col, defer=pending,
-                                          xop=xop)
-                outs.append(r)
-                events.append(ev)
-                if lag and c >= lag:
-                    # chunk c - lag's copy after chunk c's first plan (same stream as chunk c - lag)
-                    pb0, pb1, pdone = pending[c - lag]
-                    events[c - lag] = self._enqueue_copy(dev, pb0, pb1, o, pdone, after=self._plan_events[c])
-            if lag:
-                for c in range(max(0, len(parts) - lag), len(parts)):
-                    pb0, pb1, pdone = pending[c]
-                    events[c] = self._enqueue_copy(dev, pb0, pb1, o, pdone)
-        finally:
-            self._plan_events = None
-            self._offset_events = None
-        t_enq = time.perf_counter()
+        outs, done, plan_ev = [], [], []
+        # copy deferral: chunk c's D2H waits for the plans of chunk c + 2 (same stream)
+        lag = 2 if (self.copy_defer and len(parts) > 2 and len(streams) == 2 and not device_lsa) else 0
+        events = [None] * len(parts)
+        for c, part in enumerate(parts):
+            st = streams[c % len(streams)]
+            b0, b1 = (0, B) if part is bt else part.pair_range     # a chunk's range inside bt
+            with torch.cuda.stream(st):
+                if graphed:
+                    gpl, gst, _ = gs["chunks"][c]
+                    gpl.replay()
+                else:
+                    pl = self.plans(part)
+                evp = torch.cuda.Event()
+                evp.record(st)
+                plan_ev.append(evp)
+                if graphed:
+                    gst.replay()
+                    outs.append(None)
+                else:
+                    outs.append(self._stage_a(part, b0, b1, o, keep_feats, gt_ks, min_pt, gc, col=col, xop=xop,
+                                              plans=pl))
+                if device_lsa:
+                    # the Hungarian kernel is latency-bound (one wave per pair): run it and the
+                    # selection / classifier on a side stream so the next chunks' GPU stages are not
+                    # queued behind it
+                    ev = torch.cuda.Event(enable_timing=True)
+                    ev.record(st)
+                    side = self._lsa_streams(dev)[c % 2]
+                    side.wait_event(ev)
+                    with torch.cuda.stream(side):
+                        self._stage_c_device(part, b0, b1, o)
+                    events[c] = ev
+                    continue
+                ev = torch.cuda.Event()
+                ev.record(st)
+                done.append((b0, b1, ev))
+            if not lag:
+                events[c] = self._enqueue_copy(dev, b0, b1, o, ev)
+            elif c >= lag:
+                pb0, pb1, pdone = done[c - lag]
+                events[c - lag] = self._enqueue_copy(dev, pb0, pb1, o, pdone, after=plan_ev[c])
+        if lag:
+            for c in range(max(0, len(parts) - lag), len(parts)):
+                pb0, pb1, pdone = done[c]
+                events[c] = self._enqueue_copy(dev, pb0, pb1, o, pdone)
+        t_enq, t_enqc = time.perf_counter(), time.thread_time()
         t_lsa, t_first = 0.0, None
         for c, (part, ev) in enumerate(zip(parts, events)):
             if device_lsa:
                 break
-            b0, b1 = (0, B) if part is bt else part.pair_range     # a chunk's range inside bt
+            b0, b1 = (0, B) if part is bt else part.pair_range
             ev.synchronize()
             t_first = t_first or time.perf_counter()
             with torch.cuda.stream(streams[c % len(streams)]):
@@ -715,11 +779,14 @@ class Net(nn.Module):
             if bad.numel():
                 raise RuntimeError("hungarian: pair %d is infeasible or has NaN/-inf costs" % int(bad[0]))
         res = {k: v for k, v in o.items() if not k.startswith("_")}
-        if len(outs) == 1 or keep_feats:
+        if graphed:
+            for k in ("ds_mat", "perm_mat", "k_prob", "cls_logits", "cls_prob", "sk_steps"):
+                res[k] = o[k].clone()
+        elif len(outs) == 1 or keep_feats:
             for k in outs[0]:
                 if k not in ("s", "ss"):
                     res[k] = outs[0][k] if len(outs) == 1 else torch.cat([r[k] for r in outs])
-        ks, logits = o["k_prob"], o["cls_logits"]
+        ks, logits = res["k_prob"], res["cls_logits"]
         if label is not None:
             res["cls_loss"] = F.binary_cross_entropy_with_logits(logits, torch.as_tensor(label).to(dev).view(-1).float())
         else:
@@ -732,8 +799,8 @@ class Net(nn.Module):
             res["ks_error"] = 0.0
         # GPU time of the stages before the Hungarian (all chunks), from events on the streams
         self.last_timing = dict(gpu_stage_s=ev_start.elapsed_time(events[-1]) / 1e3, lsa_s=t_lsa,
-                                first_chunk_wait_s=(t_first or t0) - t0, chunks=len(parts),
-                                enqueue_s=t_enq - t0, total_s=time.perf_counter() - t0)
+                                first_chunk_wait_s=(t_first or t0) - t0, chunks=len(parts), graphs=graphed,
+                                enqueue_s=t_enq - t0, enqueue_cpu_s=t_enqc - t0c, total_s=time.perf_counter() - t0)
         return res
 
     def image_features(self, images, Ps, ns, dev=None):

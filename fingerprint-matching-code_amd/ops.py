@@ -95,9 +95,14 @@ def topk_select(ds, assign, k, lsa_out=None, out=None):
     return perm
 
 
+def profiling():
+    """True while the library's HIP-event profiling of the product GEMM is on (fpm_profile_enable)."""
+    return bool(_lib.load().fpm_profile_enabled())
+
+
 def set_tuning(key, value):
-    """Kernel-variant switch (fpm_set_tuning: "gemm_phase", "gnn_packed"; all variants are
-    bit-identical).  Returns the previous value."""
+    """Kernel-variant switch (fpm_set_tuning, include/fpm.h lists the keys).  Returns the previous
+    value."""
     prev = int(_lib.load().fpm_set_tuning(key.encode(), int(value)))
     if prev < 0:
         raise _lib.FpmError(_lib.load().fpm_last_error().decode(errors="replace"))
@@ -464,22 +469,6 @@ def gnn_layer_bwd_point(X, C, B, n1max, n2max, dXn, dz, params, dX, dagg, V):
               _p(params), _p(dX), _p(dagg), _p(V), _stream(X))
 
 
-def copy_async(dst, src, nblocks=16):
-    """dst.copy_(src) for a device tensor into pinned host memory (or device memory) on a few
-    workgroups of the current stream (fpm_copy_async)."""
-    _dev(src)
-    if not (src.is_contiguous() and dst.is_contiguous()) or src.numel() * src.element_size() != dst.numel() * dst.element_size():
-        raise _lib.FpmError("copy_async: contiguous tensors of equal size expected")
-    if not dst.is_cuda and not dst.is_pinned():
-        raise _lib.FpmError("copy_async: host destination must be pinned")
-    _lib.call("fpm_copy_async", _p(src), _p(dst), src.numel() * src.element_size(), int(nblocks), _stream(src))
-    return dst
-
-
-# ---- reference-signature mirrors (SURVEY §8(b) "Python layer") ----------------------------------
-# Same names, argument order and meaning as the reference's operators, on the HIP kernels above, so
-# code written against src/model/sinkhorn.py, src/model/soft_topk.py and utils/hungarian.py runs
-# unchanged on device tensors.  Net.forward itself uses the fused kernels directly.
 def _counts(n, B, full, dev):
     """nrows / ncols as the kernels take them: int32 on ``dev``; None -> the unpadded size."""
     if n is None:
@@ -597,15 +586,4 @@ def hungarian(s, n1=None, n2=None, nproc=1):
     perm = perm.to(device=s.device, dtype=s.dtype)
     return perm.squeeze(0) if matrix_input else perm
 
-
-def memcpy_async(dst, src, kind=2):
-    """dst.copy_(src) through hipMemcpyAsync with an explicit copy kind on the current stream
-    (fpm_memcpy_async): 2 = device -> host, 1024 = device-to-device without compute units."""
-    _dev(src)
-    if not (src.is_contiguous() and dst.is_contiguous()) or src.numel() * src.element_size() != dst.numel() * dst.element_size():
-        raise _lib.FpmError("memcpy_async: contiguous tensors of equal size expected")
-    if not dst.is_cuda and not dst.is_pinned():
-        raise _lib.FpmError("memcpy_async: host destination must be pinned")
-    _lib.call("fpm_memcpy_async", _p(dst), _p(src), src.numel() * src.element_size(), int(kind), _stream(src))
-    return dst
 

@@ -82,31 +82,19 @@ int fpm_gemm(int dtype, const void* A, long lda, long sA, const int* a_rows, con
              int N, int K, int batch, int epi, const float* bias, float* Cf, void* Ct, long ldc, long sC,
              const int* n1, const int* n2, void* stream);
 int fpm_cast_bf16(const float* x, void* y, long n, void* stream);
-/* Device -> pinned-host (or device) copy on nblocks workgroups (default 16): the ds_mat hand-off to
- * the host Hungarian (ngm.py:444 -> utils/hungarian.py:44 .cpu()) without the runtime's
- * one-workgroup-per-CU blit.  16-B aligned pointers, bytes % 16 == 0. */
-int fpm_copy_async(const void* src, void* dst, long bytes, int nblocks, void* stream);
-/* hipMemcpyAsync with an explicit kind (2 = device -> host, 1024 = device-to-device without compute
- * units, i.e. a copy engine, for a device-addressable pinned host destination): the same hand-off. */
-int fpm_memcpy_async(void* dst, const void* src, long bytes, int kind, void* stream);
-
 /* Kernel-variant switches for A/B timing.  Returns the
  * previous value, or -1 (error channel set) for an unknown key.  No reference counterpart.
  *   "gemm_phase" (env FPM_GEMM_PHASE, default 1): 256x256 bf16 GEMM tiles on the phase-pipelined
  *                kernel (1) or the two-stage kernel (0)
- *   "gemm_persist" (env FPM_GEMM_PERSIST, default 0): the SplineConv product GEMM as a persistent
- *                kernel (one workgroup per CU over the plan's real tiles, next tile's DMA prologue under
- *                the current epilogue; bit-identical; +9 % alone, -1.5 % inside the two-stream forward);
- *                env FPM_GEMM_PERSIST_GRID caps its workgroup count
  *   "combine_npb" (FPM_COMBINE_NPB, default 4): destination nodes per SplineConv combine workgroup
+ *   "plan_graph" (FPM_PLAN_GRAPH, default 1): per-graph spline plan kernels where they apply (1) or
+ *                the global plan kernels (0)
+ *   "sinkhorn_bwd_reg" (FPM_SINKHORN_BWD_REG, default 1): register-tile Sinkhorn backward (n <= 256)
+ *   "afau_attn_v" (default 1): the LDS-staged-V cross-set attention where it applies (n2max <= 512)
  * Switches whose variants round differently (results within fp32 rounding, not bit-identical):
  *   "sinkhorn_fast" (FPM_SINKHORN_FAST, default 1): shifted single-pass lse after the first step
  *       (0 = max-shifted lse every step; 2 = 1 with scalar loads in the n > 256 streaming kernel)
- *   "topk_fast" (FPM_TOPK_FAST, default 1): shifted single-pass early soft top-k column steps
- *   "afau_lut" (FPM_AFAU_LUT, default 2 = by dtype): AFA-U score lookup table (1) or 16-term sum (0);
- *                by dtype: the LUT only for bf16 rows the LDS-V kernel cannot take (n2max > 512)
- *   "afau_attn_v" (FPM_AFAU_ATTN_V, default 1): the cross-set attention with V staged in LDS and the
- *                range-classified scores (bf16) / 16-term chain (fp32) for n2max <= 512 */
+ *   "topk_fast" (FPM_TOPK_FAST, default 1): shifted single-pass early soft top-k column steps */
 int fpm_set_tuning(const char* key, int value);
 
 /* ---- SplineConv message passing ---------------------------------------------------------------
@@ -332,6 +320,7 @@ int fpm_feature_align_bwd(const float* nodes, const long* node_shape, const long
 
 /* ---- profiling hooks: HIP-event timing of the dominant kernel (edge-message GEMM) ------------ */
 int fpm_profile_enable(int on);
+int fpm_profile_enabled(void);   /* 1 while enabled: Net.run then launches eagerly (no HIP graphs) */
 int fpm_profile_read(double* ms_total, double* flops_total, int* count);
 
 /* ---- device: batched linear sum assignment -------------------------------

@@ -462,6 +462,29 @@ def test_chunked_pipeline_bitwise(sd):
         assert torch.equal(c[k], a[k][2:5]), k
 
 
+@pytest.mark.parametrize("dtype,regression", [("bf16", True), ("f32", False)])
+def test_graph_replay_bitwise_equals_eager(sd, dtype, regression):
+    """Multi-chunk forwards replay HIP graphs captured on the batch's first forward (prologue, and
+    per chunk its plans and GPU stage): bit-identical to the eager launches on a ragged batch, on
+    the capturing forward and on replays; the returned reference outputs are fresh tensors."""
+    pairs = synth.make_batch(23, 11, [48, 40, 44, 48, 30, 48, 47, 41, 48, 36, 45],
+                             n2=[48, 47, 40, 30, 48, 44, 48, 48, 39, 48, 42])
+    bt = DeviceBatch.from_pairs(pairs, DEV)
+    runs = {}
+    for graphs in (False, True):
+        net = fpm.Net(regression=regression, backbone=False, dtype=dtype, chunks=3)
+        net.load_state_dict(sd)
+        net.use_graphs = graphs
+        r = [net.run(bt) for _ in range(3)]
+        assert net.last_timing["graphs"] == graphs and net.last_timing["chunks"] > 1
+        runs[graphs] = r
+    for k in ("s", "ss", "ds_mat", "perm_mat", "k_prob", "cls_prob", "lsa"):
+        for r in runs[True]:
+            assert torch.equal(runs[False][0][k], r[k]), k
+    a, b = runs[True][0], runs[True][1]
+    assert a["ds_mat"].data_ptr() != b["ds_mat"].data_ptr() and a["perm_mat"].data_ptr() != b["perm_mat"].data_ptr()
+
+
 # ---------------------------------------------------------------------------------------- Ke, Gconv
 def test_edge_affinity_ke(sd):
     """Optional quadratic affinity (ngm.py:282-289) vs the oracle, ragged edge counts."""
@@ -716,7 +739,7 @@ def test_gnn_kernel_variants_bit_identical(sd):
     bt = DeviceBatch.from_pairs(pairs, DEV)
     outs = []
     for key, val in (("combine_npb", 4), ("combine_npb", 16),
-                     ("plan_graph", 0), ("combine_pf", 0), ("combine_pf", 1), ("gemm_persist", 1), ("nodecls_t", 0)):
+                     ("plan_graph", 0)):
         prev = ops.set_tuning(key, val)
         try:
             r = net.run(bt, chunks=1)
@@ -727,15 +750,6 @@ def test_gnn_kernel_variants_bit_identical(sd):
     for r in outs[1:]:
         for k in ("s", "ss", "ds_mat", "k_prob"):
             assert torch.equal(r[k], outs[0][k]), k
-
-
-def test_copy_async_to_pinned():
-    """fpm_copy_async (few-workgroup D2H into pinned memory; FPM_COPY_BLOCKS switch) copies exactly."""
-    x = torch.randn(3, 77, 64, device=DEV)
-    h = torch.empty(x.shape, pin_memory=True)
-    ops.copy_async(h, x, 8)
-    torch.cuda.synchronize()
-    assert torch.equal(h, x.cpu())
 
 
 def test_global_weights_kernel():
@@ -837,41 +851,6 @@ def test_cast_bf16_round_to_nearest_even(n):
     assert torch.equal(y.view(torch.int16), x.to(torch.bfloat16).view(torch.int16))
 
 
-@pytest.mark.parametrize("kind", [2, 1024])
-def test_memcpy_async_kinds_to_pinned(kind):
-    """The ds_mat hand-off copy through fpm_memcpy_async (device -> host, and the
-    no-compute-unit kind) delivers the same bytes into pinned host memory."""
-    x = torch.randn(64, 256, 256, device=DEV)
-    h = torch.empty(x.shape, dtype=x.dtype, pin_memory=True)
-    ops.memcpy_async(h, x, kind)
-    torch.cuda.synchronize()
-    assert torch.equal(h, x.cpu())
-
-
-@pytest.mark.parametrize("npairs,n", [(24, 256), (5, 100), (1, 32)])
-def test_gemm_persist_bit_identical(sd, npairs, n):
-    """The persistent product GEMM (one workgroup per CU walking the plan's real tiles, next tile's
-    prologue under the current epilogue) against the one-shot phase kernel: identical forwards.
-    24 pairs of n = 256 give ~700 tiles (several per workgroup: the tile-boundary path), the small
-    batches fewer tiles than workgroups."""
-    pairs = synth.make_batch(29 + n, npairs, n)
-    net = fpm.Net(regression=True, backbone=False, dtype="bf16")
-    net.load_state_dict(sd)
-    bt = DeviceBatch.from_pairs(pairs, DEV)
-    outs = []
-    for val in (0, 1, 0, 1):
-        prev = ops.set_tuning("gemm_persist", val)
-        try:
-            r = net.run(bt, chunks=1)
-            torch.cuda.synchronize()
-        finally:
-            ops.set_tuning("gemm_persist", prev)
-        outs.append(r)
-    for r in outs[1:]:
-        for k in ("s", "ss", "ds_mat", "k_prob", "perm_mat"):
-            assert torch.equal(r[k], outs[0][k]), k
-
-
 @pytest.mark.parametrize("B,n1,n2max,n2s", [(3, 64, 64, [64, 50, 61]), (2, 200, 256, [256, 233]), (2, 37, 45, [45, 20]),
                                              (2, 100, 512, [512, 437]), (1, 40, 301, [301])])
 def test_crossset_attn_lds_v_kernel(sd, B, n1, n2max, n2s):
@@ -887,7 +866,7 @@ def test_crossset_attn_lds_v_kernel(sd, B, n1, n2max, n2s):
     args = [wp[k] for k in ("row_Wv", "row_mix1w", "row_mix1b", "row_mix2w", "row_mix2b")]
     res = {}
     for v in (0, 1):
-        pv, pl = ops.set_tuning("afau_attn_v", v), ops.set_tuning("afau_lut", 0)
+        pv = ops.set_tuning("afau_attn_v", v)
         try:
             o32 = torch.empty(B * n1, 256, device=DEV)
             st = torch.empty(B * n1, 16, 2, device=DEV)
@@ -897,7 +876,6 @@ def test_crossset_attn_lds_v_kernel(sd, B, n1, n2max, n2s):
             torch.cuda.synchronize()
         finally:
             ops.set_tuning("afau_attn_v", pv)
-            ops.set_tuning("afau_lut", pl)
         res[v] = (o32, st, o3[:, :256].float() + o3[:, 256:512].float())
     (a0, s0, _), (a1, s1, h1) = res[0], res[1]
     scale = a0.abs().max()
@@ -905,24 +883,4 @@ def test_crossset_attn_lds_v_kernel(sd, B, n1, n2max, n2s):
     assert torch.allclose(s1, s0, rtol=1e-5, atol=1e-6)
     assert (h1 - a0).abs().max() <= 2e-5 * scale
 
-
-def test_afau_head_and_nodecls_variants_bit_identical(sd):
-    """The 8-wave AFA-U head (FPM_AFAU_HEAD1 selects the one-wave form) and the LDS-transposed node
-    classifier (nodecls_t) reproduce the other forms bit for bit (k_prob, s)."""
-    pairs = synth.make_batch(23, 5, 100, n2=[100, 90, 77, 100, 64])
-    net = fpm.Net(regression=True, backbone=False, dtype="bf16")
-    net.load_state_dict(sd)
-    bt = DeviceBatch.from_pairs(pairs, DEV)
-    r8 = net.run(bt, chunks=1)
-    torch.cuda.synchronize()
-    os.environ["FPM_AFAU_HEAD1"] = "1"
-    prev = ops.set_tuning("nodecls_t", 0)
-    try:
-        r1 = net.run(bt, chunks=1)
-        torch.cuda.synchronize()
-    finally:
-        del os.environ["FPM_AFAU_HEAD1"]
-        ops.set_tuning("nodecls_t", prev)
-    for k in ("k_prob", "s", "ss", "ds_mat", "perm_mat"):
-        assert torch.equal(r8[k], r1[k]), k
 
