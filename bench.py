@@ -217,6 +217,7 @@ def main():
                     "modes for the parity_vs_oracle report")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-f32-line", action="store_true", help="skip the fp32-mode C3 line")
+    ap.add_argument("--no-share-line", action="store_true", help="skip the 128-pairs-per-GPU line")
     ap.add_argument("--no-selfcheck", action="store_true", help="skip the timed-batch self-check (kernel-trace "
                     "profiles: its single-pair forwards would enter the per-kernel averages)")
     ap.add_argument("--lsa-threads", type=int, default=0)
@@ -385,6 +386,20 @@ def main():
         strong = {"global_batch": share * world, "pairs_per_gpu": share, "value": share * world * args.steps / es,
                   "unit": "pairs/s", "ms_per_step": es / args.steps * 1e3, "scaling": "strong"}
 
+    # the strong-scaling share on one GPU: BASELINE's global batch of 1024 over 8 GPUs is 128 pairs
+    # per GPU; the same forward timed on the first 128 pairs of this batch (its own line, not value)
+    share_line = None
+    if world == 1 and args.config == "c3" and args.batch >= 256 and not args.no_share_line:
+        sub = bt.split_range(0, 128)
+        net.run(sub)
+        es, gs_, ls_ = timed(net, sub, args.steps, "share128")
+        share_line = {"pairs_per_gpu": 128, "value": 128 * args.steps / es, "unit": "pairs/s",
+                      "ms_per_step": es / args.steps * 1e3, "gpu_stage_pairs_per_s": 128 * args.steps / gs_,
+                      "host_lsa_ms_per_step": ls_ / args.steps * 1e3, "chunks": net.last_timing["chunks"],
+                      "enqueue_ms": net.last_timing["enqueue_s"] * 1e3,
+                      "note": "BASELINE's global batch of 1024 split over 8 GPUs: 128 pairs per GPU, one GPU timed"}
+        log("share-128 line: %s" % json.dumps(share_line))
+
     # HBM bytes per launch of the same kernel from the committed rocprofv3 PMC pass (FETCH_SIZE x2 +
     # WRITE_SIZE, separate passes; tools/pmc_gemm.sh -> profiles/r01_pmc_product_gemm.json)
     traffic = None
@@ -459,6 +474,7 @@ def main():
             "timed_batch_selfcheck_detail": {k: selfcheck[k] for k in ("pairs_checked", "chunks", "outputs")},
             "f32_line": f32_line,
             "strong_scaling": strong,
+            "share128_line": share_line,
             "ranks_share_devices": shared_devices,
             "input_gen_s": t_gen,
             "graph_build": graph_build,

@@ -32,6 +32,8 @@ SIGNATURES = {
     "fpm_spline_plan": (I, [P, P, P, L, L, I, P, L, P]),
     "fpm_spline_plan_graphs": (I, [P, P, P, L, L, I, L, P, L, P]),
     "fpm_spline_plan_csr": (I, [P, L, L, ctypes.POINTER(P), ctypes.POINTER(P)]),
+    "fpm_spline_plan_multi": (I, [P, I, I, I, P, P]),
+    "fpm_spline_plan_job_bytes": (I, []),
     "fpm_spline_y_bytes": (L, [I, L, L]),
     "fpm_spline_conv_fwd": (I, [I, P, P, L, L, I, P, P, P, P, L, I, P, P, P, P, P]),
     "fpm_spline_conv_fwd_argmax": (I, [I, P, P, L, L, I, P, P, P, P, L, I, P, P, P, P, P, P]),

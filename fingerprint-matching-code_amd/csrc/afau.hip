@@ -267,19 +267,25 @@ __global__ __launch_bounds__(256) void afau_row_attn_v_kernel(const float* __res
     typedef float f2v __attribute__((ext_vector_type(2)));
     constexpr int VS = 16 * TJ + 4;                       // padded V row (floats)
     __shared__ __attribute__((aligned(16))) float vbuf[2][16 * VS];
-    __shared__ float part[2][4][256];
+    // per-wave partial outputs, element (row, d) at row * 16 + d + (row / 4) * 16: the four lane
+    // groups of a wave write rows 4q + k (k fixed per instruction) into distinct banks
+    __shared__ float part[2][4][320];
     __shared__ float2 rowms[2][4][16];
     const int b = blockIdx.x, i0 = blockIdx.y * 16, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int n2b = n2[b];
     const int r = lane & 15, i = i0 + r, jl = wv * 4 * TJ + (lane >> 4) * TJ;
 
-    // V staging: thread copies row vr, columns [vc, vc + 16) of the head's slice (zero past n2b)
-    const int vr = tid >> 4, vc = (tid & 15) * TJ;
+    // V staging: thread copies row vr, columns [vc, vc + TJ) of the head's slice (zero past n2b),
+    // its TJ / 4 16-B chunks in an order rotated by (lane / 4) % 4: the 16 lanes of one row then
+    // write 16 distinct 4-bank groups per ds_write_b128 (in order they hit 4 groups 4 times)
+    const int vr = tid >> 4, vc = (tid & 15) * TJ, rot = (tid >> 2) & 3;
     float4 vnext[TJ / 4];
+    auto vchunk = [&](int k) { return (k & ~3) | ((k + rot) & 3); };
     auto load_v = [&](int h) {
         const float* src = Wv + (long)(h * 16 + vr) * emb + vc;
 #pragma unroll
-        for (int k = 0; k < TJ / 4; ++k) {
+        for (int k0 = 0; k0 < TJ / 4; ++k0) {
+            const int k = vchunk(k0);
             const int j = vc + 4 * k;
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
             if (j + 3 < n2b) {                            // n2b <= n2max <= emb: inside the row
@@ -289,13 +295,13 @@ __global__ __launch_bounds__(256) void afau_row_attn_v_kernel(const float* __res
                 if (j + 1 < n2b) v.y = src[4 * k + 1];
                 if (j + 2 < n2b) v.z = src[4 * k + 2];
             }
-            vnext[k] = v;
+            vnext[k0] = v;
         }
     };
     auto store_v = [&](int buf) {
         float* dst = &vbuf[buf][vr * VS + vc];
 #pragma unroll
-        for (int k = 0; k < TJ / 4; ++k) *(float4*)(dst + 4 * k) = vnext[k];
+        for (int k0 = 0; k0 < TJ / 4; ++k0) *(float4*)(dst + 4 * vchunk(k0)) = vnext[k0];
     };
     load_v(0);
     // costs: this lane's 16 contiguous columns of row i
@@ -434,7 +440,7 @@ __global__ __launch_bounds__(256) void afau_row_attn_v_kernel(const float* __res
         for (int t = 0; t < TJ; ++t) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(p[t], vreg[t], acc, 0, 0, 0);
         if (h + 1 < 16) store_v(buf ^ 1);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) part[buf][wv][(4 * (lane >> 4) + k) * 16 + r] = acc[k];
+        for (int k = 0; k < 4; ++k) part[buf][wv][(4 * (lane >> 4) + k) * 16 + r + (lane >> 4) * 16] = acc[k];
         if (lane < 16) rowms[buf][wv][lane] = make_float2(mloc, sloc);
         // LDS-only barrier (no vmcnt(0): this head's output stores stay in flight)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -451,7 +457,7 @@ __global__ __launch_bounds__(256) void afau_row_attn_v_kernel(const float* __res
                 const float2 ms = rowms[buf][w][rr];
                 const float sc = fpm::fast_exp2((ms.x - M) * fpm::LOG2E_F);
                 sum = fmaf(ms.y, sc, sum);
-                o = fmaf(part[buf][w][tid], sc, o);
+                o = fmaf(part[buf][w][tid + (rr >> 2) * 16], sc, o);
             }
             if (stats && d == 0 && ii < n1max) stats[((long)b * n1max + ii) * 16 + h] = make_float2(M, sum);
             if (ii < n1max) {

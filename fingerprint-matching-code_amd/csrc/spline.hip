@@ -41,12 +41,12 @@ __host__ __device__ inline long al(long x) { return (x + 255) & ~255L; }
 
 // Deduplicated message GEMM: every (source node, cell) product x_u W_k that some edge corner needs
 // is computed once (a node's ~6 out-edges x 4 corners touch ~9 distinct cells), root = cell 25.
-inline long plan_max_rows(long E, long num_nodes) {
+__host__ __device__ inline long plan_max_rows(long E, long num_nodes) {
     long a = 4 * E, b = 25 * num_nodes;
     return (a < b ? a : b) + num_nodes;
 }
 
-PlanLayout plan_layout(long E, long num_nodes) {
+__host__ __device__ PlanLayout plan_layout(long E, long num_nodes) {
     PlanLayout L;
     L.nblk = (num_nodes + 255) / 256;
     L.max_rows = plan_max_rows(E, num_nodes);
@@ -349,19 +349,17 @@ __device__ __forceinline__ long pg_lower_bound(const int* __restrict__ a, long n
 }
 
 // K1: edge basis / group, node cell masks, per-graph cell counts, dst CSR (sorted in LDS)
-__global__ __launch_bounds__(PG_THREADS) void plan_graph_kernel(const int* __restrict__ src,
-                                                                const int* __restrict__ dst,
-                                                                const float* __restrict__ pseudo, long E, int nmax,
-                                                                int ngraphs, int* __restrict__ mask,
-                                                                float* __restrict__ basis_e, int* __restrict__ grp_e,
-                                                                int* __restrict__ cellcnt, int* __restrict__ dst_ptr,
-                                                                int* __restrict__ csr_e, int* __restrict__ nbr_local,
-                                                                int* __restrict__ eoff) {
+__device__ __forceinline__ void plan_graph_body(int g, const int* __restrict__ src, const int* __restrict__ dst,
+                                                const float* __restrict__ pseudo, long E, int nmax, int ngraphs,
+                                                int* __restrict__ mask, float* __restrict__ basis_e,
+                                                int* __restrict__ grp_e, int* __restrict__ cellcnt,
+                                                int* __restrict__ dst_ptr, int* __restrict__ csr_e,
+                                                int* __restrict__ nbr_local, int* __restrict__ eoff) {
     __shared__ unsigned key[PG_MAXE];
     __shared__ int maskL[PG_MAXN], cnt[PG_MAXN], pos[PG_MAXN + 1];
     __shared__ long range[2];
     __shared__ int ccount[NCELL];
-    const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const int tid = threadIdx.x, lane = tid & 63;
     const int base = g * nmax;
     if (tid == 0) range[0] = pg_lower_bound(src, E, base);
     if (tid == 1) range[1] = pg_lower_bound(src, E, base + nmax);
@@ -468,10 +466,21 @@ __global__ __launch_bounds__(PG_THREADS) void plan_graph_kernel(const int* __res
     if (tid < NCELL) cellcnt[g * NCELL + tid] = ccount[tid];
 }
 
+__global__ __launch_bounds__(PG_THREADS) void plan_graph_kernel(const int* __restrict__ src,
+                                                                const int* __restrict__ dst,
+                                                                const float* __restrict__ pseudo, long E, int nmax,
+                                                                int ngraphs, int* __restrict__ mask,
+                                                                float* __restrict__ basis_e, int* __restrict__ grp_e,
+                                                                int* __restrict__ cellcnt, int* __restrict__ dst_ptr,
+                                                                int* __restrict__ csr_e, int* __restrict__ nbr_local,
+                                                                int* __restrict__ eoff) {
+    plan_graph_body(blockIdx.x, src, dst, pseudo, E, nmax, ngraphs, mask, basis_e, grp_e, cellcnt, dst_ptr, csr_e,
+                    nbr_local, eoff);
+}
+
 // K2: one block -- per-cell exclusive scan over graphs (in place), cell offsets, tile tables
-__global__ __launch_bounds__(1024) void plan_graph_scan_kernel(int* cellcnt, int ngraphs, int* cell_off,
-                                                               int* tile_info, int max_tiles, int* tile_info2,
-                                                               int max_tiles2) {
+__device__ __forceinline__ void plan_graph_scan_body(int* cellcnt, int ngraphs, int* cell_off, int* tile_info,
+                                                     int max_tiles, int* tile_info2, int max_tiles2) {
     __shared__ int cell_tot[NCELL], tile_off[NCELL + 1], coff[NCELL + 1];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     for (int k = wv; k < NCELL; k += 16) {
@@ -506,20 +515,24 @@ __global__ __launch_bounds__(1024) void plan_graph_scan_kernel(int* cellcnt, int
     build_tile_table(coff, cell_tot, tile_off, fpm::G2_BM, tile_info2, max_tiles2, cell_off + NCELL + 2);
 }
 
+__global__ __launch_bounds__(1024) void plan_graph_scan_kernel(int* cellcnt, int ngraphs, int* cell_off,
+                                                               int* tile_info, int max_tiles, int* tile_info2,
+                                                               int max_tiles2) {
+    plan_graph_scan_body(cellcnt, ngraphs, cell_off, tile_info, max_tiles, tile_info2, max_tiles2);
+}
+
 // K3: rowid / arows (ranks of the graph's nodes per cell, in node order), then the CSR slots'
 // 4 product rows and basis weights
-__global__ __launch_bounds__(PG_THREADS) void plan_graph_rank_kernel(const int* __restrict__ src, const int* mask,
-                                                                     int nmax, const int* __restrict__ gbase,
-                                                                     const int* __restrict__ cell_off,
-                                                                     const int* __restrict__ eoff,
-                                                                     const int* __restrict__ csr_e,
-                                                                     const int* __restrict__ grp_e,
-                                                                     const float* __restrict__ basis_e, int* rowid,
-                                                                     int* __restrict__ arows, int4* __restrict__ rows4,
-                                                                     float4* __restrict__ basis4) {
+__device__ __forceinline__ void plan_graph_rank_body(int g, const int* __restrict__ src, const int* mask, int nmax,
+                                                     const int* __restrict__ gbase, const int* __restrict__ cell_off,
+                                                     const int* __restrict__ eoff, const int* __restrict__ csr_e,
+                                                     const int* __restrict__ grp_e,
+                                                     const float* __restrict__ basis_e, int* rowid,
+                                                     int* __restrict__ arows, int4* __restrict__ rows4,
+                                                     float4* __restrict__ basis4) {
     __shared__ int wc[PG_THREADS / 64][NCELL];
     __shared__ int run[NCELL];
-    const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const long base = (long)g * nmax;
     const unsigned long long lt = (1ull << lane) - 1ull;
     if (tid < NCELL) run[tid] = cell_off[tid] + gbase[g * NCELL + tid];
@@ -569,6 +582,68 @@ __global__ __launch_bounds__(PG_THREADS) void plan_graph_rank_kernel(const int* 
         rows4[p] = r;
         basis4[p] = *(const float4*)(basis_e + 4 * (long)e);
     }
+}
+
+__global__ __launch_bounds__(PG_THREADS) void plan_graph_rank_kernel(const int* __restrict__ src, const int* mask,
+                                                                     int nmax, const int* __restrict__ gbase,
+                                                                     const int* __restrict__ cell_off,
+                                                                     const int* __restrict__ eoff,
+                                                                     const int* __restrict__ csr_e,
+                                                                     const int* __restrict__ grp_e,
+                                                                     const float* __restrict__ basis_e, int* rowid,
+                                                                     int* __restrict__ arows, int4* __restrict__ rows4,
+                                                                     float4* __restrict__ basis4) {
+    plan_graph_rank_body(blockIdx.x, src, mask, nmax, gbase, cell_off, eoff, csr_e, grp_e, basis_e, rowid, arows,
+                         rows4, basis4);
+}
+
+// Several plans (e.g. every pipeline chunk of one side of a batch) built by one launch of each
+// per-graph kernel: job j's graphs are blocks [gstart_j, gstart_j + ngraphs_j) of the K1 / K3
+// grids and block j of the K2 grid; job j's plan lives at ws + ws_off_j.  Each plan is the one
+// fpm_spline_plan_graphs builds for that job alone (bit-identical).
+struct PlanJob {
+    const int* src;
+    const int* dst;
+    const float* pseudo;
+    long E, num_nodes, ws_off;
+    int ngraphs, gstart;
+};
+
+__device__ __forceinline__ int plan_job_of(const PlanJob* __restrict__ jobs, int njobs, int blk) {
+    int j = 0;
+    while (j + 1 < njobs && jobs[j + 1].gstart <= blk) ++j;
+    return j;
+}
+
+__global__ __launch_bounds__(PG_THREADS) void plan_multi_graph_kernel(const PlanJob* __restrict__ jobs, int njobs,
+                                                                      int nmax, char* ws) {
+    const int j = plan_job_of(jobs, njobs, blockIdx.x);
+    const PlanJob J = jobs[j];
+    const PlanLayout L = plan_layout(J.E, J.num_nodes);
+    char* w = ws + J.ws_off;
+    plan_graph_body(blockIdx.x - J.gstart, J.src, J.dst, J.pseudo, J.E, nmax, J.ngraphs, (int*)(w + L.mask),
+                    (float*)(w + L.basis_e), (int*)(w + L.grp_e), (int*)(w + L.indeg), (int*)(w + L.dst_ptr),
+                    (int*)(w + L.csr_e), (int*)(w + L.nbr_local), (int*)(w + L.dslot));
+}
+
+__global__ __launch_bounds__(1024) void plan_multi_scan_kernel(const PlanJob* __restrict__ jobs, char* ws) {
+    const PlanJob J = jobs[blockIdx.x];
+    const PlanLayout L = plan_layout(J.E, J.num_nodes);
+    char* w = ws + J.ws_off;
+    plan_graph_scan_body((int*)(w + L.indeg), J.ngraphs, (int*)(w + L.cell_off), (int*)(w + L.tile_info),
+                         (int)L.max_tiles, (int*)(w + L.tile_info2), (int)L.max_tiles2);
+}
+
+__global__ __launch_bounds__(PG_THREADS) void plan_multi_rank_kernel(const PlanJob* __restrict__ jobs, int njobs,
+                                                                     int nmax, char* ws) {
+    const int j = plan_job_of(jobs, njobs, blockIdx.x);
+    const PlanJob J = jobs[j];
+    const PlanLayout L = plan_layout(J.E, J.num_nodes);
+    char* w = ws + J.ws_off;
+    plan_graph_rank_body(blockIdx.x - J.gstart, J.src, (const int*)(w + L.mask), nmax, (const int*)(w + L.indeg),
+                         (const int*)(w + L.cell_off), (const int*)(w + L.dslot), (const int*)(w + L.csr_e),
+                         (const int*)(w + L.grp_e), (const float*)(w + L.basis_e), (int*)(w + L.rowid),
+                         (int*)(w + L.arows), (int4*)(w + L.rows4), (float4*)(w + L.basis4));
 }
 
 // out[v] = max_{in-edges e} sum_s basis[e,s] * Y[row(src_e, cell_s)] + Y[root row v] + bias
@@ -999,6 +1074,25 @@ extern "C" int fpm_spline_plan_graphs(const int* src, const int* dst, const floa
                        (float4*)(w + L.basis4));
     return fpm::check_launch("fpm_spline_plan_graphs");
 }
+
+// jobs: device array of njobs PlanJob (host-built: each job's inputs, sizes, first block and
+// 256-aligned offset into ws, where job j's plan needs fpm_spline_plan_bytes(E_j, nodes_j));
+// every job must satisfy the per-graph conditions of fpm_spline_plan_graphs (checked by the
+// caller: graphs of <= 4096 edges, 26 <= nmax <= 1024, num_nodes = ngraphs * nmax).
+extern "C" int fpm_spline_plan_multi(const void* jobs, int njobs, int total_graphs, int nmax, void* ws, void* stream) {
+    FPM_CHECK_ARG(njobs >= 1 && total_graphs >= njobs, "spline_plan_multi: bad job count");
+    FPM_CHECK_ARG(nmax >= NCELL && nmax <= PG_MAXN, "spline_plan_multi: nmax must be in [%d, %d]", NCELL, PG_MAXN);
+    hipStream_t st = (hipStream_t)stream;
+    const PlanJob* J = (const PlanJob*)jobs;
+    hipLaunchKernelGGL(plan_multi_graph_kernel, dim3((unsigned)total_graphs), dim3(PG_THREADS), 0, st, J, njobs, nmax,
+                       (char*)ws);
+    hipLaunchKernelGGL(plan_multi_scan_kernel, dim3((unsigned)njobs), dim3(1024), 0, st, J, (char*)ws);
+    hipLaunchKernelGGL(plan_multi_rank_kernel, dim3((unsigned)total_graphs), dim3(PG_THREADS), 0, st, J, njobs, nmax,
+                       (char*)ws);
+    return fpm::check_launch("fpm_spline_plan_multi");
+}
+
+extern "C" int fpm_spline_plan_job_bytes(void) { return (int)sizeof(PlanJob); }
 
 // Pointers into the plan for the GNN layer (dst CSR with local neighbour indices).
 extern "C" int fpm_spline_plan_csr(void* ws, long E, long num_nodes, int** dst_ptr, int** nbr_local) {

@@ -510,7 +510,8 @@ class Net(nn.Module):
             return max(1, min(self.chunks, B))
         if os.environ.get("FPM_CHUNKS"):
             return max(1, min(int(os.environ["FPM_CHUNKS"]), B))
-        return max(1, min(8, B // 128))
+        # FPM_CHUNK_MIN: fewest pairs per chunk (A/B for small per-GPU batches)
+        return max(1, min(8, B // int(os.environ.get("FPM_CHUNK_MIN", "128"))))
 
     def _enqueue_copy(self, dev, b0, b1, o, done, after=None):
         """ds_mat[b0:b1] -> pinned host memory on the copy stream (the copy is a blit kernel: on a
@@ -590,18 +591,25 @@ class Net(nn.Module):
         o["_lsa_status"] = torch.zeros(B, device=dev, dtype=torch.int32)
         return o
 
-    def _prologue(self, bt, cast=True, col_idx=None):
+    def _prologue(self, bt, parts, cast=True, col_idx=None):
         """Per-forward work before the chunks (main stream): global weights + affinity
         coefficients, the bf16 operand rows of both sides' node features in one launch each (before
         any chunk's ds_mat D2H is in flight: cast per chunk, they ran beside the copy's blit kernel
-        and stalled ~14x; a shared probe side is cast inside its chunk's one-graph SplineConv), and
-        the AFA-U column block once per distinct n2."""
+        and stalled ~14x; a shared probe side is cast inside its chunk's one-graph SplineConv), the
+        AFA-U column block once per distinct n2, and every chunk's spline plans (one launch per plan
+        kernel and side for all chunks, ops.spline_plans_multi: dozens of small latency-bound
+        launches, which stalled ~10x when they ran beside a ds_mat D2H blit, become six, before any
+        copy is in flight) -> (gc, xop, col, plans per chunk or None)."""
+        pre = None
+        if len(parts) > 1:
+            pre = [ops.spline_plans_multi(parts, s, bt.nmax[s]) for s in range(2)]
+            pre = None if any(p is None for p in pre) else [list(pc) for pc in zip(*pre)]
         gc = self.global_coef(bt)
         xop = None
         if self.dtype_mode == "bf16" and cast:
             xop = tuple(None if (s == 0 and bt.shared0) else ops.cast_bf16(bt.x[s]) for s in range(2))
         col = self._afau_col(self.packed(bt.device), bt, col_idx) if self.regression else None
-        return gc, xop, col
+        return gc, xop, col, pre
 
     def _graph_state(self, bt, parts, dev):
         """HIP graphs of one batch's forward, captured on first use and replayed while the batch,
@@ -629,19 +637,26 @@ class Net(nn.Module):
         streams = self._streams(dev)
         pools = [torch.cuda.graph_pool_handle() for _ in range(len(streams) + 1)]
         g["col_idx"] = self._afau_col_index(bt) if self.regression else None
+        if len(parts) > 1:                    # the multi-plan job tables (host-to-device copies)
+            for s_ in range(2):
+                ops.spline_plan_jobs(parts, s_, bt.nmax[s_])
         torch.cuda.synchronize(dev)
         gp = torch.cuda.CUDAGraph()
         # captured on a side stream (capture needs a non-default stream), replayed on the main one
         with torch.cuda.graph(gp, pool=pools[-1], stream=self._copy_stream(dev)):
-            gc, xop, col = self._prologue(bt, col_idx=g["col_idx"])
-        g["prologue"], g["pro_out"] = gp, (gc, xop, col)
+            gc, xop, col, pre = self._prologue(bt, parts, col_idx=g["col_idx"])
+        g["prologue"], g["pro_out"] = gp, (gc, xop, col, pre)
         g["chunks"] = []
         for c, part in enumerate(parts):
             st = streams[c % len(streams)]
             b0, b1 = rng[c]
-            gpl, gst = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gpl, pool=pools[c % len(streams)], stream=st):
-                pl = self.plans(part)
+            gpl, gst = None, torch.cuda.CUDAGraph()
+            if pre is not None:
+                pl = pre[c]
+            else:
+                gpl = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gpl, pool=pools[c % len(streams)], stream=st):
+                    pl = self.plans(part)
             with torch.cuda.graph(gst, pool=pools[c % len(streams)], stream=st):
                 self._stage_a(part, b0, b1, o, False, g["gt_ks"], g["min_pt"], gc, col=col, xop=xop, plans=pl)
             g["chunks"].append((gpl, gst, pl))
@@ -704,9 +719,9 @@ class Net(nn.Module):
         ev_start.record(main)
         if graphed:
             gs["prologue"].replay()
-            gc, xop, col = gs["pro_out"]
+            gc, xop, col, pre = gs["pro_out"]
         else:
-            gc, xop, col = self._prologue(bt, cast=len(parts) > 1)
+            gc, xop, col, pre = self._prologue(bt, parts, cast=len(parts) > 1)
         ev_coef = torch.cuda.Event()
         ev_coef.record(main)
         streams = self._streams(dev) if (len(parts) > 1 and self.n_streams > 1) else [main]
@@ -714,8 +729,9 @@ class Net(nn.Module):
             if st is not main:
                 st.wait_event(ev_coef)
         outs, done, plan_ev = [], [], []
-        # copy deferral: chunk c's D2H waits for the plans of chunk c + 2 (same stream)
-        lag = 2 if (self.copy_defer and len(parts) > 2 and len(streams) == 2 and not device_lsa) else 0
+        # copy deferral (plans computed per chunk only): chunk c's D2H waits for the plans of chunk
+        # c + 2 (same stream)
+        lag = 2 if (self.copy_defer and pre is None and len(parts) > 2 and len(streams) == 2 and not device_lsa) else 0
         events = [None] * len(parts)
         for c, part in enumerate(parts):
             st = streams[c % len(streams)]
@@ -723,12 +739,14 @@ class Net(nn.Module):
             with torch.cuda.stream(st):
                 if graphed:
                     gpl, gst, _ = gs["chunks"][c]
-                    gpl.replay()
+                    if gpl is not None:
+                        gpl.replay()
                 else:
-                    pl = self.plans(part)
-                evp = torch.cuda.Event()
-                evp.record(st)
-                plan_ev.append(evp)
+                    pl = pre[c] if pre is not None else self.plans(part)
+                if lag:
+                    evp = torch.cuda.Event()
+                    evp.record(st)
+                    plan_ev.append(evp)
                 if graphed:
                     gst.replay()
                     outs.append(None)

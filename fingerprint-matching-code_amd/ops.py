@@ -181,6 +181,56 @@ def spline_plan(src, dst, pseudo, num_nodes, nmax, max_graph_edges=0):
     return ws
 
 
+def spline_plan_jobs(parts, side, nmax):
+    """The device job table of spline_plans_multi for ``parts`` (built once, cached while the first
+    part lives; its host-to-device copy must not run inside a graph capture) -> tuple or None."""
+    first = parts[0]
+    dev = first.src[side].device
+    key = (id(first), len(parts), side)
+    store = _PLAN_JOBS.get(key)
+    if store is not None and store[0]() is first:
+        return store
+    import weakref
+    jobs, off, gstart = [], 0, 0
+    for p in parts:
+        E, nn = p.E[side], p.B * nmax
+        if not (0 < p.max_graph_edges(side) <= 4096 and 26 <= nmax <= 1024 and p.B + 1 <= E):
+            _PLAN_JOBS[key] = store = (weakref.ref(first), None)
+            return store
+        nbytes = int(_lib.load().fpm_spline_plan_bytes(E, nn))
+        jobs.append([p.src[side].data_ptr(), p.dst[side].data_ptr(), p.pseudo[side].data_ptr(), E, nn, off,
+                     (gstart << 32) | p.B])
+        off += (nbytes + 255) // 256 * 256
+        gstart += p.B
+    if int(_lib.load().fpm_spline_plan_job_bytes()) != 56:
+        raise _lib.FpmError("spline_plans_multi: PlanJob layout mismatch")
+    table = torch.tensor(jobs, dtype=torch.int64).to(dev)
+    sizes = [int(_lib.load().fpm_spline_plan_bytes(p.E[side], p.B * nmax)) for p in parts]
+    store = (weakref.ref(first), table, [j[5] for j in jobs], sizes, off, gstart)
+    _PLAN_JOBS[key] = store
+    if len(_PLAN_JOBS) > 64:
+        for k in [k for k, v in _PLAN_JOBS.items() if v[0]() is None]:
+            del _PLAN_JOBS[k]
+    return store
+
+
+def spline_plans_multi(parts, side, nmax):
+    """The spline plans of ``side`` for every sub-batch in ``parts`` (pipeline chunks of one batch)
+    by one launch of each per-graph plan kernel (fpm_spline_plan_multi) -> list of plan workspaces
+    (views into one allocation), each identical to spline_plan() of that sub-batch alone; None when
+    some sub-batch needs the global plan kernels (graphs over 4096 edges, nmax outside [26, 1024])."""
+    store = spline_plan_jobs(parts, side, nmax)
+    if store[1] is None:
+        return None
+    _, table, offs, sizes, total, ngraphs = store
+    ws = torch.empty(total, device=table.device, dtype=torch.uint8)
+    _lib.call("fpm_spline_plan_multi", _p(table), len(parts), ngraphs, nmax, _p(ws), _stream(ws))
+    return [ws[o:o + n] for o, n in zip(offs, sizes)]
+
+
+_PLAN_JOBS = {}
+
+
 def plan_csr(ws, E, num_nodes):
     """(dst_ptr, nbr_local) raw device pointers (ints) inside a plan workspace."""
     a, b = ctypes.c_void_p(), ctypes.c_void_p()

@@ -117,6 +117,16 @@ int fpm_spline_plan(const int* src, const int* dst, const float* pseudo, long E,
 int fpm_spline_plan_graphs(const int* src, const int* dst, const float* pseudo, long E, long num_nodes, int nmax,
                            long max_graph_edges, void* ws, long ws_bytes, void* stream);
 int fpm_spline_plan_csr(void* ws, long E, long num_nodes, int** dst_ptr, int** nbr_local);
+/* several per-graph plans (e.g. every pipeline chunk of one side of a batch) by one launch of each
+ * plan kernel.  jobs: device array of njobs records of fpm_spline_plan_job_bytes() (= 56) bytes,
+ * {const int* src; const int* dst; const float* pseudo; long E, num_nodes, ws_off;
+ *  int ngraphs, gstart}: job j's inputs, its first graph's index among all jobs' graphs
+ * (gstart, ascending; total_graphs = the sum of ngraphs) and the 256-aligned offset of its plan
+ * (fpm_spline_plan_bytes(E, num_nodes) bytes) in ws.  Every job must meet fpm_spline_plan_graphs'
+ * per-graph conditions (graphs of <= 4096 edges as contiguous ranges, num_nodes = ngraphs nmax,
+ * 26 <= nmax <= 1024).  Each plan equals fpm_spline_plan_graphs of that job alone. */
+int fpm_spline_plan_multi(const void* jobs, int njobs, int total_graphs, int nmax, void* ws, void* stream);
+int fpm_spline_plan_job_bytes(void);
 int fpm_spline_conv_fwd(int dtype, const void* x_op, const void* plan_ws, long E, long num_nodes, int nmax,
                         const int* nvalid, const void* W, const float* bias, void* y_ws, long y_ws_bytes, int mode,
                         const float* xres, const float* cscale, float* out_f, void* out_t, void* stream);

@@ -462,6 +462,40 @@ def test_chunked_pipeline_bitwise(sd):
         assert torch.equal(c[k], a[k][2:5]), k
 
 
+def test_spline_plans_multi_equal_per_chunk_plans(sd):
+    """Every chunk's spline plans built by one launch per plan kernel (fpm_spline_plan_multi) equal
+    the per-chunk plans: dst CSR arrays identical, and the forward through each plan identical."""
+    pairs = synth.make_batch(27, 9, [48, 40, 44, 48, 30, 48, 47, 41, 48], n2=[48, 47, 40, 30, 48, 44, 48, 48, 39])
+    bt = DeviceBatch.from_pairs(pairs, DEV)
+    parts = bt.split(3, 1)
+    for side in range(2):
+        multi = ops.spline_plans_multi(parts, side, bt.nmax[side])
+        assert multi is not None and len(multi) == len(parts)
+        for p, m in zip(parts, multi):
+            one = ops.spline_plan(p.src[side], p.dst[side], p.pseudo[side], p.B * p.nmax[side], p.nmax[side],
+                                  p.max_graph_edges(side))
+            nn = p.B * p.nmax[side]
+            ca, cb = ops.plan_csr(one, p.E[side], nn), ops.plan_csr(m, p.E[side], nn)
+            for pa, pb, cnt in ((ca[0], cb[0], nn + 1), (ca[1], cb[1], p.E[side])):
+                torch.cuda.synchronize()
+                assert torch.equal(_view_i32(pa, cnt), _view_i32(pb, cnt))
+    net = fpm.Net(regression=True, backbone=False, dtype="bf16", chunks=3)
+    net.load_state_dict(sd)
+    a = net.run(bt)
+    b = net.run(bt, chunks=1)
+    for k in ("s", "ss", "ds_mat", "perm_mat", "k_prob", "cls_prob"):
+        assert torch.equal(a[k], b[k]), k
+
+
+def _view_i32(ptr, n):
+    """A device int32 array at a raw pointer, as a torch tensor (copy)."""
+    out = torch.empty(n, dtype=torch.int32, device=DEV)
+    import ctypes
+    lib = ctypes.CDLL("libamdhip64.so")
+    lib.hipMemcpy(ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ptr), ctypes.c_size_t(4 * n), 3)
+    return out
+
+
 @pytest.mark.parametrize("dtype,regression", [("bf16", True), ("f32", False)])
 def test_graph_replay_bitwise_equals_eager(sd, dtype, regression):
     """Multi-chunk forwards replay HIP graphs captured on the batch's first forward (prologue, and

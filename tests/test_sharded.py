@@ -103,11 +103,11 @@ def test_sharded_forward_data_dict():
 @pytest.mark.gpu
 def test_sharded_host_enqueue_flat():
     """ShardedNet's device threads replay per-shard HIP graphs (captured once per batch object):
-    the host CPU time spent enqueueing per forward (summed over the device threads: the
-    GIL-serialised part) does not grow with the shard count, and the outputs stay equal to the
-    single-device forward."""
+    the host CPU time spent enqueueing a 1024-pair forward (summed over the device threads: the
+    GIL-serialised part) stays flat from 1 to 4 shards (~1 ms per forward, vs ~8 ms of eager
+    launches at C3), and the outputs stay equal to the single-device forward."""
     sd = params.init_params(7)
-    pairs = synth.make_batch(43, 256, 64)
+    pairs = synth.make_batch(43, 1024, 32)
     net = fpm.Net(regression=True, dtype="bf16", backbone=False)
     net.load_state_dict(sd)
     bt = DeviceBatch.from_pairs(pairs, DEV)
@@ -123,5 +123,26 @@ def test_sharded_host_enqueue_flat():
             else:
                 enq[n] = min(enq.get(n, 1.0), sh.last_timing["enqueue_cpu_s"])
         assert all(t["graphs"] for t in sh.last_timing["shards"])
-    print("enqueue per forward: 1 shard %.2f ms, 4 shards %.2f ms" % (enq[1] * 1e3, enq[4] * 1e3))
-    assert enq[4] < max(2.0 * enq[1], 2e-3), enq
+    print("enqueue CPU per 1024-pair forward: 1 shard %.2f ms, 4 shards %.2f ms" % (enq[1] * 1e3, enq[4] * 1e3))
+    assert enq[4] < 2.0 * enq[1] + 1.5e-3, enq
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two or more GPUs (distinct devices)")
+def test_sharded_distinct_devices_equal_single_device():
+    """Real cross-device sharding (peer copies of the shards, per-device streams and graphs, the
+    gather's peer copies into the output device): equal to the single-device forward bit for bit.
+    Runs on the first multi-GPU box (the one-GPU pool skips it)."""
+    sd = params.init_params(7)
+    pairs = synth.make_batch(45, 10, [48, 40, 44, 48, 30, 48, 47, 41, 48, 36], n2=[48, 47, 40, 30, 48, 44, 48, 48, 39, 48])
+    net = fpm.Net(regression=True, dtype="bf16", backbone=False)
+    net.load_state_dict(sd)
+    bt = DeviceBatch.from_pairs(pairs, DEV)
+    ref = net.run(bt)
+    devices = list(range(min(4, torch.cuda.device_count())))
+    sh = ShardedNet(net, devices=devices)
+    for _ in range(2):
+        out = sh.run(bt)
+        for k in ("s", "ss", "ds_mat", "perm_mat", "k_prob", "cls_prob"):
+            assert out[k].device == DEV
+            assert torch.equal(out[k], ref[k]), k
