@@ -227,6 +227,8 @@ def main():
                          "256 pairs/GPU, fp32; c4 = 1 probe x --gallery graphs (n=128) sharded over ranks, probe "
                          "stage shared; c5 = n=512, 1024 pairs/GPU")
     ap.add_argument("--gallery", type=int, default=10000, help="c4: gallery size over all ranks")
+    ap.add_argument("--tuning", default="", help="kernel-variant switches for A/B runs, key=value[,key=value] "
+                    "(fpm_set_tuning keys, include/fpm.h); recorded in the JSON line")
     args = ap.parse_args()
     if args.config == "c2":
         args.n, args.batch, args.dtype = 128, 256, "f32"
@@ -278,6 +280,12 @@ def main():
     shared_devices = ndev < world
     torch.cuda.set_device(local % ndev)
     dev = torch.device("cuda", local % ndev)
+    tuning = {}
+    for kv in filter(None, args.tuning.split(",")):
+        key, val = kv.split("=")
+        from fpm import ops as _ops
+        _ops.set_tuning(key, int(val))
+        tuning[key] = int(val)
     sd = params.init_params(args.seed)
     net = fpm.Net(regression=True, backbone=False, dtype=args.dtype, lsa_threads=args.lsa_threads or None)
     net.load_state_dict(sd)
@@ -475,6 +483,7 @@ def main():
             "f32_line": f32_line,
             "strong_scaling": strong,
             "share128_line": share_line,
+            "tuning": tuning or None,
             "ranks_share_devices": shared_devices,
             "input_gen_s": t_gen,
             "graph_build": graph_build,

@@ -78,6 +78,7 @@ int& plan_graph_flag();
 int& combine_npb_flag();
 int& sinkhorn_bwd_reg_flag();
 int& sinkhorn_fast_flag();
+int& sinkhorn_lform_flag();
 int& soft_topk_fast_flag();
 int& afau_attn_v_flag();
 
@@ -88,6 +89,7 @@ extern "C" int fpm_set_tuning(const char* key, int value) {
     else if (key && !strcmp(key, "combine_npb")) f = &combine_npb_flag();
     else if (key && !strcmp(key, "sinkhorn_bwd_reg")) f = &sinkhorn_bwd_reg_flag();
     else if (key && !strcmp(key, "sinkhorn_fast")) f = &sinkhorn_fast_flag();
+    else if (key && !strcmp(key, "sinkhorn_lform")) f = &sinkhorn_lform_flag();
     else if (key && !strcmp(key, "topk_fast")) f = &soft_topk_fast_flag();
     else if (key && !strcmp(key, "afau_attn_v")) f = &afau_attn_v_flag();
     if (!f) {

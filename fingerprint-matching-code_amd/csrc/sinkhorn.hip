@@ -11,6 +11,7 @@
 // Arithmetic runs in log2 units (L2 = L log2 e): every exp/log is one native v_exp_f32 / v_log_f32.
 #include "fpm_common.h"
 #include <cstdlib>
+#include <type_traits>
 
 namespace {
 
@@ -558,6 +559,301 @@ __global__ __launch_bounds__(1024) void sinkhorn_bwd_sweep_kernel(SinkArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Forward, max(n1max, n2max) <= 256: the log matrix itself is the register tile (L form).  Each
+// step subtracts its lines' logsumexps from L, as the reference's ``L -= logsumexp(L, dim)``
+// (pygmtools sinkhorn; oracle/ngm_oracle.py sinkhorn_m), instead of keeping S / tau and two
+// potential vectors (sinkhorn_reg_kernel, kept for the backward's replay).  A step's subtraction is
+// deferred into the next step's pass, which reads every entry anyway: one subtract, one v_exp and
+// one add per entry and step, the subtract and the add on packed-f32 pairs (v_pk_add_f32), against
+// two adds, a subtract, the v_exp and an add in the potential form.  The dummy rows (nd identical
+// rows of value -100 over the valid algorithmic columns) are one log vector in LDS (``ldv``,
+// indexed along the physical axis that carries the algorithmic columns).
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+template <int ER, int EC, int NT>
+__global__ __launch_bounds__(NT) void sinkhorn_lform_kernel(SinkArgs a) {
+    static_assert(EC % 2 == 0, "column pairs");
+    constexpr int NCOL = 32 * EC, EP = EC / 2, NP = ER > EC ? ER : EC;
+    constexpr int TR = NT / 32, NW = NT / 64;   // thread rows, waves
+    constexpr int NLD = (TR * ER > NCOL) ? TR * ER : NCOL;
+    static_assert(NCOL <= NT, "one thread per column in the column reductions");
+    __shared__ float red_m[NW][NCOL];
+    __shared__ float red_s[NW][NCOL];
+    __shared__ float fin[NCOL];
+    __shared__ float ldv[NLD];
+    __shared__ float ud_sh;
+    __shared__ int redo_flag;
+
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int tr = tid >> 5, tc = tid & 31, wv = tid >> 6, lane = tid & 63;
+    const int n1b = a.n1[b], n2b = a.n2[b];
+    const bool transposed = n1b > n2b;
+    const int R = transposed ? n2b : n1b;
+    const int C = transposed ? n1b : n2b;
+    const int nd = (a.dummy_row && C > R) ? (C - R) : 0;
+    const float fnd = (float)nd;
+    const int limPR = a.contig_j ? n1b : n2b;
+    const int limPC = a.contig_j ? n2b : n1b;
+    const int boxPR = a.contig_j ? a.n1max : a.n2max;
+    const int boxPC = a.contig_j ? a.n2max : a.n1max;
+    const bool u_on_R = (a.contig_j != 0) == (!transposed);
+    const float DUMMY = -100.f * fpm::LOG2E_F;
+
+    const float* in = a.in + (long)b * a.in_sb;
+    const int ispr = (int)(a.contig_j ? a.in_si : a.in_sj);
+    const int ispc = (int)(a.contig_j ? a.in_sj : a.in_si);
+
+    f2 L[ER][EP];   // entry (tr + 32 e, tc + 32 (2p + k)) in L[e][p][k]
+#pragma unroll
+    for (int e = 0; e < ER; ++e) {
+        const int pr = tr + TR * e;
+#pragma unroll
+        for (int p = 0; p < EP; ++p) {
+            f2 v = {-INFINITY, -INFINITY};
+            const int pc0 = tc + 64 * p, pc1 = pc0 + 32;
+            if (pr < limPR && pc0 < limPC) v.x = (in[pr * ispr + pc0 * ispc] / a.tau) * fpm::LOG2E_F;
+            if (pr < limPR && pc1 < limPC) v.y = (in[pr * ispr + pc1 * ispc] / a.tau) * fpm::LOG2E_F;
+            L[e][p] = v;
+        }
+    }
+    // pending deltas of the last step (row deltas pd[e] after a row-side step, column deltas pd[f]
+    // after a column-side step), subtracted by the next pass
+    float pd[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) pd[k] = 0.f;
+    // dummy log vector along the algorithmic-column axis: pr (u_on_R false) or pc (u_on_R true)
+    const int limY = u_on_R ? limPC : limPR;
+    for (int k = tid; k < NLD; k += NT) ldv[k] = (nd > 0 && k < limY) ? DUMMY : -INFINITY;
+    if (tid == 0) redo_flag = 0;
+    __syncthreads();
+
+    auto ok_s = [](float x) { return x >= 0x1p-30f && x <= 0x1p30f; };
+    // The bounds tests are recomputed where they are used, from copies the compiler cannot see
+    // through: hoisted and shared between the loads, the steps and the stores, the 128 per-entry
+    // masks stayed live for the whole kernel (SGPR spills into VGPR lanes, then VGPR spills).
+    auto opaque = [](int v) { asm volatile("" : "+v"(v)); return v; };
+#define pc_of(f) (tc + 32 * (f))   // f = 2p + k
+    // Thread coordinates, re-derived inside each step for the same reason: loop-invariant lane
+    // indices, row numbers and LDS addresses hoisted out of the step loop held ~30 VGPRs.
+#define SK_LOCAL_COORDS                                                       \
+    const int tid = opaque((int)threadIdx.x);                                 \
+    const int tr = tid >> 5, tc = tid & 31, wv = tid >> 6, lane = tid & 63;   \
+    (void)tr; (void)tc; (void)wv; (void)lane;
+
+    // Row side: every physical row pr minus its lse over pc (+ the dummy term when the pr axis
+    // carries the algorithmic columns, add_dummy).  Pending column deltas come in.
+    auto step_R = [&](bool add_dummy, bool fast) __attribute__((always_inline)) {
+        SK_LOCAL_COORDS
+        const int limR = opaque(limPR);
+        // the pending column deltas first, in one unconditional pass (L is written in one place
+        // per step: updates inside the fast / fallback branches merged into register copies)
+        {
+            f2 dc[EP];
+#pragma unroll
+            for (int p = 0; p < EP; ++p) dc[p] = f2{pd[2 * p], pd[2 * p + 1]};
+#pragma unroll
+            for (int e = 0; e < ER; ++e)
+#pragma unroll
+                for (int p = 0; p < EP; ++p) L[e][p] -= dc[p];
+        }
+        if (fast) {
+            float s[ER];
+#pragma unroll
+            for (int e = 0; e < ER; ++e) {
+                f2 acc = {fpm::fast_exp2(L[e][0].x), fpm::fast_exp2(L[e][0].y)};
+#pragma unroll
+                for (int p = 1; p < EP; ++p) acc += f2{fpm::fast_exp2(L[e][p].x), fpm::fast_exp2(L[e][p].y)};
+                s[e] = acc.x + acc.y;
+            }
+#pragma unroll
+            for (int e = 0; e < ER; ++e) s[e] = lane32_sum(s[e]);
+            bool bad = false;
+#pragma unroll
+            for (int e = 0; e < ER; ++e) {
+                const int pr = tr + TR * e;
+                if (add_dummy) s[e] += fnd * fpm::fast_exp2(ldv[pr < NLD ? pr : 0]);
+                bad |= pr < limR && !ok_s(s[e]);
+            }
+            if (__ballot(bad) == 0ull) {
+#pragma unroll
+                for (int e = 0; e < ER; ++e) {
+                    const int pr = tr + TR * e;
+                    pd[e] = pr < limR ? fpm::fast_log2(s[e]) : 0.f;
+                    if (add_dummy && tc == 0 && pr < limR) ldv[pr] -= pd[e];
+                }
+                return;
+            }
+        }
+        // max-shifted lse on L (pending deltas already applied)
+#pragma unroll
+        for (int e = 0; e < ER; ++e) {
+            const int pr = tr + TR * e;
+            float m = -INFINITY;
+#pragma unroll
+            for (int p = 0; p < EP; ++p) m = fmaxf(m, fmaxf(L[e][p].x, L[e][p].y));
+            m = lane32_max(m);
+            const float ld = add_dummy ? ldv[pr < NLD ? pr : 0] : -INFINITY;
+            m = fmaxf(m, ld);
+            float t = 0.f;
+            if (m != -INFINITY) {
+#pragma unroll
+                for (int p = 0; p < EP; ++p)
+                    t += fpm::fast_exp2(L[e][p].x - m) + fpm::fast_exp2(L[e][p].y - m);
+            }
+            t = lane32_sum(t);
+            if (add_dummy && m != -INFINITY) t += fnd * fpm::fast_exp2(ld - m);
+            pd[e] = (m == -INFINITY || pr >= limR) ? 0.f : m + fpm::fast_log2(t);
+            if (add_dummy && tc == 0 && pr < limR) ldv[pr] -= pd[e];
+        }
+    };
+
+    // Column side: every physical column pc minus its lse over pr (+ the dummy term when the pc
+    // axis carries the algorithmic columns).  Pending row deltas come in; the 32 thread rows of a
+    // column reduce through one lane swap and LDS.
+    auto step_C = [&](bool add_dummy, bool fast) __attribute__((always_inline)) {
+        SK_LOCAL_COORDS
+        const int limC = opaque(limPC);
+#pragma unroll
+        for (int e = 0; e < ER; ++e) {
+            const f2 dr = {pd[e], pd[e]};
+#pragma unroll
+            for (int p = 0; p < EP; ++p) L[e][p] -= dr;
+        }
+        if (fast) {
+            f2 cs[EP];
+#pragma unroll
+            for (int p = 0; p < EP; ++p) cs[p] = f2{fpm::fast_exp2(L[0][p].x), fpm::fast_exp2(L[0][p].y)};
+#pragma unroll
+            for (int e = 1; e < ER; ++e)
+#pragma unroll
+                for (int p = 0; p < EP; ++p) cs[p] += f2{fpm::fast_exp2(L[e][p].x), fpm::fast_exp2(L[e][p].y)};
+#pragma unroll
+            for (int p = 0; p < EP; ++p) {
+                const float s0 = cs[p].x + xor32(cs[p].x), s1 = cs[p].y + xor32(cs[p].y);
+                if (lane < 32) {
+                    red_s[wv][pc_of(2 * p)] = s0;
+                    red_s[wv][pc_of(2 * p + 1)] = s1;
+                }
+            }
+            __syncthreads();
+            if (tid < NCOL) {
+                float s = red_s[0][tid];
+                for (int w = 1; w < NW; ++w) s += red_s[w][tid];
+                if (add_dummy) s += fnd * fpm::fast_exp2(ldv[tid < NLD ? tid : 0]);
+                if (tid >= limC) fin[tid] = 0.f;
+                else if (ok_s(s)) fin[tid] = fpm::fast_log2(s);
+                else redo_flag = 1;
+            }
+            __syncthreads();
+            const bool redo = redo_flag != 0;
+            if (!redo) {
+#pragma unroll
+                for (int f = 0; f < EC; ++f) pd[f] = fin[pc_of(f)];
+                if (add_dummy && tid < NCOL && tid < limC) ldv[tid] -= fin[tid];
+                return;   // the next read of ldv / redo_flag is behind a barrier
+            }
+        }
+        // max-shifted: per-thread (max, sum) over its ER rows, combined over the column
+#pragma unroll
+        for (int f = 0; f < EC; ++f) {
+            const int p = f >> 1;
+            float m = -INFINITY;
+#pragma unroll
+            for (int e = 0; e < ER; ++e) m = fmaxf(m, (f & 1) ? L[e][p].y : L[e][p].x);
+            float s = 0.f;
+            if (m != -INFINITY) {
+#pragma unroll
+                for (int e = 0; e < ER; ++e) s += fpm::fast_exp2(((f & 1) ? L[e][p].y : L[e][p].x) - m);
+            }
+            float mo = xor32(m), so = xor32(s);
+            lse_combine(m, s, mo, so);
+            if (lane < 32) {
+                red_m[wv][pc_of(f)] = m;
+                red_s[wv][pc_of(f)] = s;
+            }
+        }
+        __syncthreads();
+        if (tid < NCOL) {
+            float m = red_m[0][tid], s = red_s[0][tid];
+            for (int w = 1; w < NW; ++w) lse_combine(m, s, red_m[w][tid], red_s[w][tid]);
+            if (add_dummy) lse_combine(m, s, ldv[tid < NLD ? tid : 0], fnd);
+            const float d = (m == -INFINITY || tid >= limC) ? 0.f : m + fpm::fast_log2(s);
+            fin[tid] = d;
+            if (add_dummy && tid < limC) ldv[tid] -= d;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int f = 0; f < EC; ++f) pd[f] = fin[pc_of(f)];
+        if (tid == 0) redo_flag = 0;    // every thread read it before the barrier above
+    };
+
+    // dummy rows: ldv minus its lse over the valid algorithmic columns (one wave; rare path)
+    auto update_dummy = [&]() __attribute__((always_inline)) {
+        SK_LOCAL_COORDS
+        __syncthreads();
+        if (wv == 0) {
+            float m = -INFINITY;
+            for (int k = lane; k < limY; k += 64) m = fmaxf(m, ldv[k]);
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+            float s = 0.f;
+            for (int k = lane; k < limY; k += 64) s += fpm::fast_exp2(ldv[k] - m);
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+            const float d = m == -INFINITY ? 0.f : m + fpm::fast_log2(s);
+            for (int k = lane; k < limY; k += 64) ldv[k] -= d;
+        }
+        __syncthreads();
+    };
+    (void)ud_sh;
+
+    // Steps in (row, column) pairs with the physical sides fixed at compile time: L then flows
+    // through straight-line code (a runtime choice of side per step merged the two updated tiles
+    // at every join -- register copies and spills).  Row steps (even) normalise the algorithmic
+    // rows; column steps (odd) count the dummy rows.  Returns whether the last step was row-side.
+    auto run_steps = [&](auto rfirst) __attribute__((always_inline)) {
+        constexpr bool RF = decltype(rfirst)::value;
+        int it = 0;
+        for (; it + 1 < a.iters; it += 2) {
+            const bool fast0 = it > 0 && a.fast;
+            if constexpr (RF) step_R(false, fast0); else step_C(false, fast0);
+            if (nd > 0) update_dummy();
+            if constexpr (RF) step_C(nd > 0, a.fast != 0); else step_R(nd > 0, a.fast != 0);
+        }
+        if (it < a.iters) {
+            const bool fast0 = it > 0 && a.fast;
+            if constexpr (RF) step_R(false, fast0); else step_C(false, fast0);
+            if (nd > 0) update_dummy();
+            return RF;
+        }
+        return !RF;
+    };
+    const bool last_R = u_on_R ? run_steps(std::true_type{}) : run_steps(std::false_type{});
+
+    float* out = a.out + (long)b * a.out_sb;
+    const int opr = (int)(a.contig_j ? a.out_si : a.out_sj);
+    const int opc = (int)(a.contig_j ? a.out_sj : a.out_si);
+#undef pc_of
+#undef SK_LOCAL_COORDS
+    const int oPR = opaque(limPR), oPC = opaque(limPC), obPR = opaque(boxPR), obPC = opaque(boxPC);
+#pragma unroll
+    for (int e = 0; e < ER; ++e) {
+        const int pr = tr + TR * e;
+        if (pr >= obPR) continue;
+#pragma unroll
+        for (int f = 0; f < EC; ++f) {
+            const int pc = tc + 32 * f;
+            if (pc >= obPC) continue;
+            const float l = (f & 1) ? L[e][f >> 1].y : L[e][f >> 1].x;
+            float v = 0.f;
+            if (pr < oPR && pc < oPC) v = fpm::fast_exp2(l - (last_R ? pd[e] : pd[f]));
+            out[pr * opr + pc * opc] = v;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Large blocks (max(n1max, n2max) > 256, e.g. n = 512): the block no longer fits the register file,
 // so every half-iteration streams the pair's block from L2 / HBM (1 MB at n = 512) while the
 // potentials stay in LDS.  Same algorithm and semantics as sinkhorn_reg_kernel; the per-thread
@@ -810,6 +1106,14 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
 // row/column rescales with a log-domain fallback when a line sum leaves [2^-40, 2^40] -- was
 // measured 2.8x slower at n = 256, tau = 0.01: small temperatures move the potentials by tens of
 // log2 units per step, so the guard tripped on most steps; removed.)
+// Forward kernel for blocks <= 256 (fpm_set_tuning("sinkhorn_lform")): 1 (default) the L-form
+// register kernel, 2 the same with 512 threads x 128 entries at n = 256, 0 the potential-form
+// sinkhorn_reg_kernel (A/B).
+int& sinkhorn_lform_flag() {
+    static int v = 1;
+    return v;
+}
+
 int& sinkhorn_fast_flag() {
     static int v = [] {
         const char* e = getenv("FPM_SINKHORN_FAST");
@@ -868,12 +1172,21 @@ extern "C" int fpm_sinkhorn_log_fwd(const float* s, long s_sb, long s_si, long s
     int nmax = n1max > n2max ? n1max : n2max;
     hipStream_t st = (hipStream_t)stream;
     void (*k)(SinkArgs) = nullptr;
-    if (nmax <= 32) k = sinkhorn_reg_kernel<1, 1>;
-    else if (nmax <= 64) k = sinkhorn_reg_kernel<2, 2>;
-    else if (nmax <= 128) k = sinkhorn_reg_kernel<4, 4>;
-    else if (nmax <= 256) k = sinkhorn_reg_kernel<8, 8>;
+    int nt = 1024;
+    if (sinkhorn_lform_flag()) {
+        if (nmax <= 32) k = sinkhorn_lform_kernel<1, 2, 1024>;
+        else if (nmax <= 64) k = sinkhorn_lform_kernel<2, 2, 1024>;
+        else if (nmax <= 128) k = sinkhorn_lform_kernel<4, 4, 1024>;
+        else if (nmax <= 256 && sinkhorn_lform_flag() == 2) { k = sinkhorn_lform_kernel<16, 8, 512>; nt = 512; }
+        else if (nmax <= 256) k = sinkhorn_lform_kernel<8, 8, 1024>;
+    } else {
+        if (nmax <= 32) k = sinkhorn_reg_kernel<1, 1>;
+        else if (nmax <= 64) k = sinkhorn_reg_kernel<2, 2>;
+        else if (nmax <= 128) k = sinkhorn_reg_kernel<4, 4>;
+        else if (nmax <= 256) k = sinkhorn_reg_kernel<8, 8>;
+    }
     if (k)
-        hipLaunchKernelGGL(k, dim3(B), dim3(1024), 0, st, a);
+        hipLaunchKernelGGL(k, dim3(B), dim3(nt), 0, st, a);
     else
         hipLaunchKernelGGL(sinkhorn_stream_kernel, dim3(B), dim3(1024), 0, st, a);
     return fpm::check_launch("fpm_sinkhorn_log_fwd");

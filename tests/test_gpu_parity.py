@@ -39,21 +39,29 @@ def sd():
     ((256, 256), (256, 256), 20, 0.01),
     ((200, 256, 131), (256, 190, 256), 10, 0.01),
 ])
-def test_sinkhorn_vs_oracle(n1s, n2s, iters, tau):
+@pytest.mark.parametrize("lform", [1, 2, 0])
+def test_sinkhorn_vs_oracle(n1s, n2s, iters, tau, lform):
+    """Register-tile forwards (lform 1: L-form, 1024 threads; 2: L-form, 512 threads at n = 256;
+    0: potential form) against the float64 oracle."""
     g = torch.Generator().manual_seed(len(n1s) * 100 + n1s[0])
     B = len(n1s)
     n1max, n2max = max(n1s), max(n2s)
     s = torch.randn(B, n1max, n2max, generator=g) * 0.3
     ref = O.pygm_sinkhorn(s.double(), n1s, n2s, dummy_row=True, max_iter=iters, tau=tau)
-    out = ops.sinkhorn(s.to(DEV), _i32(n1s), _i32(n2s), iters, tau, True).cpu()
+    prev = ops.set_tuning("sinkhorn_lform", lform)
+    try:
+        out = ops.sinkhorn(s.to(DEV), _i32(n1s), _i32(n2s), iters, tau, True).cpu()
+        # strided (transposed) input and output views
+        sT = s.transpose(1, 2).contiguous().to(DEV).transpose(1, 2)
+        o2 = torch.zeros(B, n2max, n1max, device=DEV).transpose(1, 2)
+        ops.sinkhorn(sT, _i32(n1s), _i32(n2s), iters, tau, True, out=o2)
+    finally:
+        ops.set_tuning("sinkhorn_lform", prev)
     assert (out.double() - ref).abs().max() < 1e-4
-    # strided (transposed) input and output views
-    sT = s.transpose(1, 2).contiguous().to(DEV).transpose(1, 2)
-    o2 = torch.zeros(B, n2max, n1max, device=DEV).transpose(1, 2)
-    ops.sinkhorn(sT, _i32(n1s), _i32(n2s), iters, tau, True, out=o2)
     assert (o2.cpu().double() - ref).abs().max() < 1e-4
 
 
+@pytest.mark.parametrize("lform", [1, 0])
 @pytest.mark.parametrize("form", [0, 1])
 @pytest.mark.parametrize("n1s,n2s,iters,tau,scale", [
     ((256, 200, 131), (256, 256, 240), 20, 0.001, 0.1),    # small tau: shifted sums out of range -> max-shifted
@@ -63,7 +71,7 @@ def test_sinkhorn_vs_oracle(n1s, n2s, iters, tau):
     ((64, 50), (64, 64), 1, 0.05, 0.3),                     # a single (log-domain) step
     ((128, 128, 77), (128, 60, 128), 21, 0.02, 1.0),        # odd step count, dummy rows, transposed pair
 ])
-def test_sinkhorn_forms_vs_oracle(form, n1s, n2s, iters, tau, scale):
+def test_sinkhorn_forms_vs_oracle(form, n1s, n2s, iters, tau, scale, lform):
     """Both Sinkhorn step forms (0 max-shifted log, 1 shifted single-pass lse with its range guard)
     against the float64 oracle, incl. inputs that trip the guards
     (scale < 0: |scale| x randn with column 3 and row 5 set to -6, ~330 log2 units below the
@@ -76,6 +84,7 @@ def test_sinkhorn_forms_vs_oracle(form, n1s, n2s, iters, tau, scale):
         s[:, 5, :] = -6.0
     ref = O.pygm_sinkhorn(s.double(), n1s, n2s, dummy_row=True, max_iter=iters, tau=tau)
     prev = ops.set_tuning("sinkhorn_fast", form)
+    prev_l = ops.set_tuning("sinkhorn_lform", lform)
     try:
         out = ops.sinkhorn(s.to(DEV), _i32(n1s), _i32(n2s), iters, tau, True).cpu()
         sT = s.transpose(1, 2).contiguous().to(DEV).transpose(1, 2)
@@ -83,6 +92,7 @@ def test_sinkhorn_forms_vs_oracle(form, n1s, n2s, iters, tau, scale):
         ops.sinkhorn(sT, _i32(n1s), _i32(n2s), iters, tau, True, out=o2)
     finally:
         ops.set_tuning("sinkhorn_fast", prev)
+        ops.set_tuning("sinkhorn_lform", prev_l)
     assert (out.double() - ref).abs().max() < 1e-4
     assert (o2.cpu().double() - ref).abs().max() < 1e-4
 
