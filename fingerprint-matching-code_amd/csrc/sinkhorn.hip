@@ -1107,8 +1107,9 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
 // measured 2.8x slower at n = 256, tau = 0.01: small temperatures move the potentials by tens of
 // log2 units per step, so the guard tripped on most steps; removed.)
 // Forward kernel for blocks <= 256 (fpm_set_tuning("sinkhorn_lform")): 1 (default) the L-form
-// register kernel, 2 the same with 512 threads x 128 entries at n = 256, 0 the potential-form
-// sinkhorn_reg_kernel (A/B).
+// register kernel, 0 the potential-form sinkhorn_reg_kernel (A/B: 0.444 vs 0.501 ms per launch at
+// 1024 pairs, n = 256, 20 steps, profiles/r03k_sinkhorn_kernel_ab.txt; a 512-thread L-form with 128
+// entries per thread measured 0.578 ms and was dropped).
 int& sinkhorn_lform_flag() {
     static int v = 1;
     return v;
@@ -1172,12 +1173,10 @@ extern "C" int fpm_sinkhorn_log_fwd(const float* s, long s_sb, long s_si, long s
     int nmax = n1max > n2max ? n1max : n2max;
     hipStream_t st = (hipStream_t)stream;
     void (*k)(SinkArgs) = nullptr;
-    int nt = 1024;
     if (sinkhorn_lform_flag()) {
         if (nmax <= 32) k = sinkhorn_lform_kernel<1, 2, 1024>;
         else if (nmax <= 64) k = sinkhorn_lform_kernel<2, 2, 1024>;
         else if (nmax <= 128) k = sinkhorn_lform_kernel<4, 4, 1024>;
-        else if (nmax <= 256 && sinkhorn_lform_flag() == 2) { k = sinkhorn_lform_kernel<16, 8, 512>; nt = 512; }
         else if (nmax <= 256) k = sinkhorn_lform_kernel<8, 8, 1024>;
     } else {
         if (nmax <= 32) k = sinkhorn_reg_kernel<1, 1>;
@@ -1186,7 +1185,7 @@ extern "C" int fpm_sinkhorn_log_fwd(const float* s, long s_sb, long s_si, long s
         else if (nmax <= 256) k = sinkhorn_reg_kernel<8, 8>;
     }
     if (k)
-        hipLaunchKernelGGL(k, dim3(B), dim3(nt), 0, st, a);
+        hipLaunchKernelGGL(k, dim3(B), dim3(1024), 0, st, a);
     else
         hipLaunchKernelGGL(sinkhorn_stream_kernel, dim3(B), dim3(1024), 0, st, a);
     return fpm::check_launch("fpm_sinkhorn_log_fwd");

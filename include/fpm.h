@@ -95,8 +95,7 @@ int fpm_cast_bf16(const float* x, void* y, long n, void* stream);
  *   "sinkhorn_fast" (FPM_SINKHORN_FAST, default 1): shifted single-pass lse after the first step
  *       (0 = max-shifted lse every step; 2 = 1 with scalar loads in the n > 256 streaming kernel)
  *   "sinkhorn_lform" (default 1): Sinkhorn forward for n <= 256 on the L-form register kernel
- *       (the log matrix as the tile, lse subtracted per step; 2 = 512-thread tiles at n = 256) or
- *       on the potential-form kernel (0)
+ *       (the log matrix as the tile, lse subtracted per step) or on the potential-form kernel (0)
  *   "topk_fast" (FPM_TOPK_FAST, default 1): shifted single-pass early soft top-k column steps */
 int fpm_set_tuning(const char* key, int value);
 

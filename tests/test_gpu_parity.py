@@ -39,10 +39,9 @@ def sd():
     ((256, 256), (256, 256), 20, 0.01),
     ((200, 256, 131), (256, 190, 256), 10, 0.01),
 ])
-@pytest.mark.parametrize("lform", [1, 2, 0])
+@pytest.mark.parametrize("lform", [1, 0])
 def test_sinkhorn_vs_oracle(n1s, n2s, iters, tau, lform):
-    """Register-tile forwards (lform 1: L-form, 1024 threads; 2: L-form, 512 threads at n = 256;
-    0: potential form) against the float64 oracle."""
+    """Register-tile forwards (lform 1: L-form, 0: potential form) against the float64 oracle."""
     g = torch.Generator().manual_seed(len(n1s) * 100 + n1s[0])
     B = len(n1s)
     n1max, n2max = max(n1s), max(n2s)

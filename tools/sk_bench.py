@@ -15,7 +15,7 @@ s = (torch.randn(B, n, n, generator=g) * 0.3).to(dev)
 nn_ = torch.full((B,), n, dtype=torch.int32, device=dev)
 out = torch.empty_like(s)
 res = {}
-for v in (0, 1, 2):
+for v in (0, 1):
     prev = ops.set_tuning("sinkhorn_lform", v)
     for _ in range(3):
         ops.sinkhorn(s, nn_, nn_, 20, 0.05, True, out=out)
