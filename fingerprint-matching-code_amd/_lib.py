@@ -60,6 +60,8 @@ SIGNATURES = {
     "fpm_match_cls_ws_floats": (L, [I, I, I]),
     "fpm_match_cls_fwd": (I, [I, P, P, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),
     "fpm_lsa_batch_host": (I, [P, L, L, P, P, I, I, P, I]),
+    "fpm_lsa_submit": (L, [P, L, L, P, P, I, I, P, I]),
+    "fpm_lsa_wait": (I, [L, I, ctypes.POINTER(ctypes.c_double)]),
     "fpm_lsa_batch_device": (I, [P, L, L, P, P, I, I, I, P, P, P]),
     "fpm_csr_dot_csc_to_dense": (I, [I, P, P, P, P, P, P, L, L, L, P, P]),
     "fpm_dense_dot_csc_to_dense": (I, [I, P, P, P, P, L, L, L, L, P, P]),

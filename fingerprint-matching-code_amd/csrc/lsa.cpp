@@ -43,8 +43,12 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
+#include <deque>
 #include <functional>
+#include <map>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -714,6 +718,99 @@ Pool& pool() {
     return p;
 }
 
+// Asynchronous batches: a FIFO of jobs served pair by pair by persistent workers, so a batch's
+// pairs start as soon as workers free up -- while the previous batch's slowest pairs still run --
+// instead of each batch waiting for the whole pool (fpm_lsa_submit / fpm_lsa_wait).
+struct LsaJob {
+    const float* s;
+    long sb, ld;
+    const int* n1;
+    const int* n2;
+    int B, n1max;
+    int* assign;
+    std::atomic<int> next{0};
+    int done = 0;            // guarded by the queue mutex
+    int fail = 0;            // first failing pair + 1
+    std::chrono::steady_clock::time_point t0, t1;
+    bool started = false;
+};
+
+class Queue {
+  public:
+    long submit(std::unique_ptr<LsaJob> job, int nthreads) {
+        std::lock_guard<std::mutex> lk(mu_);
+        while ((int)workers_.size() < nthreads) workers_.emplace_back([this] { loop(); });
+        const long id = ++last_id_;
+        LsaJob* j = job.get();
+        jobs_[id] = std::move(job);
+        if (j->B > 0) fifo_.push_back(j);
+        cv_.notify_all();
+        return id;
+    }
+    // 0 / failing pair + 1 when done (seconds: first pair start -> last pair end); -2 while running
+    int wait(long id, bool block, double* seconds) {
+        std::unique_lock<std::mutex> lk(mu_);
+        auto it = jobs_.find(id);
+        if (it == jobs_.end()) return -1;
+        LsaJob* j = it->second.get();
+        if (!block && j->done < j->B) return -2;
+        done_cv_.wait(lk, [&] { return j->done >= j->B; });
+        const int rc = j->fail;
+        if (seconds) *seconds = j->B > 0 ? std::chrono::duration<double>(j->t1 - j->t0).count() : 0.0;
+        jobs_.erase(it);
+        return rc;
+    }
+    ~Queue() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : workers_) t.join();
+    }
+
+  private:
+    void loop() {
+        std::unique_lock<std::mutex> lk(mu_);
+        while (true) {
+            cv_.wait(lk, [&] { return stop_ || !fifo_.empty(); });
+            if (stop_) return;
+            LsaJob* j = fifo_.front();
+            const int b = j->next.fetch_add(1);
+            if (b >= j->B) {                 // every pair of the front job is taken
+                if (!fifo_.empty() && fifo_.front() == j) fifo_.pop_front();
+                continue;
+            }
+            if (b == j->B - 1 && fifo_.front() == j) fifo_.pop_front();
+            if (!j->started) {
+                j->started = true;
+                j->t0 = std::chrono::steady_clock::now();
+            }
+            lk.unlock();
+            const int rc = lsa_pair(j->s + (long)b * j->sb, j->ld, j->n1[b], j->n2[b], j->assign + (long)b * j->n1max,
+                                    j->n1max);
+            lk.lock();
+            if (rc && (j->fail == 0 || b + 1 < j->fail)) j->fail = b + 1;
+            if (++j->done == j->B) {
+                j->t1 = std::chrono::steady_clock::now();
+                done_cv_.notify_all();
+            }
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    std::vector<std::thread> workers_;
+    std::deque<LsaJob*> fifo_;
+    std::map<long, std::unique_ptr<LsaJob>> jobs_;
+    long last_id_ = 0;
+    bool stop_ = false;
+};
+
+Queue& queue() {
+    static Queue q;
+    return q;
+}
+
 }  // namespace
 
 extern "C" {
@@ -741,6 +838,24 @@ int fpm_lsa_batch_host(const float* s, long sb, long ld, const int* n1, const in
         pool().run(nthreads, B, work);
     }
     return fail.load();
+}
+
+// Asynchronous form of fpm_lsa_batch_host: queue the batch (pointers must stay valid until
+// fpm_lsa_wait) and return a ticket > 0.  Pairs of successive batches are served first-in first-out
+// by nthreads persistent workers.
+long fpm_lsa_submit(const float* s, long sb, long ld, const int* n1, const int* n2, int B, int n1max, int* assign,
+                    int nthreads) {
+    std::unique_ptr<LsaJob> j(new LsaJob());
+    j->s = s; j->sb = sb; j->ld = ld; j->n1 = n1; j->n2 = n2;
+    j->B = B < 0 ? 0 : B; j->n1max = n1max; j->assign = assign;
+    return queue().submit(std::move(j), nthreads < 1 ? 1 : nthreads);
+}
+
+// block != 0: wait for the ticket's batch; returns 0 or the first failing pair + 1 (like
+// fpm_lsa_batch_host) and releases the ticket.  block == 0: -2 while it is still running.  -1: unknown
+// ticket.  seconds (optional): the batch's span from its first pair's start to its last pair's end.
+int fpm_lsa_wait(long ticket, int block, double* seconds) {
+    return queue().wait(ticket, block != 0, seconds);
 }
 
 }  // extern "C"

@@ -125,12 +125,18 @@ class Net(nn.Module):
         # the last chunk halved this many times: the two streams' last chunks land together, so the
         # host Hungarian's tail after the GPU is their (short) LSA
         self.tail_splits = int(os.environ.get("FPM_TAIL", "2"))
+        # FPM_TAIL_PAIR=1: halve the last two chunks as equal pairs instead (DeviceBatch.split)
+        self.tail_pair = os.environ.get("FPM_TAIL_PAIR", "0") != "0"
         # defer each chunk's ds_mat D2H until the spline plans of the chunk queued two places later
         # (same compute stream) have run: those latency-bound kernels otherwise run beside the
         # copy's blit kernel and stall ~10x
         self.copy_defer = int(os.environ.get("FPM_COPY_DEFER", "1"))
         if self.copy_defer not in (0, 1):
             raise ValueError("FPM_COPY_DEFER must be 0 or 1")
+        # FPM_LSA_ASYNC=1: chunks' Hungarian batches queue on persistent workers that serve pairs
+        # first-in first-out across chunks (a chunk's pairs start while the previous chunk's slowest
+        # pairs still run) instead of one blocking batch per chunk
+        self.lsa_async = os.environ.get("FPM_LSA_ASYNC", "1") != "0"
         # FPM_GRAPHS=1: multi-chunk inference forwards replay HIP graphs captured per (batch, chunk)
         # (host enqueue 8 -> 1 ms per 1024 pairs; the GPU stage measured 4 % slower than eager
         # launches, so off by default; fpm.parallel.ShardedNet turns it on); see run()
@@ -563,13 +569,15 @@ class Net(nn.Module):
                       logits=o["cls_logits"][b0:b1], prob=o["cls_prob"][b0:b1],
                       dtype=ops.BF16 if self.dtype_mode == "bf16" else ops.F32)
 
-    def _stage_c(self, part, b0, b1, o):
+    def _stage_c(self, part, b0, b1, o, assign=None):
         """Host Hungarian (utils/hungarian.py: LSA of -ds_mat per pair) + greedy selection +
-        MatchClassifier of one chunk; the caller waits for the chunk's D2H event first."""
+        MatchClassifier of one chunk; the caller waits for the chunk's D2H event first.  ``assign``:
+        the chunk's assignment when its Hungarian already ran (ops.lsa_submit)."""
         dev = part.device
         wp = self._pack
         t = time.perf_counter()
-        assign = ops.lsa_batch_host(self._pinned[b0:b1], part.n_host[0], part.n_host[1], self.lsa_threads)
+        if assign is None:
+            assign = ops.lsa_batch_host(self._pinned[b0:b1], part.n_host[0], part.n_host[1], self.lsa_threads)
         dt = time.perf_counter() - t
         assign_d = assign.to(dev, non_blocking=True)
         ops.topk_select(o["ds_mat"][b0:b1], assign_d, o["_kk"][b0:b1], lsa_out=o["lsa"][b0:b1],
@@ -668,7 +676,7 @@ class Net(nn.Module):
         K = chunks if chunks is not None else self.pipeline_chunks(bt.B)
         if self.compute_ke:
             K = 1          # Ke blocks are padded to per-chunk edge maxima: keep one chunk
-        return bt.split(K, self.tail_splits if K > 1 else 0)
+        return bt.split(K, self.tail_splits if K > 1 else 0, pair=self.tail_pair and self.n_streams == 2)
 
     def _graphed(self, parts, keep_feats=False):
         return (self.use_graphs and not keep_feats and self.lsa_mode != "device" and not self.compute_ke
@@ -779,14 +787,40 @@ class Net(nn.Module):
                 events[c] = self._enqueue_copy(dev, pb0, pb1, o, pdone)
         t_enq, t_enqc = time.perf_counter(), time.thread_time()
         t_lsa, t_first = 0.0, None
+        timeline = []      # per chunk: host ms (from t0) when its ds_mat had landed / its stage C was queued
+        pending = []       # chunks whose Hungarian is queued on the LSA workers (lsa_async)
+
+        def finish(entry, assign):
+            c_, part_, b0_, b1_, tk, t_rdy_ = entry
+            with torch.cuda.stream(streams[c_ % len(streams)]):
+                self._stage_c(part_, b0_, b1_, o, assign=assign)
+            timeline.append((round((t_rdy_ - t0) * 1e3, 3), round((time.perf_counter() - t0) * 1e3, 3)))
+            return tk.seconds
+
         for c, (part, ev) in enumerate(zip(parts, events)):
             if device_lsa:
                 break
             b0, b1 = (0, B) if part is bt else part.pair_range
             ev.synchronize()
-            t_first = t_first or time.perf_counter()
+            t_rdy = time.perf_counter()
+            t_first = t_first or t_rdy
+            if self.lsa_async and len(parts) > 1:
+                # queue this chunk's pairs behind the earlier chunks' on the workers, then run the
+                # selection / classifier of every earlier chunk whose Hungarian has finished
+                tk = ops.lsa_submit(self._pinned[b0:b1], part.n_host[0], part.n_host[1], self.lsa_threads)
+                pending.append((c, part, b0, b1, tk, t_rdy))
+                while len(pending) > 1:
+                    a = ops.lsa_wait(pending[0][4], block=False)
+                    if a is None:
+                        break
+                    t_lsa += finish(pending.pop(0), a)
+                continue
             with torch.cuda.stream(streams[c % len(streams)]):
                 t_lsa += self._stage_c(part, b0, b1, o)
+            timeline.append((round((t_rdy - t0) * 1e3, 3), round((time.perf_counter() - t0) * 1e3, 3)))
+        while pending:
+            t_lsa += finish(pending[0], ops.lsa_wait(pending[0][4]))
+            pending.pop(0)
         for st in streams:
             if st is not main:
                 main.wait_stream(st)
@@ -818,7 +852,8 @@ class Net(nn.Module):
         # GPU time of the stages before the Hungarian (all chunks), from events on the streams
         self.last_timing = dict(gpu_stage_s=ev_start.elapsed_time(events[-1]) / 1e3, lsa_s=t_lsa,
                                 first_chunk_wait_s=(t_first or t0) - t0, chunks=len(parts), graphs=graphed,
-                                enqueue_s=t_enq - t0, enqueue_cpu_s=t_enqc - t0c, total_s=time.perf_counter() - t0)
+                                enqueue_s=t_enq - t0, enqueue_cpu_s=t_enqc - t0c, total_s=time.perf_counter() - t0,
+                                chunk_timeline_ms=timeline)
         return res
 
     def image_features(self, images, Ps, ns, dev=None):

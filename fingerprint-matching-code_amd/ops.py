@@ -437,6 +437,44 @@ def lsa_batch_host(s_host, n1_host, n2_host, nthreads=1):
     return out
 
 
+class LsaTicket:
+    """A batch queued on the host LSA workers (``lsa_submit``); holds its tensors until waited."""
+
+    def __init__(self, ticket, keep, out):
+        self.ticket, self._keep, self.out = ticket, keep, out
+        self.seconds = 0.0
+
+
+def lsa_submit(s_host, n1_host, n2_host, nthreads=1):
+    """Asynchronous ``lsa_batch_host``: queue the batch on the persistent LSA workers (pairs of
+    successive batches are served first-in first-out) and return a ticket for ``lsa_wait``."""
+    if s_host.is_cuda:
+        raise _lib.FpmError("lsa_submit expects host memory")
+    s_host = s_host.contiguous()
+    B, n1max, n2max = s_host.shape
+    n1c = n1_host.to(torch.int32).contiguous()
+    n2c = n2_host.to(torch.int32).contiguous()
+    out = torch.empty(B, n1max, dtype=torch.int32)
+    t = _lib.load().fpm_lsa_submit(_p(s_host), n1max * n2max, n2max, _p(n1c), _p(n2c), B, n1max, _p(out),
+                                   int(nthreads))
+    return LsaTicket(t, (s_host, n1c, n2c), out)
+
+
+def lsa_wait(tk, block=True):
+    """The assignment of a ``lsa_submit`` batch ((B, n1max) int32), or None if ``block`` is False
+    and it is still running.  ``tk.seconds``: the batch's span on the workers."""
+    sec = ctypes.c_double(0.0)
+    rc = _lib.load().fpm_lsa_wait(tk.ticket, 1 if block else 0, ctypes.byref(sec))
+    if rc == -2:
+        return None
+    if rc == -1:
+        raise _lib.FpmError("lsa_wait: unknown or already waited ticket")
+    tk.seconds = sec.value
+    if rc != 0:
+        raise _lib.FpmError("fpm_lsa_submit: pair %d is infeasible or has NaN/-inf costs" % (rc - 1))
+    return tk.out
+
+
 # ---- training backward (SURVEY §8f rank 3) -----------------------------------------------------
 def sinkhorn_bwd(s, dp, ds, n1, n2, iters, tau, dummy_row, ws):
     """d/ds of ``sinkhorn`` given dp = d/d(out); s, dp: strided (B, n1max, n2max) views; ds contiguous."""

@@ -412,6 +412,15 @@ int fpm_kron_gnn_layer_bwd_point(const float* X, int C, int B, int n1max, int n2
  * assignment bit for bit (tests/test_lsa_isa.py). */
 int fpm_lsa_batch_host(const float* s, long sb, long ld, const int* n1, const int* n2, int B, int n1max, int* assign,
                        int nthreads);
+/* Asynchronous form (the pipelined forward's Hungarian): fpm_lsa_submit queues the batch on
+ * nthreads persistent workers that serve pairs first-in first-out across batches and returns a
+ * ticket > 0 (the pointers must stay valid until the wait); fpm_lsa_wait(ticket, block, seconds)
+ * returns 0 / failing pair + 1 like fpm_lsa_batch_host and releases the ticket, -2 while the batch
+ * is still running when block == 0, -1 for an unknown ticket; seconds (optional) receives the
+ * batch's span on the workers. */
+long fpm_lsa_submit(const float* s, long sb, long ld, const int* n1, const int* n2, int B, int n1max, int* assign,
+                    int nthreads);
+int fpm_lsa_wait(long ticket, int block, double* seconds);
 
 #ifdef __cplusplus
 }

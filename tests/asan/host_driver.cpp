@@ -9,6 +9,7 @@
 //     sb > n1max * ld) and single-row batches, 1 and 8 pool threads, several calls reusing the pool;
 //     every assignment is a valid matching whose cost equals a brute-force optimum (n <= 8) and
 //     equals the single-thread result bit for bit; NaN input reports the failing pair.
+//   * fpm_lsa_submit / fpm_lsa_wait: two batches queued from two threads equal the synchronous result.
 //   * the sparse host twins against dense products on random CSR/CSC data (f32 and f64), incl. the
 //     two-call protocol of csr_dot_csc_to_csr with an exact and an undersized capacity.
 #include <math.h>
@@ -19,6 +20,7 @@
 
 #include <algorithm>
 #include <random>
+#include <thread>
 #include <vector>
 
 #include "fpm.h"
@@ -88,6 +90,19 @@ static void test_lsa(std::mt19937& rng) {
             rc = fpm_lsa_batch_host(s.data(), sb, ld, n1.data(), n2.data(), cs.B, cs.n1max, a8.data(), 8);
             CHECK(rc == 0, "lsa rc %d (8 threads)", rc);
             CHECK(a1 == a8, "lsa: pool result differs from the single-thread result");
+            // the asynchronous queue: two batches in flight from two submitting threads
+            std::vector<int> q1((size_t)cs.B * cs.n1max, -5), q2((size_t)cs.B * cs.n1max, -5);
+            long t1 = 0, t2 = 0;
+            std::thread th([&] { t2 = fpm_lsa_submit(s.data(), sb, ld, n1.data(), n2.data(), cs.B, cs.n1max, q2.data(), 8); });
+            t1 = fpm_lsa_submit(s.data(), sb, ld, n1.data(), n2.data(), cs.B, cs.n1max, q1.data(), 8);
+            th.join();
+            double sec = -1.0;
+            rc = fpm_lsa_wait(t2, 1, &sec);
+            CHECK(rc == 0 && sec >= 0.0, "lsa async rc %d", rc);
+            rc = fpm_lsa_wait(t1, 1, nullptr);
+            CHECK(rc == 0, "lsa async rc %d", rc);
+            CHECK(fpm_lsa_wait(t1, 1, nullptr) == -1, "lsa async: released ticket still known");
+            CHECK(q1 == a1 && q2 == a1, "lsa: async queue result differs from the synchronous one");
         }
         for (int b = 0; b < cs.B; ++b) {
             const int* a = a1.data() + (size_t)b * cs.n1max;

@@ -1,0 +1,57 @@
+"""Asynchronous host LSA queue (fpm_lsa_submit / fpm_lsa_wait, the pipelined forward's Hungarian):
+batches submitted back to back, served pair by pair first-in first-out by persistent workers,
+return exactly the synchronous solver's (scipy's) assignments; non-blocking polls; errors."""
+import numpy as np
+import pytest
+import scipy.optimize as opt
+import torch
+
+from fpm import _lib, ops
+
+
+def _ref(s, n1, n2):
+    r, c = opt.linear_sum_assignment(s[:n1, :n2] * -1)
+    a = -np.ones(s.shape[0], np.int32)
+    a[r] = c
+    return a
+
+
+def _batch(rng, B, n1max, n2max, ties=False):
+    s = np.zeros((B, n1max, n2max), np.float32)
+    n1 = rng.integers(1, n1max + 1, B).astype(np.int32)
+    n2 = rng.integers(1, n2max + 1, B).astype(np.int32)
+    for b in range(B):
+        shp = (n1[b], n2[b])
+        s[b, :n1[b], :n2[b]] = rng.integers(0, 3, shp) if ties else rng.random(shp) ** 4
+    return torch.from_numpy(s), torch.from_numpy(n1), torch.from_numpy(n2)
+
+
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_lsa_submit_fifo_matches_sync_and_scipy(threads):
+    rng = np.random.default_rng(11)
+    batches = [_batch(rng, B, 40, 37, ties=(i % 2 == 1)) for i, B in enumerate((17, 1, 9, 30, 0, 5))]
+    tickets = [ops.lsa_submit(s, n1, n2, threads) for s, n1, n2 in batches]
+    # poll the last one without blocking (may or may not be done), then wait in reverse order
+    first = ops.lsa_wait(tickets[-1], block=False)
+    for tk, (s, n1, n2) in reversed(list(zip(tickets, batches))):
+        if tk is tickets[-1] and first is not None:
+            got = first
+        else:
+            got = ops.lsa_wait(tk)
+        assert got.shape == (s.shape[0], s.shape[1])
+        sync = ops.lsa_batch_host(s, n1, n2, threads)
+        assert torch.equal(got, sync)
+        for b in range(s.shape[0]):
+            np.testing.assert_array_equal(got[b].numpy(), _ref(s[b].numpy(), int(n1[b]), int(n2[b])))
+        assert tk.seconds >= 0.0
+
+
+def test_lsa_wait_errors():
+    rng = np.random.default_rng(3)
+    s, n1, n2 = _batch(rng, 4, 12, 12)
+    s[2, 0, 0] = float("nan")
+    tk = ops.lsa_submit(s, n1, n2, 2)
+    with pytest.raises(_lib.FpmError, match="pair 2"):
+        ops.lsa_wait(tk)
+    with pytest.raises(_lib.FpmError):
+        ops.lsa_wait(tk)          # already released
