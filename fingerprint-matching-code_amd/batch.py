@@ -32,35 +32,20 @@ class DeviceBatch:
         self.edge_off = edge_off
         self._splits = {}
 
-    def split(self, k, tail=0, pair=False):
+    def split(self, k, tail=0):
         """k contiguous sub-batches of pairs (views of x/w, renumbered edge copies); cached.
         ``tail`` > 0 halves the last chunk ``tail`` times (a short final chunk shortens the host
-        Hungarian that runs after the GPU has finished).  ``pair``: split the last TWO chunks
-        instead, as equal pairs of halving sizes (S/2, S/2, S/4, S/4, ..., then the rest in two), so
-        that on two alternating streams each pair of chunks lands together and the Hungarian left
-        after the GPU is that of the smallest pair."""
+        Hungarian that runs after the GPU has finished).  (Halving the last two chunks as equal
+        pairs -- 64, 64, 32, 32, ... -- shortened that tail but slowed the GPU stage 2-4 % with the
+        extra chunks: profiles/r03l_tail_split_ab.txt.)"""
         if k <= 1 or self.B < 2:
             return [self]
-        key = (k, tail, pair)
+        key = (k, tail)
         if key in self._splits:
             return self._splits[key]
         if self.edge_off is None:
             raise ValueError("split() needs per-pair edge offsets")
         bounds = [round(i * self.B / k) for i in range(k + 1)]
-        if pair and k >= 2 and tail > 0:
-            a = bounds[-3]
-            rest, h, sizes = self.B - a, (self.B - a) // 2, []
-            for _ in range(tail):
-                h //= 2
-                if h < 1 or rest - 2 * h < 2:
-                    break
-                sizes += [h, h]
-                rest -= 2 * h
-            sizes += [rest // 2, rest - rest // 2]
-            bounds = bounds[:-2]
-            for sz in sizes:
-                bounds.append(bounds[-1] + sz)
-            tail = 0
         for _ in range(tail):
             a, b = bounds[-2], bounds[-1]
             if b - a >= 2:

@@ -125,8 +125,6 @@ class Net(nn.Module):
         # the last chunk halved this many times: the two streams' last chunks land together, so the
         # host Hungarian's tail after the GPU is their (short) LSA
         self.tail_splits = int(os.environ.get("FPM_TAIL", "2"))
-        # FPM_TAIL_PAIR=1: halve the last two chunks as equal pairs instead (DeviceBatch.split)
-        self.tail_pair = os.environ.get("FPM_TAIL_PAIR", "0") != "0"
         # defer each chunk's ds_mat D2H until the spline plans of the chunk queued two places later
         # (same compute stream) have run: those latency-bound kernels otherwise run beside the
         # copy's blit kernel and stall ~10x
@@ -676,7 +674,7 @@ class Net(nn.Module):
         K = chunks if chunks is not None else self.pipeline_chunks(bt.B)
         if self.compute_ke:
             K = 1          # Ke blocks are padded to per-chunk edge maxima: keep one chunk
-        return bt.split(K, self.tail_splits if K > 1 else 0, pair=self.tail_pair and self.n_streams == 2)
+        return bt.split(K, self.tail_splits if K > 1 else 0)
 
     def _graphed(self, parts, keep_feats=False):
         return (self.use_graphs and not keep_feats and self.lsa_mode != "device" and not self.compute_ke
