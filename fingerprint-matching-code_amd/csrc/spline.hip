@@ -648,10 +648,13 @@ __global__ __launch_bounds__(PG_THREADS) void plan_multi_rank_kernel(const PlanJ
 
 // out[v] = max_{in-edges e} sum_s basis[e,s] * Y[row(src_e, cell_s)] + Y[root row v] + bias
 //   mode 0: relu(.) ; mode 1: xres[v] + 0.1 * (.)   (+ optional per-pair column scale on out_t)
-// One wave per node, 12 channels per lane (3 x 4 contiguous).  (An in-edge prefetch variant --
-// row ids in lanes, two edges' 8 product rows in flight -- measured neutral and was dropped.)
+// One wave per node, 12 channels per lane: 8 contiguous at 8 lane (one 16-B bf16 load per product
+// row) + 4 at 512 + 4 lane (comb_chan).  (An in-edge prefetch variant -- row ids in lanes, two
+// edges' 8 product rows in flight -- measured neutral and was dropped.)
 // ARG (training forward): also record, per (node, channel), the CSR slot of the in-edge attaining
 // the max (the first one in CSR order, -1 without in-edges) for the scatter backward.
+__device__ __forceinline__ int comb_chan(int lane, int t) { return t < 2 ? 8 * lane + 4 * t : 512 + 4 * lane; }
+
 template <typename T, int NPB = 4, bool ARG = false>
 __global__ __launch_bounds__(64 * NPB) void combine_kernel(const T* __restrict__ Y, const int* __restrict__ cell_off,
                                                       const float* __restrict__ bias,
@@ -686,13 +689,14 @@ __global__ __launch_bounds__(64 * NPB) void combine_kernel(const T* __restrict__
     for (int e = beg; e < end; ++e) {
         const int4 r = rows4[e];
         const float4 bs = basis4[e];
-        const T* y0 = Y + (long)r.x * 768;
-        const T* y1 = Y + (long)r.y * 768;
-        const T* y2 = Y + (long)r.z * 768;
-        const T* y3 = Y + (long)r.w * 768;
+        // 16-B aligned rows (768 channels): lets the two 8-B loads of t = 0, 1 merge into one
+        const T* y0 = (const T*)__builtin_assume_aligned(Y + (long)r.x * 768, 16);
+        const T* y1 = (const T*)__builtin_assume_aligned(Y + (long)r.y * 768, 16);
+        const T* y2 = (const T*)__builtin_assume_aligned(Y + (long)r.z * 768, 16);
+        const T* y3 = (const T*)__builtin_assume_aligned(Y + (long)r.w * 768, 16);
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
-            const int c0 = 4 * lane + 256 * t;
+            const int c0 = comb_chan(lane, t);
             float a0[4], a1[4], a2[4], a3[4];
             fpm::load4(y0 + c0, a0);
             fpm::load4(y1 + c0, a1);
@@ -714,27 +718,33 @@ __global__ __launch_bounds__(64 * NPB) void combine_kernel(const T* __restrict__
     if constexpr (ARG) {
 #pragma unroll
         for (int t = 0; t < 3; ++t)
-            *(int4*)(argmax + v * 768 + 4 * lane + 256 * t) = make_int4(am[t][0], am[t][1], am[t][2], am[t][3]);
+            *(int4*)(argmax + v * 768 + comb_chan(lane, t)) = make_int4(am[t][0], am[t][1], am[t][2], am[t][3]);
     }
-    const T* yr = Y + root_row * 768;
+    const T* yr = (const T*)__builtin_assume_aligned(Y + root_row * 768, 16);
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
-        const int c0 = 4 * lane + 256 * t;
-        float rt[4];
+        const int c0 = comb_chan(lane, t);
+        float rt[4], bi[4], xr[4] = {0.f, 0.f, 0.f, 0.f};
         fpm::load4(yr + c0, rt);
+        fpm::load4(bias + c0, bi);                       // 16-B vector loads (rows are 3 KB aligned)
+        if (mode != 0) fpm::load4(xres + v * 768 + c0, xr);
         float y[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            float o = (m[t][j] + rt[j]) + bias[c0 + j];
+            float o = (m[t][j] + rt[j]) + bi[j];
             if (mode == 0) y[j] = fmaxf(o, 0.f);
-            else y[j] = xres[v * 768 + c0 + j] + 0.1f * o;
+            else y[j] = xr[j] + 0.1f * o;
             if (!valid) y[j] = 0.f;
         }
         if (out_f) *(float4*)(out_f + v * 768 + c0) = make_float4(y[0], y[1], y[2], y[3]);
         if (out_t) {
-            float z[4];
+            float z[4] = {y[0], y[1], y[2], y[3]};
+            if (cscale) {
+                float cs[4];
+                fpm::load4(cscale + (long)b * 768 + c0, cs);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) z[j] = cscale ? y[j] * cscale[(long)b * 768 + c0 + j] : y[j];
+                for (int j = 0; j < 4; ++j) z[j] = y[j] * cs[j];
+            }
             fpm::store4(out_t + v * 768 + c0, z);
         }
     }

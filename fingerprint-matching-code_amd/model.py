@@ -135,6 +135,7 @@ class Net(nn.Module):
         # first-in first-out across chunks (a chunk's pairs start while the previous chunk's slowest
         # pairs still run) instead of one blocking batch per chunk
         self.lsa_async = os.environ.get("FPM_LSA_ASYNC", "1") != "0"
+        self._enqueue_lock = None      # set by fpm.parallel.ShardedNet (one lock for its replicas)
         # FPM_GRAPHS=1: multi-chunk inference forwards replay HIP graphs captured per (batch, chunk)
         # (host enqueue 8 -> 1 ms per 1024 pairs; the GPU stage measured 4 % slower than eager
         # launches, so off by default; fpm.parallel.ShardedNet turns it on); see run()
@@ -721,69 +722,77 @@ class Net(nn.Module):
             gt_ks.copy_(torch.as_tensor(gt_perm).to(dev).reshape(B, -1).sum(-1).to(torch.float32))
         elif graphed:
             gt_ks.copy_(min_pt)        # synthetic pairs: identity ground truth
-        ev_start = torch.cuda.Event(enable_timing=True)
-        ev_start.record(main)
-        if graphed:
-            gs["prologue"].replay()
-            gc, xop, col, pre = gs["pro_out"]
-        else:
-            gc, xop, col, pre = self._prologue(bt, parts, cast=len(parts) > 1)
-        ev_coef = torch.cuda.Event()
-        ev_coef.record(main)
-        streams = self._streams(dev) if (len(parts) > 1 and self.n_streams > 1) else [main]
-        for st in streams:
-            if st is not main:
-                st.wait_event(ev_coef)
-        outs, done, plan_ev = [], [], []
-        # copy deferral (plans computed per chunk only): chunk c's D2H waits for the plans of chunk
-        # c + 2 (same stream)
-        lag = 2 if (self.copy_defer and pre is None and len(parts) > 2 and len(streams) == 2 and not device_lsa) else 0
-        events = [None] * len(parts)
-        for c, part in enumerate(parts):
-            st = streams[c % len(streams)]
-            b0, b1 = (0, B) if part is bt else part.pair_range     # a chunk's range inside bt
-            with torch.cuda.stream(st):
-                if graphed:
-                    gpl, gst, _ = gs["chunks"][c]
-                    if gpl is not None:
-                        gpl.replay()
-                else:
-                    pl = pre[c] if pre is not None else self.plans(part)
-                if lag:
-                    evp = torch.cuda.Event()
-                    evp.record(st)
-                    plan_ev.append(evp)
-                if graphed:
-                    gst.replay()
-                    outs.append(None)
-                else:
-                    outs.append(self._stage_a(part, b0, b1, o, keep_feats, gt_ks, min_pt, gc, col=col, xop=xop,
-                                              plans=pl))
-                if device_lsa:
-                    # the Hungarian kernel is latency-bound (one wave per pair): run it and the
-                    # selection / classifier on a side stream so the next chunks' GPU stages are not
-                    # queued behind it
-                    ev = torch.cuda.Event(enable_timing=True)
+        # ShardedNet: device threads enqueue one at a time (their HIP calls contend otherwise)
+        lk = self._enqueue_lock
+        if lk is not None:
+            lk.acquire()
+        try:
+            ev_start = torch.cuda.Event(enable_timing=True)
+            ev_start.record(main)
+            if graphed:
+                gs["prologue"].replay()
+                gc, xop, col, pre = gs["pro_out"]
+            else:
+                gc, xop, col, pre = self._prologue(bt, parts, cast=len(parts) > 1)
+            ev_coef = torch.cuda.Event()
+            ev_coef.record(main)
+            streams = self._streams(dev) if (len(parts) > 1 and self.n_streams > 1) else [main]
+            for st in streams:
+                if st is not main:
+                    st.wait_event(ev_coef)
+            outs, done, plan_ev = [], [], []
+            # copy deferral (plans computed per chunk only): chunk c's D2H waits for the plans of chunk
+            # c + 2 (same stream)
+            lag = 2 if (self.copy_defer and pre is None and len(parts) > 2 and len(streams) == 2 and not device_lsa) else 0
+            events = [None] * len(parts)
+            for c, part in enumerate(parts):
+                st = streams[c % len(streams)]
+                b0, b1 = (0, B) if part is bt else part.pair_range     # a chunk's range inside bt
+                with torch.cuda.stream(st):
+                    if graphed:
+                        gpl, gst, _ = gs["chunks"][c]
+                        if gpl is not None:
+                            gpl.replay()
+                    else:
+                        pl = pre[c] if pre is not None else self.plans(part)
+                    if lag:
+                        evp = torch.cuda.Event()
+                        evp.record(st)
+                        plan_ev.append(evp)
+                    if graphed:
+                        gst.replay()
+                        outs.append(None)
+                    else:
+                        outs.append(self._stage_a(part, b0, b1, o, keep_feats, gt_ks, min_pt, gc, col=col, xop=xop,
+                                                  plans=pl))
+                    if device_lsa:
+                        # the Hungarian kernel is latency-bound (one wave per pair): run it and the
+                        # selection / classifier on a side stream so the next chunks' GPU stages are not
+                        # queued behind it
+                        ev = torch.cuda.Event(enable_timing=True)
+                        ev.record(st)
+                        side = self._lsa_streams(dev)[c % 2]
+                        side.wait_event(ev)
+                        with torch.cuda.stream(side):
+                            self._stage_c_device(part, b0, b1, o)
+                        events[c] = ev
+                        continue
+                    ev = torch.cuda.Event()
                     ev.record(st)
-                    side = self._lsa_streams(dev)[c % 2]
-                    side.wait_event(ev)
-                    with torch.cuda.stream(side):
-                        self._stage_c_device(part, b0, b1, o)
-                    events[c] = ev
-                    continue
-                ev = torch.cuda.Event()
-                ev.record(st)
-                done.append((b0, b1, ev))
-            if not lag:
-                events[c] = self._enqueue_copy(dev, b0, b1, o, ev)
-            elif c >= lag:
-                pb0, pb1, pdone = done[c - lag]
-                events[c - lag] = self._enqueue_copy(dev, pb0, pb1, o, pdone, after=plan_ev[c])
-        if lag:
-            for c in range(max(0, len(parts) - lag), len(parts)):
-                pb0, pb1, pdone = done[c]
-                events[c] = self._enqueue_copy(dev, pb0, pb1, o, pdone)
-        t_enq, t_enqc = time.perf_counter(), time.thread_time()
+                    done.append((b0, b1, ev))
+                if not lag:
+                    events[c] = self._enqueue_copy(dev, b0, b1, o, ev)
+                elif c >= lag:
+                    pb0, pb1, pdone = done[c - lag]
+                    events[c - lag] = self._enqueue_copy(dev, pb0, pb1, o, pdone, after=plan_ev[c])
+            if lag:
+                for c in range(max(0, len(parts) - lag), len(parts)):
+                    pb0, pb1, pdone = done[c]
+                    events[c] = self._enqueue_copy(dev, pb0, pb1, o, pdone)
+            t_enq, t_enqc = time.perf_counter(), time.thread_time()
+        finally:
+            if lk is not None:
+                lk.release()
         t_lsa, t_first = 0.0, None
         timeline = []      # per chunk: host ms (from t0) when its ds_mat had landed / its stage C was queued
         pending = []       # chunks whose Hungarian is queued on the LSA workers (lsa_async)

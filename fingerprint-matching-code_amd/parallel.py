@@ -74,11 +74,16 @@ class ShardedNet(nn.Module):
         self._replicas = [_replica(net) for _ in self.devices]
         # one shared Hungarian pool: each device's batch uses the whole share in turn
         threads = lsa_threads or 2 * host_cpu_share()
+        enq_lock = threading.Lock()
         for r in self._replicas:
             r.lsa_threads = threads
             # every device thread enqueues its shard under the one GIL: its multi-chunk forwards
             # replay HIP graphs (~0.1 ms of host time per chunk instead of ~0.8 ms of launches)
             r.use_graphs = True
+            # one device thread enqueues at a time: concurrent HIP calls from the device threads
+            # contend in the runtime (enqueue CPU per 1024 pairs ~1.2 ms, in some runs ~6 ms with 4
+            # shards on one device)
+            r._enqueue_lock = enq_lock
         self._shards = None
         self.last_timing = {}
 
