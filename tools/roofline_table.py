@@ -45,6 +45,7 @@ def work(n, E, rows_per_node):
         ("gnn_layer_kernel<17", "bytes", (17 + 17) * f4 + (17 + 2) * f4, 2, "layers 2-3: X in, 16 ch + z / vpart + z out"),
         ("gnn_layer_kernel<1,", "bytes", 18 * f4, 1, "layer 1: 1 ch in, 16 ch + z out"),
         ("sinkhorn_reg_kernel", "bytes", 4 * 2 * f4, 4, "3 GNN Sinkhorns (20 it) + final (10 it), s in, out out"),
+        ("sinkhorn_lform_kernel", "bytes", 4 * 2 * f4, 4, "3 GNN Sinkhorns (20 it) + final (10 it), s in, out out"),
         ("sinkhorn_stream_kernel", "bytes", 4 * 2 * f4, 4, "same, n > 256"),
         ("soft_topk_kernel", "bytes", 2 * f4, 1, "ss in, ds_mat out"),
         ("combine_kernel", "bytes", 2 * (comb_l1 + comb_l2), 4, "2 sides x 2 layers: product rows + output (+ residual)"),
