@@ -7,7 +7,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfpm_hip.so")
+# FPM_LIB_PATH: an alternative in-tree build (A/B timing of two builds in one GPU call)
+LIB_PATH = os.environ.get("FPM_LIB_PATH") or os.path.join(_HERE, "libfpm_hip.so")
 
 P = ctypes.c_void_p
 I = ctypes.c_int

@@ -19,10 +19,14 @@ __device__ __forceinline__ float bf2f(bf16_t h) {
 }
 
 // round-to-nearest-even f32 -> bf16 (inputs are finite here; NaN handling not required)
-__device__ __forceinline__ bf16_t f2bf(float f) {
-    uint32_t u = __float_as_uint(f);
-    u += 0x7FFFu + ((u >> 16) & 1u);
-    return (bf16_t)(u >> 16);
+// fp32 -> bf16, round to nearest even: the native v_cvt_pk_bf16_f32 (identical to the integer
+// rounding u += 0x7FFF + ((u >> 16) & 1) for every non-NaN input, denormals included)
+__device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+// two values in one v_cvt_pk_bf16_f32: lo in bits 0-15, hi in bits 16-31
+typedef float f32x2_cvt_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_cvt_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t f2bf2(float lo, float hi) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_cvt_t){lo, hi}, bf16x2_cvt_t));
 }
 
 template <typename T> __device__ __forceinline__ float to_f(T v);

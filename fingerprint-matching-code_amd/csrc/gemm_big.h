@@ -171,16 +171,21 @@ __global__ __launch_bounds__(G2_THREADS, 1) void gemm_big_kernel(GemmParams p) {
     if (!F32OUT) {
         // bf16 tile [256][BN] with (2*BN + 16)-B rows
         constexpr int ROW = BN * 2 + 16;
+        // rows j, j+1 of a lane's column converted by one v_cvt_pk_bf16_f32, the halves stored
+        // with ds_write_b16 / ds_write_b16_d16_hi
 #pragma unroll
         for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < 4; j += 2) {
                 const int r = wm * FM * 16 + fm * 16 + (lane >> 4) * 4 + j;
 #pragma unroll
                 for (int fn = 0; fn < FN; ++fn) {
                     const int c = wn * FN * 16 + fn * 16 + (lane & 15);
                     const int n = n0 + c < p.N ? n0 + c : p.N - 1;
-                    *(bf16_t*)(smem + r * ROW + c * 2) = f2bf(g2_epi<EPI>(p.bias, acc[fm][fn][j], row0 + r, n, n1b, n2b));
+                    const uint32_t pk = f2bf2(g2_epi<EPI>(p.bias, acc[fm][fn][j], row0 + r, n, n1b, n2b),
+                                              g2_epi<EPI>(p.bias, acc[fm][fn][j + 1], row0 + r + 1, n, n1b, n2b));
+                    *(bf16_t*)(smem + r * ROW + c * 2) = (bf16_t)pk;
+                    *(bf16_t*)(smem + (r + 1) * ROW + c * 2) = (bf16_t)(pk >> 16);
                 }
             }
         __syncthreads();

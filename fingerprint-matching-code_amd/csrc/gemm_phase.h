@@ -218,14 +218,17 @@ __global__ __launch_bounds__(G2_THREADS, 1) void gemm_phase_kernel(GemmParams p)
 #pragma unroll
                 for (int fm = 0; fm < 4; ++fm)
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
+                    for (int j = 0; j < 4; j += 2) {     // rows j, j+1: one v_cvt_pk_bf16_f32
                         const int r = h * 128 + wr * 64 + fm * 16 + (lane >> 4) * 4 + j;
 #pragma unroll
                         for (int fn = 0; fn < 2; ++fn) {
                             const int c = g * 128 + wc * 32 + fn * 16 + (lane & 15);
                             const int n = n0 + c < p.N ? n0 + c : p.N - 1;
-                            *(bf16_t*)(smem + r * ROW + c * 2) =
-                                f2bf(g2_epi<EPI>(p.bias, acc[h][g][fm][fn][j], row0 + r, n, n1b, n2b));
+                            const uint32_t pk =
+                                f2bf2(g2_epi<EPI>(p.bias, acc[h][g][fm][fn][j], row0 + r, n, n1b, n2b),
+                                      g2_epi<EPI>(p.bias, acc[h][g][fm][fn][j + 1], row0 + r + 1, n, n1b, n2b));
+                            *(bf16_t*)(smem + r * ROW + c * 2) = (bf16_t)pk;
+                            *(bf16_t*)(smem + (r + 1) * ROW + c * 2) = (bf16_t)(pk >> 16);
                         }
                     }
         __syncthreads();
