@@ -774,15 +774,16 @@ def test_match_cls_bf16_vs_f32(sd):
 
 
 def test_gnn_kernel_variants_bit_identical(sd):
-    """GNN-layer launch variants (2 graph-2 nodes per workgroup, neighbour-load unroll) and combine
-    workgroup sizes give bit-identical forwards."""
+    """Launch variants give bit-identical forwards: combine workgroup sizes, the global plan kernels,
+    and the product GEMM on the 256 x 256 two-stage kernel (gemm_phase 0) instead of the phase
+    kernel."""
     pairs = synth.make_batch(17, 3, 64)
     net = fpm.Net(regression=True, backbone=False, dtype="bf16")
     net.load_state_dict(sd)
     bt = DeviceBatch.from_pairs(pairs, DEV)
     outs = []
     for key, val in (("combine_npb", 4), ("combine_npb", 16),
-                     ("plan_graph", 0)):
+                     ("plan_graph", 0), ("gemm_phase", 0)):
         prev = ops.set_tuning(key, val)
         try:
             r = net.run(bt, chunks=1)
