@@ -74,6 +74,31 @@ int& gemm_phase_flag() {
 }
 }  // namespace fpm
 
+// AFA-U encoder block tail (afau.py:188-199 + the max over positions): gmax[b][n] =
+// max_p InstanceNorm_p(res[b*P + p][n] + (A W^T)[b*P + p][n] + bias[n]) * nw[n] + nb[n], P = 256
+// positions per pair = one 256-row tile (EPI_NORM_MAX epilogue of gemm_big_kernel<128>).
+extern "C" int fpm_gemm_norm_max(const void* A, long lda, const void* B, long ldb, int M, int N, int K,
+                                 const float* bias, const float* res, long ldres, const float* nw, const float* nb,
+                                 float eps, int P, float* gmax, void* stream) {
+    using namespace fpm;
+    FPM_CHECK_ARG(P == G2_BM, "gemm_norm_max: P=%d must be %d (one tile per pair)", P, G2_BM);
+    FPM_CHECK_ARG(M >= 0 && M % P == 0 && N > 0 && K > 0 && K % G2_BK == 0, "gemm_norm_max: bad sizes M=%d N=%d K=%d",
+                  M, N, K);
+    FPM_CHECK_ARG(lda % 8 == 0 && ldb % 8 == 0 && ldres >= N, "gemm_norm_max: bad strides");
+    FPM_CHECK_ARG(res && nw && nb && gmax, "gemm_norm_max: null operand");
+    if (M == 0) return 0;
+    GemmParams p = {};
+    p.A = A; p.lda = lda; p.B = B; p.ldb = ldb;
+    p.M = M; p.N = N; p.K = K; p.nseg = 1;
+    p.epi = EPI_NORM_MAX; p.bias = bias; p.ldc = ldres;
+    p.res = res; p.nw = nw; p.nb = nb; p.eps = eps; p.gmax = gmax;
+    const int mt = M / G2_BM;
+    p.remap_mtiles = mt;
+    dim3 grid(remap_grid_big(N, 128, mt), 1, 1);
+    hipLaunchKernelGGL((gemm_big_kernel<128, EPI_NORM_MAX, true>), grid, dim3(G2_THREADS), 0, (hipStream_t)stream, p);
+    return fpm::check_launch("fpm_gemm_norm_max");
+}
+
 int& plan_graph_flag();
 int& combine_npb_flag();
 int& sinkhorn_bwd_reg_flag();

@@ -165,6 +165,100 @@ __global__ __launch_bounds__(G2_THREADS, 1) void gemm_big_kernel(GemmParams p) {
         __syncthreads();
     }
 
+    if constexpr (EPI == EPI_NORM_MAX) {
+        // AFA-U block tail (afau.py:188-199 InstanceNorm1d + the max over positions), fused: the
+        // 256-row tile is one pair's positions; per column c: v = res + (acc + bias), two-pass mean /
+        // variance over the 256 rows (lane column groups via shuffles, the 4 row waves via LDS),
+        // y = (v - mean) rstd w + b, gmax[pair][c] = max over rows.  Fixed reduction order.
+        static_assert(BN == 128, "norm-max epilogue: 256 x 128 tiles");
+        float* red = (float*)smem;                         // [WM][BN]; the K loop's LDS is free
+        const int pair = row0 / G2_BM;
+        float v[FM][FN][4];
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+            for (int fn = 0; fn < FN; ++fn) {
+                const int c = wn * FN * 16 + fn * 16 + (lane & 15);
+                const int n = n0 + c < p.N ? n0 + c : p.N - 1;
+                const float bv = p.bias ? p.bias[n] : 0.f;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int r = wm * FM * 16 + fm * 16 + (lane >> 4) * 4 + j;
+                    v[fm][fn][j] = p.res[(long)(row0 + r) * p.ldc + n] + (acc[fm][fn][j] + bv);
+                }
+            }
+        // column reduction over the tile's 256 rows: OP over this lane's rows, the lane groups,
+        // then the row waves
+        auto colred = [&](float (&t)[FN], bool is_max) {
+#pragma unroll
+            for (int fn = 0; fn < FN; ++fn) {
+                float x = t[fn];
+                const float y1 = __shfl_xor(x, 16);
+                x = is_max ? fmaxf(x, y1) : x + y1;
+                const float y2 = __shfl_xor(x, 32);
+                x = is_max ? fmaxf(x, y2) : x + y2;
+                if ((lane >> 4) == 0) red[wm * BN + wn * FN * 16 + fn * 16 + lane] = x;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int fn = 0; fn < FN; ++fn) {
+                const int c = wn * FN * 16 + fn * 16 + (lane & 15);
+                float x = red[c];
+#pragma unroll
+                for (int w = 1; w < Cfg::WM; ++w) x = is_max ? fmaxf(x, red[w * BN + c]) : x + red[w * BN + c];
+                t[fn] = x;
+            }
+            __syncthreads();
+        };
+        float mean[FN], var[FN];
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+            float s = 0.f;
+#pragma unroll
+            for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) s += v[fm][fn][j];
+            mean[fn] = s;
+        }
+        colred(mean, false);
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+            mean[fn] /= (float)G2_BM;
+            float s = 0.f;
+#pragma unroll
+            for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float d = v[fm][fn][j] - mean[fn];
+                    s += d * d;
+                }
+            var[fn] = s;
+        }
+        colred(var, false);
+        float mx[FN];
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+            const int c = wn * FN * 16 + fn * 16 + (lane & 15);
+            const int n = n0 + c < p.N ? n0 + c : p.N - 1;
+            const float rstd = 1.f / sqrtf(var[fn] / (float)G2_BM + p.eps);
+            const float ww = p.nw[n], bb = p.nb[n];
+            float m = -INFINITY;
+#pragma unroll
+            for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) m = fmaxf(m, (v[fm][fn][j] - mean[fn]) * rstd * ww + bb);
+            mx[fn] = m;
+        }
+        colred(mx, true);
+        if (wm == 0 && (lane >> 4) == 0) {
+#pragma unroll
+            for (int fn = 0; fn < FN; ++fn) {
+                const int c = wn * FN * 16 + fn * 16 + lane;
+                if (n0 + c < p.N) p.gmax[(long)pair * p.N + n0 + c] = mx[fn];
+            }
+        }
+        return;
+    }
     // epilogue through LDS
     int n1b = 0, n2b = 0;
     if (EPI == EPI_AFFINITY) { n1b = p.n1[batch]; n2b = p.n2[batch]; }

@@ -25,6 +25,8 @@ enum GemmEpi : int {
     EPI_TANH = 2,       // tanh(v + bias)
     EPI_AFFINITY = 3,   // C[j][i] = (j < n2b && i < n1b) ? softplus(v) - 0.5 : 0  (per pair)
     EPI_HALF_AFFINITY = 4,   // 0.5 * (softplus(v) - 0.5) on the same mask (quadratic Ke, ngm.py:289)
+    EPI_NORM_MAX = 5,   // AFA-U block tail (gemm_big<128> only, fpm_gemm_norm_max): per 256-row
+                        // tile = one pair, max_r InstanceNorm(res + v + bias) over the tile's rows
 };
 
 struct GemmParams {
@@ -45,6 +47,12 @@ struct GemmParams {
     const int* n1;
     const int* n2;
     int remap_mtiles;        // > 0: 1-D XCD-aware grid over remap_mtiles x ceil(N/128) tiles
+    // EPI_NORM_MAX: residual rows (ldc stride), norm weight / bias, eps, per-pair max output (B x N)
+    const float* res;
+    const float* nw;
+    const float* nb;
+    float eps;
+    float* gmax;
 };
 
 // 1-D grid for the XCD-aware tile order: padded to whole rounds of 8 chunks so the remap is a

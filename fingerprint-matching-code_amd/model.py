@@ -136,6 +136,8 @@ class Net(nn.Module):
         # pairs still run) instead of one blocking batch per chunk
         self.lsa_async = os.environ.get("FPM_LSA_ASYNC", "1") != "0"
         self._enqueue_lock = None      # set by fpm.parallel.ShardedNet (one lock for its replicas)
+        # FPM_AFAU_FUSE=0: the AFA-U block's FFN output through HBM + a separate instance norm (A/B)
+        self.afau_fuse_norm = os.environ.get("FPM_AFAU_FUSE", "1") != "0"
         # FPM_GRAPHS=1: multi-chunk inference forwards replay HIP graphs captured per (batch, chunk)
         # (host enqueue 8 -> 1 ms per 1024 pairs; the GPU stage measured 4 % slower than eager
         # launches, so off by default; fpm.parallel.ShardedNet turns it on); see run()
@@ -332,6 +334,12 @@ class Net(nn.Module):
             ops.gemm(o1t, wp[blk + "_W1"], rows, FF, KE, KE, KE, epi=ops.EPI_RELU, bias=wp[blk + "_b1"],
                      out_t=hbuf if op != torch.float32 else None, out_f=hbuf if op == torch.float32 else None,
                      ldc=FF)
+            if op != torch.float32 and P_ == 256 and self.afau_fuse_norm:
+                # the second GEMM's epilogue takes the instance norm + max over the pair's 256
+                # positions (one GEMM tile): the (rows x 600) FFN output never reaches HBM
+                gm = torch.empty(nb_, E, device=dev, dtype=torch.float32)
+                return ops.gemm_norm_max(hbuf, wp[blk + "_W2"], rows, E, FF, FF, FF, wp[blk + "_b2"], o1f,
+                                         wp[blk + "_n2w"], wp[blk + "_n2b"], gm)
             ops.gemm(hbuf, wp[blk + "_W2"], rows, E, FF, FF, FF, bias=wp[blk + "_b2"], out_f=ff, ldc=E)
         gm = torch.empty(nb_, E, device=dev, dtype=torch.float32)
         ops.instnorm(o1f, nb_, P_, E, wp[blk + "_n2w"], wp[blk + "_n2b"], in2=ff, gmax=gm)

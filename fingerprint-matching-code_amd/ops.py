@@ -331,6 +331,15 @@ def instnorm(in1, B, P, Cn, w, b, in2=None, nvalid=None, onehot_bias=None, out_f
               float(eps), _p(out_f), _p(out_t), int(ldt), _p(gmax), _stream(ref))
 
 
+def gemm_norm_max(A, Bw, M, N, K, lda, ldb, bias, res, nw, nb, gmax, P=256, eps=1e-5):
+    """AFA-U block tail fused (fpm_gemm_norm_max): gmax[b][n] = max over the pair's P rows of
+    InstanceNorm(res + A Bw^T + bias) * nw + nb; bf16 A / Bw, P = 256 rows per pair."""
+    _dev(A, Bw, res, gmax)
+    _lib.call("fpm_gemm_norm_max", _p(A), int(lda), _p(Bw), int(ldb), int(M), int(N), int(K), _p(bias), _p(res),
+              int(res.stride(0)), _p(nw), _p(nb), float(eps), int(P), _p(gmax), _stream(A))
+    return gmax
+
+
 def afau_head(gr, gc, B, E, r0w, r0b, r2w, r2b, c0w, c0b, c2w, c2b, ks):
     _lib.call("fpm_afau_head", _p(gr), _p(gc), B, E, _p(r0w), _p(r0b), _p(r2w), _p(r2b), _p(c0w), _p(c0b),
               _p(c2w), _p(c2b), _p(ks), _stream(gr))

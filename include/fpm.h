@@ -82,6 +82,13 @@ int fpm_gemm(int dtype, const void* A, long lda, long sA, const int* a_rows, con
              int N, int K, int batch, int epi, const float* bias, float* Cf, void* Ct, long ldc, long sC,
              const int* n1, const int* n2, void* stream);
 int fpm_cast_bf16(const float* x, void* y, long n, void* stream);
+/* AFA-U encoder block tail fused into the FFN's second GEMM (afau.py:188-199 InstanceNorm1d, then
+ * the max over positions taken by the caller, afau.py:231-300): per pair b (P = 256 rows, one GEMM
+ * tile) gmax[b][n] = max_p ((v - mean_p v) / sqrt(var_p v + eps) * nw[n] + nb[n]),
+ * v = res[b P + p][n] + (A B^T)[b P + p][n] + bias[n]; bf16 A (M x K, lda) and B (N x K, ldb). */
+int fpm_gemm_norm_max(const void* A, long lda, const void* B, long ldb, int M, int N, int K, const float* bias,
+                      const float* res, long ldres, const float* nw, const float* nb, float eps, int P, float* gmax,
+                      void* stream);
 /* Kernel-variant switches for A/B timing.  Returns the
  * previous value, or -1 (error channel set) for an unknown key.  No reference counterpart.
  *   "gemm_phase" (env FPM_GEMM_PHASE, default 1): 256x256 bf16 GEMM tiles on the phase-pipelined

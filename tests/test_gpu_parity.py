@@ -796,6 +796,48 @@ def test_gnn_kernel_variants_bit_identical(sd):
             assert torch.equal(r[k], outs[0][k]), k
 
 
+def test_afau_gemm_norm_max_fused():
+    """AFA-U block tail fused into the FFN's second GEMM (fpm_gemm_norm_max): equal to the GEMM +
+    separate instance norm + max (same GEMM accumulators; only the norm's reduction order differs)
+    and to a float64 torch statement of InstanceNorm1d + max over positions."""
+    g = torch.Generator().manual_seed(3)
+    nb, P, E, FF = 5, 256, 600, 256
+    rows = nb * P
+    A = torch.randn(rows, FF, generator=g).to(torch.bfloat16).to(DEV)
+    W = (torch.randn(E, FF, generator=g) * 0.06).to(torch.bfloat16).to(DEV)
+    bias = (torch.randn(E, generator=g) * 0.1).to(DEV)
+    res = torch.randn(rows, E, generator=g).to(DEV)
+    nw = (torch.rand(E, generator=g) + 0.5).to(DEV)
+    nbv = (torch.randn(E, generator=g) * 0.1).to(DEV)
+    gm = ops.gemm_norm_max(A, W, rows, E, FF, FF, FF, bias, res, nw, nbv, torch.empty(nb, E, device=DEV))
+    ff = torch.empty(rows, E, device=DEV)
+    ops.gemm(A, W, rows, E, FF, FF, FF, bias=bias, out_f=ff, ldc=E)
+    gm2 = torch.empty(nb, E, device=DEV)
+    ops.instnorm(res, nb, P, E, nw, nbv, in2=ff, gmax=gm2)
+    assert (gm - gm2).abs().max() < 2e-5
+    v = (res.double() + (A.double() @ W.double().t() + bias.double())).view(nb, P, E)
+    y = (v - v.mean(1, keepdim=True)) / torch.sqrt(v.var(1, unbiased=False, keepdim=True) + 1e-5)
+    ref = (y * nw.double() + nbv.double()).max(1).values
+    assert (gm.double() - ref).abs().max() < 1e-4
+    with pytest.raises(fpm._lib.FpmError):
+        ops.gemm_norm_max(A[:100], W, 100, E, FF, FF, FF, bias, res[:100], nw, nbv, gm)
+
+
+def test_afau_fused_forward_matches_unfused(sd):
+    """Whole bf16 forwards with the fused AFA-U tail agree with the unfused path (k_prob within
+    2e-6, identical perm_mat) on a 256-keypoint batch."""
+    pairs = synth.make_batch(41, 4, 256)
+    bt = DeviceBatch.from_pairs(pairs, DEV)
+    res = {}
+    for fuse in (False, True):
+        net = fpm.Net(regression=True, backbone=False, dtype="bf16", chunks=1)
+        net.load_state_dict(sd)
+        net.afau_fuse_norm = fuse
+        res[fuse] = net.run(bt)
+    assert (res[True]["k_prob"] - res[False]["k_prob"]).abs().max() < 2e-6
+    assert torch.equal(res[True]["ss"], res[False]["ss"])
+
+
 def test_global_weights_kernel():
     """normalize_over_channels(cat(w1, w2)) (ngm.py:65-67, 262-268): within 1e-6 of the oracle, and a
     pair's row does not depend on how many pairs share the launch (shards / chunks computed alone)."""
