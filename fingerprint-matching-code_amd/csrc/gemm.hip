@@ -99,6 +99,33 @@ extern "C" int fpm_gemm_norm_max(const void* A, long lda, const void* B, long ld
     return fpm::check_launch("fpm_gemm_norm_max");
 }
 
+// AFA-U encoder block head (afau.py:188-199 first InstanceNorm1d on the attention-combine output):
+// out_f = InstanceNorm_p((A W^T)[b*P + p] + bias) * nw + nb over each pair's P = 256 rows (one GEMM
+// tile, EPI_NORM_OUT epilogue), out_t (optional) its bf16 copy with row stride ldt and zero columns
+// [N, ldt) -- the combine output never reaches HBM un-normalised.
+extern "C" int fpm_gemm_norm_out(const void* A, long lda, const void* B, long ldb, int M, int N, int K,
+                                 const float* bias, const float* nw, const float* nb, float eps, int P, float* out_f,
+                                 long ldc, void* out_t, long ldt, void* stream) {
+    using namespace fpm;
+    FPM_CHECK_ARG(P == G2_BM, "gemm_norm_out: P=%d must be %d (one tile per pair)", P, G2_BM);
+    FPM_CHECK_ARG(M >= 0 && M % P == 0 && N > 0 && N % 4 == 0 && K > 0 && K % G2_BK == 0,
+                  "gemm_norm_out: bad sizes M=%d N=%d K=%d", M, N, K);
+    FPM_CHECK_ARG(lda % 8 == 0 && ldb % 8 == 0 && ldc >= N && ldc % 4 == 0 && (!out_t || (ldt >= N && ldt % 4 == 0 &&
+                  ldt <= ((N + 127) / 128) * 128)), "gemm_norm_out: bad strides");
+    FPM_CHECK_ARG(nw && nb && out_f, "gemm_norm_out: null operand");
+    if (M == 0) return 0;
+    GemmParams p = {};
+    p.A = A; p.lda = lda; p.B = B; p.ldb = ldb;
+    p.M = M; p.N = N; p.K = K; p.nseg = 1;
+    p.epi = EPI_NORM_OUT; p.bias = bias; p.Cf = out_f; p.ldc = ldc; p.Ct = out_t; p.ldt = ldt;
+    p.nw = nw; p.nb = nb; p.eps = eps;
+    const int mt = M / G2_BM;
+    p.remap_mtiles = mt;
+    dim3 grid(remap_grid_big(N, 128, mt), 1, 1);
+    hipLaunchKernelGGL((gemm_big_kernel<128, EPI_NORM_OUT, true>), grid, dim3(G2_THREADS), 0, (hipStream_t)stream, p);
+    return fpm::check_launch("fpm_gemm_norm_out");
+}
+
 int& plan_graph_flag();
 int& combine_npb_flag();
 int& sinkhorn_bwd_reg_flag();

@@ -56,6 +56,7 @@ typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
 // variant so the unrolled 128-element epilogue stays small)
 template <int EPI>
 __device__ __forceinline__ float g2_epi(const float* __restrict__ bias, float v, int r, int n, int n1b, int n2b) {
+    if (EPI == EPI_NORM_OUT) return v;        // bias and norm already applied to the accumulators
     if (bias) v += bias[n];
     if (EPI == EPI_RELU) return fmaxf(v, 0.f);
     if (EPI == EPI_AFFINITY) return (r < n2b && n < n1b) ? softplus_f(v) - 0.5f : 0.f;
@@ -165,12 +166,13 @@ __global__ __launch_bounds__(G2_THREADS, 1) void gemm_big_kernel(GemmParams p) {
         __syncthreads();
     }
 
-    if constexpr (EPI == EPI_NORM_MAX) {
-        // AFA-U block tail (afau.py:188-199 InstanceNorm1d + the max over positions), fused: the
-        // 256-row tile is one pair's positions; per column c: v = res + (acc + bias), two-pass mean /
-        // variance over the 256 rows (lane column groups via shuffles, the 4 row waves via LDS),
-        // y = (v - mean) rstd w + b, gmax[pair][c] = max over rows.  Fixed reduction order.
-        static_assert(BN == 128, "norm-max epilogue: 256 x 128 tiles");
+    if constexpr (EPI == EPI_NORM_MAX || EPI == EPI_NORM_OUT) {
+        // AFA-U instance norms (afau.py:188-199 InstanceNorm1d) over a pair's 256 positions = one
+        // 256-row tile, per column c: v = (res +) acc + bias, two-pass mean / variance over the rows
+        // (lane column groups via shuffles, the 4 row waves via LDS), y = (v - mean) rstd w + b.
+        // NORM_MAX: gmax[pair][c] = max over rows (the block tail); NORM_OUT: y to Cf / Ct through
+        // the fp32 store path below (the block head).  Fixed reduction order.
+        static_assert(BN == 128 && F32OUT, "norm epilogues: 256 x 128 fp32 tiles");
         float* red = (float*)smem;                         // [WM][BN]; the K loop's LDS is free
         const int pair = row0 / G2_BM;
         float v[FM][FN][4];
@@ -184,7 +186,8 @@ __global__ __launch_bounds__(G2_THREADS, 1) void gemm_big_kernel(GemmParams p) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int r = wm * FM * 16 + fm * 16 + (lane >> 4) * 4 + j;
-                    v[fm][fn][j] = p.res[(long)(row0 + r) * p.ldc + n] + (acc[fm][fn][j] + bv);
+                    v[fm][fn][j] = EPI == EPI_NORM_MAX ? p.res[(long)(row0 + r) * p.ldc + n] + (acc[fm][fn][j] + bv)
+                                                       : acc[fm][fn][j] + bv;
                 }
             }
         // column reduction over the tile's 256 rows: OP over this lane's rows, the lane groups,
@@ -235,29 +238,43 @@ __global__ __launch_bounds__(G2_THREADS, 1) void gemm_big_kernel(GemmParams p) {
             var[fn] = s;
         }
         colred(var, false);
-        float mx[FN];
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn) {
-            const int c = wn * FN * 16 + fn * 16 + (lane & 15);
-            const int n = n0 + c < p.N ? n0 + c : p.N - 1;
-            const float rstd = 1.f / sqrtf(var[fn] / (float)G2_BM + p.eps);
-            const float ww = p.nw[n], bb = p.nb[n];
-            float m = -INFINITY;
-#pragma unroll
-            for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) m = fmaxf(m, (v[fm][fn][j] - mean[fn]) * rstd * ww + bb);
-            mx[fn] = m;
-        }
-        colred(mx, true);
-        if (wm == 0 && (lane >> 4) == 0) {
+        if constexpr (EPI == EPI_NORM_MAX) {
+            float mx[FN];
 #pragma unroll
             for (int fn = 0; fn < FN; ++fn) {
-                const int c = wn * FN * 16 + fn * 16 + lane;
-                if (n0 + c < p.N) p.gmax[(long)pair * p.N + n0 + c] = mx[fn];
+                const int c = wn * FN * 16 + fn * 16 + (lane & 15);
+                const int n = n0 + c < p.N ? n0 + c : p.N - 1;
+                const float rstd = 1.f / sqrtf(var[fn] / (float)G2_BM + p.eps);
+                const float ww = p.nw[n], bb = p.nb[n];
+                float m = -INFINITY;
+#pragma unroll
+                for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) m = fmaxf(m, (v[fm][fn][j] - mean[fn]) * rstd * ww + bb);
+                mx[fn] = m;
+            }
+            colred(mx, true);
+            if (wm == 0 && (lane >> 4) == 0) {
+#pragma unroll
+                for (int fn = 0; fn < FN; ++fn) {
+                    const int c = wn * FN * 16 + fn * 16 + lane;
+                    if (n0 + c < p.N) p.gmax[(long)pair * p.N + n0 + c] = mx[fn];
+                }
+            }
+            return;
+        } else {
+#pragma unroll
+            for (int fn = 0; fn < FN; ++fn) {
+                const int c = wn * FN * 16 + fn * 16 + (lane & 15);
+                const int n = n0 + c < p.N ? n0 + c : p.N - 1;
+                const float rstd = 1.f / sqrtf(var[fn] / (float)G2_BM + p.eps);
+                const float ww = p.nw[n], bb = p.nb[n];
+#pragma unroll
+                for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc[fm][fn][j] = (v[fm][fn][j] - mean[fn]) * rstd * ww + bb;
             }
         }
-        return;
     }
     // epilogue through LDS
     int n1b = 0, n2b = 0;
@@ -325,6 +342,14 @@ __global__ __launch_bounds__(G2_THREADS, 1) void gemm_big_kernel(GemmParams p) {
                 if (gr < row_end && n0 + ch * 4 < p.N) {
                     uint4 v = *(const uint4*)(smem + r * ROW + ch * 16);
                     *(uint4*)(Cf + (long)gr * p.ldc + n0 + ch * 4) = v;
+                    if (EPI == EPI_NORM_OUT && p.Ct) {          // the bf16 operand copy
+                        uint2 o;
+                        o.x = f2bf2(__uint_as_float(v.x), __uint_as_float(v.y));
+                        o.y = f2bf2(__uint_as_float(v.z), __uint_as_float(v.w));
+                        *(uint2*)((bf16_t*)p.Ct + (long)gr * p.ldt + n0 + ch * 4) = o;
+                    }
+                } else if (EPI == EPI_NORM_OUT && p.Ct && gr < row_end && n0 + ch * 4 < p.ldt) {
+                    *(uint2*)((bf16_t*)p.Ct + (long)gr * p.ldt + n0 + ch * 4) = make_uint2(0u, 0u);   // K padding
                 }
             }
             __syncthreads();

@@ -27,6 +27,8 @@ enum GemmEpi : int {
     EPI_HALF_AFFINITY = 4,   // 0.5 * (softplus(v) - 0.5) on the same mask (quadratic Ke, ngm.py:289)
     EPI_NORM_MAX = 5,   // AFA-U block tail (gemm_big<128> only, fpm_gemm_norm_max): per 256-row
                         // tile = one pair, max_r InstanceNorm(res + v + bias) over the tile's rows
+    EPI_NORM_OUT = 6,   // AFA-U block head (gemm_big<128> only, fpm_gemm_norm_out): InstanceNorm(v +
+                        // bias) over each 256-row tile, to Cf (fp32) and Ct (bf16, ldt, zero K-pad)
 };
 
 struct GemmParams {
@@ -53,6 +55,7 @@ struct GemmParams {
     const float* nb;
     float eps;
     float* gmax;
+    long ldt;                // EPI_NORM_OUT: row stride of the bf16 copy Ct
 };
 
 // 1-D grid for the XCD-aware tile order: padded to whole rounds of 8 chunks so the remap is a

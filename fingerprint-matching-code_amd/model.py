@@ -302,22 +302,29 @@ class Net(nn.Module):
         ops.rows_bcast_scale(y, bt.B, coef=cscale, out_f=outf, out_t=out)
         return out, outf
 
-    def _afau_block(self, wp, blk, nb_, P_, mh=None, n2u_d=None):
+    def _afau_norm1_bufs(self, rows, dev):
+        """The block's first-norm outputs: fp32 rows and (bf16 modes) the zero-K-padded operand copy."""
+        op = torch.bfloat16 if self.afau_mode in ("bf16", "bf16s") else torch.float32
+        o1f = torch.empty(rows, C.AFAU_EMB, device=dev, dtype=torch.float32)
+        o1t = o1f if op == torch.float32 else torch.empty(rows, C.AFAU_EMB_PAD, device=dev, dtype=op)
+        return o1f, o1t
+
+    def _afau_block(self, wp, blk, nb_, P_, mh=None, n2u_d=None, pre=None):
         """One AFA-U encoder block's instance norms + FFN (afau.py:145-199) -> max over positions
         (nb_, E).  "row": on the attention-combine output mh; "col": the synthesised one-hot input
-        C0 + combine bias of each distinct n2 (n2u_d)."""
+        C0 + combine bias of each distinct n2 (n2u_d).  ``pre``: the first norm's (o1f, o1t) when the
+        combine GEMM's epilogue already produced them (fpm_gemm_norm_out)."""
         dev = wp["row_Wc"].device
         op = torch.bfloat16 if self.afau_mode in ("bf16", "bf16s") else torch.float32
         E, FF = C.AFAU_EMB, C.AFAU_FF
         x3 = self.afau_mode == "bf16x3"
         rows = nb_ * P_
-        o1f = torch.empty(rows, E, device=dev, dtype=torch.float32)
         KE = E if op == torch.float32 else C.AFAU_EMB_PAD      # bf16 operand copy: zero-padded K
-        o1t = o1f if op == torch.float32 else torch.empty(rows, KE, device=dev, dtype=op)
-        if blk == "row":
+        o1f, o1t = pre if pre is not None else self._afau_norm1_bufs(rows, dev)
+        if pre is None and blk == "row":
             ops.instnorm(mh, nb_, P_, E, wp["row_n1w"], wp["row_n1b"], out_f=o1f,
                          out_t=None if op == torch.float32 else o1t, ldt=KE)
-        else:
+        elif pre is None:
             ops.instnorm(None, nb_, P_, E, wp["col_n1w"], wp["col_n1b"], nvalid=n2u_d, onehot_bias=wp["col_bc"],
                          out_f=o1f, out_t=None if op == torch.float32 else o1t, ldt=KE)
         ff = torch.empty(rows, E, device=dev, dtype=torch.float32)
@@ -383,13 +390,22 @@ class Net(nn.Module):
                           dtype=torch.bfloat16 if split else op)
         ops.crossset_attn(ss, bt.n2, wp["row_Wv"], wp["row_mix1w"], wp["row_mix1b"], wp["row_mix2w"],
                           wp["row_mix2b"], att, split=split)
-        mh = torch.empty(B * n1max, E, device=dev, dtype=torch.float32)
         if x3:
             att = ops.split_bf16x3(att, HD)
         # bf16s: hi*W_hi + lo*W_hi (2 terms; the W_lo term changed nothing measurable, +0.7 % time)
         kc = 2 * HD if split else (3 * HD if x3 else HD)
-        ops.gemm(att, wp["row_Wc"], B * n1max, E, kc, att.shape[1], att.shape[1], bias=wp["row_bc"], out_f=mh, ldc=E)
-        g_row = self._afau_block(wp, "row", B, n1max, mh=mh)
+        if att.dtype == torch.bfloat16 and n1max == 256 and self.afau_fuse_norm:
+            # the combine projection's epilogue applies the block's first instance norm (one GEMM
+            # tile = one pair's 256 positions): mh never reaches HBM un-normalised
+            o1f, o1t = self._afau_norm1_bufs(B * n1max, dev)
+            ops.gemm_norm_out(att, wp["row_Wc"], B * n1max, E, kc, att.shape[1], att.shape[1], wp["row_bc"],
+                              wp["row_n1w"], wp["row_n1b"], o1f, out_t=None if o1t is o1f else o1t)
+            g_row = self._afau_block(wp, "row", B, n1max, pre=(o1f, o1t))
+        else:
+            mh = torch.empty(B * n1max, E, device=dev, dtype=torch.float32)
+            ops.gemm(att, wp["row_Wc"], B * n1max, E, kc, att.shape[1], att.shape[1], bias=wp["row_bc"], out_f=mh,
+                     ldc=E)
+            g_row = self._afau_block(wp, "row", B, n1max, mh=mh)
         if col is None or col[2] != n2max:
             col, b0 = self._afau_col(wp, bt), 0
         n2u, gm_u, _, inv = col

@@ -340,6 +340,16 @@ def gemm_norm_max(A, Bw, M, N, K, lda, ldb, bias, res, nw, nb, gmax, P=256, eps=
     return gmax
 
 
+def gemm_norm_out(A, Bw, M, N, K, lda, ldb, bias, nw, nb, out_f, out_t=None, ldt=0, P=256, eps=1e-5):
+    """AFA-U block head fused (fpm_gemm_norm_out): out_f = InstanceNorm over each pair's P rows of
+    (A Bw^T + bias) * nw + nb, out_t its bf16 copy (row stride ldt, zero columns [N, ldt))."""
+    _dev(A, Bw, out_f)
+    _lib.call("fpm_gemm_norm_out", _p(A), int(lda), _p(Bw), int(ldb), int(M), int(N), int(K), _p(bias), _p(nw),
+              _p(nb), float(eps), int(P), _p(out_f), int(out_f.stride(0)), _p(out_t),
+              int(ldt or (out_t.stride(0) if out_t is not None else 0)), _stream(A))
+    return out_f
+
+
 def afau_head(gr, gc, B, E, r0w, r0b, r2w, r2b, c0w, c0b, c2w, c2b, ks):
     _lib.call("fpm_afau_head", _p(gr), _p(gc), B, E, _p(r0w), _p(r0b), _p(r2w), _p(r2b), _p(c0w), _p(c0b),
               _p(c2w), _p(c2b), _p(ks), _stream(gr))

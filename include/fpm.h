@@ -89,6 +89,13 @@ int fpm_cast_bf16(const float* x, void* y, long n, void* stream);
 int fpm_gemm_norm_max(const void* A, long lda, const void* B, long ldb, int M, int N, int K, const float* bias,
                       const float* res, long ldres, const float* nw, const float* nb, float eps, int P, float* gmax,
                       void* stream);
+/* AFA-U encoder block head (afau.py:188-199, the first InstanceNorm1d on the attention-combine
+ * projection afau.py:231-300): out_f[b P + p][n] = ((v - mean_p v) / sqrt(var_p v + eps)) * nw[n] +
+ * nb[n], v = (A B^T)[b P + p][n] + bias[n], P = 256 rows per pair (one GEMM tile); out_t (optional)
+ * its bf16 copy, row stride ldt, columns [N, ldt) written as zeros (the next GEMM's K padding). */
+int fpm_gemm_norm_out(const void* A, long lda, const void* B, long ldb, int M, int N, int K, const float* bias,
+                      const float* nw, const float* nb, float eps, int P, float* out_f, long ldc, void* out_t, long ldt,
+                      void* stream);
 /* Kernel-variant switches for A/B timing.  Returns the
  * previous value, or -1 (error channel set) for an unknown key.  No reference counterpart.
  *   "gemm_phase" (env FPM_GEMM_PHASE, default 1): 256x256 bf16 GEMM tiles on the phase-pipelined

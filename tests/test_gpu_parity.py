@@ -375,7 +375,9 @@ def _record(name, d):
 
 # bf16 mode vs the fp32 oracle: the largest deviations measured on the box by the fidelity tests
 # (round 2: n = 128 / 256 / 512 -> gpurun_out/bf16_fidelity_*.json) and the bench's 8-pair C3 sample
-BF16_MEASURED = {"Kp": 1.3e-5, "ss": 1.3e-6, "ds_mat": 3.6e-6, "k_prob": 8.7e-4, "cls_prob": 2.7e-5}
+BF16_MEASURED = {"Kp": 1.4e-5, "ss": 1.4e-6, "ds_mat": 4.5e-6, "k_prob": 8.7e-4, "cls_prob": 2.7e-5}
+# (round-3 final tree: largest values over the C2 / C3 / C3-16 / C4 / C5 fidelity records and the bench
+# sample -- Kp 1.36e-5, ss 1.40e-6, ds_mat 4.44e-6 (C4), k_prob 7.7e-4 (bench), cls_prob 2.7e-5)
 
 
 def _bf16_gate(d):
@@ -823,9 +825,41 @@ def test_afau_gemm_norm_max_fused():
         ops.gemm_norm_max(A[:100], W, 100, E, FF, FF, FF, bias, res[:100], nw, nbv, gm)
 
 
+def test_afau_gemm_norm_out_fused():
+    """AFA-U block head fused into the attention-combine GEMM (fpm_gemm_norm_out): fp32 rows and the
+    zero-K-padded bf16 copy equal to the GEMM + separate instance norm within reduction-order
+    rounding, and to a float64 statement of InstanceNorm1d."""
+    g = torch.Generator().manual_seed(4)
+    nb, P, E, K, KE = 3, 256, 600, 512, 640
+    rows = nb * P
+    A = torch.randn(rows, K, generator=g).to(torch.bfloat16).to(DEV)
+    W = (torch.randn(E, K, generator=g) * 0.05).to(torch.bfloat16).to(DEV)
+    bias = (torch.randn(E, generator=g) * 0.1).to(DEV)
+    nw = (torch.rand(E, generator=g) + 0.5).to(DEV)
+    nbv = (torch.randn(E, generator=g) * 0.1).to(DEV)
+    o1f = torch.empty(rows, E, device=DEV)
+    o1t = torch.full((rows, KE), 7.0, device=DEV).to(torch.bfloat16)
+    ops.gemm_norm_out(A, W, rows, E, K, K, K, bias, nw, nbv, o1f, out_t=o1t)
+    mh = torch.empty(rows, E, device=DEV)
+    ops.gemm(A, W, rows, E, K, K, K, bias=bias, out_f=mh, ldc=E)
+    r_f = torch.empty(rows, E, device=DEV)
+    r_t = torch.empty(rows, KE, device=DEV).to(torch.bfloat16)
+    ops.instnorm(mh, nb, P, E, nw, nbv, out_f=r_f, out_t=r_t, ldt=KE)
+    assert (o1f - r_f).abs().max() < 2e-5
+    assert (o1t.float() - r_t.float()).abs().max() <= 2 ** -6 * (r_f.abs().max() + 1)   # one bf16 ulp
+    assert (o1t[:, E:] == 0).all()
+    v = (A.double() @ W.double().t() + bias.double()).view(nb, P, E)
+    y = (v - v.mean(1, keepdim=True)) / torch.sqrt(v.var(1, unbiased=False, keepdim=True) + 1e-5)
+    ref = (y * nw.double() + nbv.double()).view(rows, E)
+    assert (o1f.double() - ref).abs().max() < 1e-4
+
+
 def test_afau_fused_forward_matches_unfused(sd):
-    """Whole bf16 forwards with the fused AFA-U tail agree with the unfused path (k_prob within
-    2e-6, identical perm_mat) on a 256-keypoint batch."""
+    """Whole bf16 forwards with the fused AFA-U block head and tail agree with the unfused path on
+    a 256-keypoint batch: ss identical (computed before AFA-U); k_prob within 2e-4 -- the fused
+    first norm sums in another order, which can move a bf16 rounding of its operand copy by one
+    ulp (the bf16 mode's own k_prob distance from the fp32 oracle is ~6e-4); the fp32 mode is not
+    fused."""
     pairs = synth.make_batch(41, 4, 256)
     bt = DeviceBatch.from_pairs(pairs, DEV)
     res = {}
@@ -834,7 +868,7 @@ def test_afau_fused_forward_matches_unfused(sd):
         net.load_state_dict(sd)
         net.afau_fuse_norm = fuse
         res[fuse] = net.run(bt)
-    assert (res[True]["k_prob"] - res[False]["k_prob"]).abs().max() < 2e-6
+    assert (res[True]["k_prob"] - res[False]["k_prob"]).abs().max() < 2e-4
     assert torch.equal(res[True]["ss"], res[False]["ss"])
 
 
