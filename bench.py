@@ -250,6 +250,11 @@ def main():
         sys.exit(subprocess.call(cmd))
     if world != args.gpus:
         raise SystemExit("bench: WORLD_SIZE=%d but --gpus=%d" % (world, args.gpus))
+    # stdout carries exactly one JSON line: anything native code writes to fd 1 (gloo prints
+    # "[Gloo] Rank r is connected to ..." from every rank at rendezvous) goes to stderr instead
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
 
     # inputs first (forked workers must not inherit a GPU context)
     t_gen = time.perf_counter()
@@ -488,7 +493,7 @@ def main():
             "input_gen_s": t_gen,
             "graph_build": graph_build,
         }
-        print(json.dumps(res))
+        print(json.dumps(res), file=json_out, flush=True)
     if world > 1:
         dist.destroy_process_group()
 
