@@ -437,62 +437,102 @@ extern "C" int fpm_soft_topk_bwd(const float* ss, long sb, long ld, const int* n
 // out[o][c] = sum_{b, p} U[b][o][p] V[b][c][p] (and, with ones, out[o][C] = sum U[b][o][p]):
 // the (O x K)(K x C) products with K = B * N (millions of positions) and O, C <= 17.  One
 // workgroup per (pair, slice of <= 4096 positions) stages 256-position tiles of U and V in LDS
-// (rows padded to 257 floats: conflict-free column reads) and thread q = o * (C + ones) + c keeps
-// one accumulator; per-workgroup partials part[b * S + s][q] are summed in order by fpm_rows_sum.
+// (one global read of each value) and runs the product on f32 MFMA (v_mfma_f32_16x16x4_f32: exact
+// f32, a fixed fmaf chain per output): wave w takes positions [64 w, 64 w + 64) of each tile, the
+// output is 2 x 2 tiles of 16 x 16 (only those inside O x C1 run), the ones column is B = 1.  The
+// earlier one-output-per-thread VALU form read two LDS floats per FMA and was LDS-bound at ~2x
+// the HBM time.  The four waves' tiles are summed in order through LDS; per-workgroup partials
+// part[b * S + s][q] are summed in order by fpm_rows_sum.
 namespace {
-constexpr int OS_T = 256, OS_L = 4096, OS_MAXC = 17;
-// rows padded to OS_T + 4 floats: 16-B aligned float4 reads (4 FMAs per two ds_read_b128) into four
-// independent accumulators (the single fmaf chain per thread was latency-bound)
-constexpr int OS_LD = OS_T + 4;
-__global__ __launch_bounds__(512) void outer_sum_kernel(const float* __restrict__ U, long sUb, long sUo, int O,
-                                                        const float* __restrict__ V, long sVb, long sVc, int Cc,
-                                                        int ones, long N, int S, float* __restrict__ part) {
-    __shared__ __attribute__((aligned(16))) float Ut[OS_MAXC][OS_LD];
-    __shared__ __attribute__((aligned(16))) float Vt[OS_MAXC][OS_LD];
+constexpr int OS_T = 256, OS_L = 4096, OS_MAXC = 17, OS_LD = OS_T + 4, OS_THREADS = 256;
+typedef float os_f32x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(OS_THREADS) void outer_sum_kernel(const float* __restrict__ U, long sUb, long sUo, int O,
+                                                               const float* __restrict__ V, long sVb, long sVc, int Cc,
+                                                               int ones, long N, int S, float* __restrict__ part) {
+    // rows padded to 260 floats: the MFMA operand reads (row l & 15, position l >> 4) hit 64 banks
+    __shared__ __attribute__((aligned(16))) float sm[2 * OS_MAXC * OS_LD];
+    float (*Ut)[OS_LD] = (float (*)[OS_LD])sm;
+    float (*Vt)[OS_LD] = (float (*)[OS_LD])(sm + OS_MAXC * OS_LD);
     const int b = blockIdx.x / S, s = blockIdx.x % S, t = threadIdx.x;
+    const int lane = t & 63, wave = t >> 6;
     const int C1 = Cc + ones, nq = O * C1;
-    const int o = t / C1, c = t - o * C1;
+    const int i0 = lane & 15, kq = lane >> 4;
+    const bool two_o = O > 16, two_c = C1 > 16;
+    // operand rows of this lane (clamped; out-of-range rows read as 0, the ones column as 1)
+    const int ra0 = min(i0, O - 1), ra1 = min(16 + i0, O - 1);
+    const bool va0 = i0 < O, va1 = 16 + i0 < O;
+    const int rb0 = min(i0, max(Cc - 1, 0)), rb1 = min(16 + i0, max(Cc - 1, 0));
+    const float cb0 = i0 < Cc ? -1.f : (i0 < C1 ? 1.f : 0.f);            // -1: read V
+    const float cb1 = 16 + i0 < Cc ? -1.f : (16 + i0 < C1 ? 1.f : 0.f);
+    const float* Ub = U + (long)b * sUb;
     const long p0 = (long)s * OS_L, p1 = min(N, p0 + OS_L);
-    float acc = 0.f;
-    float4 a4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (long q0 = p0; q0 < p1; q0 += OS_T) {
-        const int len = (int)min((long)OS_T, p1 - q0);
-        for (int k = t; k < O * OS_T; k += 512) {
-            const int r = k / OS_T, p = k - r * OS_T;
-            Ut[r][p] = p < len ? U[b * sUb + r * sUo + q0 + p] : 0.f;
+    os_f32x4 acc[2][2];
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) acc[x][y] = os_f32x4{0.f, 0.f, 0.f, 0.f};
+    // thread t stages position t of every row; the next tile's values are loaded into registers
+    // before the current tile's MFMAs, so each workgroup keeps one tile of loads in flight
+    const float* Us = Ub + p0;                            // slice bases: 32-bit lane offsets below
+    const float* Vs = V + (long)b * sVb + p0;
+    const int slen = (int)(p1 - p0);
+    float pu[OS_MAXC], pv[OS_MAXC];
+    auto load_regs = [&](int q) {
+        const int e = q + t;
+        const bool in = e < slen;
+#pragma unroll
+        for (int r = 0; r < OS_MAXC; ++r) {
+            pu[r] = (r < O && in) ? (Us + r * sUo)[e] : 0.f;
+            pv[r] = (r < Cc && in) ? (Vs + r * sVc)[e] : 0.f;
         }
-        for (int k = t; k < Cc * OS_T; k += 512) {
-            const int r = k / OS_T, p = k - r * OS_T;
-            Vt[r][p] = p < len ? V[b * sVb + r * sVc + q0 + p] : 0.f;
+    };
+    load_regs(0);
+    for (long q0 = p0; q0 < p1; q0 += OS_T) {
+        __syncthreads();                                  // previous tile read
+#pragma unroll
+        for (int r = 0; r < OS_MAXC; ++r) {
+            if (r < O) Ut[r][t] = pu[r];
+            if (r < Cc) Vt[r][t] = pv[r];
         }
         __syncthreads();
-        if (t < nq) {
-            const float4* u4 = (const float4*)&Ut[o][0];
-            if (c < Cc) {
-                const float4* v4 = (const float4*)&Vt[c][0];
+        if (q0 + OS_T < p1) load_regs((int)(q0 - p0) + OS_T);
 #pragma unroll 4
-                for (int p = 0; p < OS_T / 4; ++p) {
-                    const float4 x = u4[p], y = v4[p];
-                    a4.x = fmaf(x.x, y.x, a4.x);
-                    a4.y = fmaf(x.y, y.y, a4.y);
-                    a4.z = fmaf(x.z, y.z, a4.z);
-                    a4.w = fmaf(x.w, y.w, a4.w);
-                }
-            } else {
-#pragma unroll 4
-                for (int p = 0; p < OS_T / 4; ++p) {
-                    const float4 x = u4[p];
-                    a4.x += x.x;
-                    a4.y += x.y;
-                    a4.z += x.z;
-                    a4.w += x.w;
-                }
+        for (int kk = 0; kk < 16; ++kk) {
+            const int p = wave * 64 + kk * 4 + kq;
+            const float a0 = va0 ? Ut[ra0][p] : 0.f;
+            const float b0 = cb0 < 0.f ? Vt[rb0][p] : cb0;
+            acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
+            float b1 = 0.f;
+            if (two_c) {
+                b1 = cb1 < 0.f ? Vt[rb1][p] : cb1;
+                acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
+            }
+            if (two_o) {
+                const float a1 = va1 ? Ut[ra1][p] : 0.f;
+                acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
+                if (two_c) acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
             }
         }
-        __syncthreads();
     }
-    acc = (a4.x + a4.y) + (a4.z + a4.w);
-    if (t < nq) part[(long)blockIdx.x * nq + t] = acc;
+    // red[w][(x * 2 + y) * 4 + r][lane] = wave w's C tile (x, y), element row 4 (lane >> 4) + r,
+    // column lane & 15; the four waves are added in order
+    __syncthreads();
+    float* red = sm;                                      // 4 x 16 x 64 floats (16 KB) over the staging rows
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) red[(wave * 16 + (x * 2 + y) * 4 + r) * 64 + lane] = acc[x][y][r];
+    __syncthreads();
+    for (int q = t; q < nq; q += OS_THREADS) {
+        const int o = q / C1, c = q - o * C1;
+        const int slot = ((o >> 4) * 2 + (c >> 4)) * 4 + (o & 3), ln = ((o & 15) >> 2) * 16 + (c & 15);
+        float v = red[slot * 64 + ln];
+#pragma unroll
+        for (int w = 1; w < 4; ++w) v += red[(w * 16 + slot) * 64 + ln];
+        part[(long)blockIdx.x * nq + q] = v;
+    }
 }
 }  // namespace
 
@@ -504,7 +544,7 @@ extern "C" int fpm_outer_sum(const float* U, long sUb, long sUo, int O, const fl
                   "outer_sum: 0 < O, C <= 17 required");
     if (B == 0) return 0;
     const int S = (int)((N + OS_L - 1) / OS_L);
-    hipLaunchKernelGGL(outer_sum_kernel, dim3((unsigned)(B * S)), dim3(512), 0, (hipStream_t)stream, U, sUb, sUo, O, V,
+    hipLaunchKernelGGL(outer_sum_kernel, dim3((unsigned)(B * S)), dim3(OS_THREADS), 0, (hipStream_t)stream, U, sUb, sUo, O, V,
                        sVb, sVc, Cc, ones != 0, N, S, part);
     return fpm::check_launch("fpm_outer_sum");
 }
