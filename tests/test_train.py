@@ -511,3 +511,27 @@ def test_train_second_net_uses_its_own_weights():
             ref = O.forward(pairs, sdx, regression=True, training=True, gt_perm=gt, labels=torch.ones(2))
             assert (net.last_outputs["ss"].detach().cpu() - ref["ss"].detach()).abs().max() < 1e-4, (seed, step)
         del net
+
+
+@pytest.mark.gpu
+def test_rows_sum_vector_path_bitwise():
+    """fpm_rows_sum's 16-B path (K % 4 == 0, aligned rows) gives the same bits as its scalar path (a
+    view shifted by one float), with and without keys, and equals the in-order float32 sum."""
+    from fpm.afau_grad import rows_sum
+    g = torch.Generator().manual_seed(7)
+    for B, K in ((64, 4096), (300, 768), (5, 12)):
+        x = torch.randn(B, K, generator=g)
+        xa = x.to(DEV)
+        buf = torch.empty(B * K + 1, device=DEV)
+        buf[1:].copy_(xa.reshape(-1))
+        xm = buf[1:].view(B, K)                                  # 4-B offset: scalar path
+        assert xm.data_ptr() % 16 != 0
+        ra, rm = rows_sum(xa), rows_sum(xm)
+        assert torch.equal(ra, rm)
+        if B <= 256:
+            ref = torch.zeros(K)
+            for b in range(B):
+                ref = ref + x[b]
+            assert torch.equal(ra.cpu(), ref)
+        key = torch.randint(0, 3, (B,), generator=g, dtype=torch.int32).to(DEV)
+        assert torch.equal(rows_sum(xa, key=key, nkeys=3), rows_sum(xm, key=key, nkeys=3))
