@@ -535,3 +535,20 @@ def test_rows_sum_vector_path_bitwise():
             assert torch.equal(ra.cpu(), ref)
         key = torch.randint(0, 3, (B,), generator=g, dtype=torch.int32).to(DEV)
         assert torch.equal(rows_sum(xa, key=key, nkeys=3), rows_sum(xm, key=key, nkeys=3))
+
+
+def test_gather_transpose_bf16_paths():
+    """fpm_gather_transpose (bf16): the 16-B path (Q, ldo multiples of 8) and the 32-bit path (ldo =
+    Q + 2) both give out[c][q] = in[rows[q]][c] (0 for rows[q] < 0), bit for bit."""
+    from fpm import _lib
+    g = torch.Generator().manual_seed(11)
+    R, C, Q = 300, 128, 200
+    x = torch.randn(R, C, generator=g).to(torch.bfloat16).to(DEV)
+    rows = torch.randint(-1, R, (Q,), generator=g, dtype=torch.int32).to(DEV)
+    ref = torch.where(rows.long()[None, :] >= 0, x[rows.long().clamp(min=0)].t(), torch.zeros((), dtype=x.dtype, device=DEV))
+    for ldo in (Q, Q + 2):
+        out = torch.full((C, ldo), 7.0, dtype=torch.bfloat16, device=DEV)
+        _lib.call("fpm_gather_transpose", 1, ops._p(x), x.stride(0), ops._p(rows), Q, C, ops._p(out), ldo,
+                  ops._stream(x))
+        torch.cuda.synchronize()
+        assert torch.equal(out[:, :Q], ref), ldo
