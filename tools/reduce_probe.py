@@ -1,0 +1,49 @@
+"""Which torch reductions in a training step cost GPU time: one step under torch.profiler with
+Python stacks, top aten ops by self device time (development probe)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import torch
+    import fpm
+    from fpm import params, synth, train
+    from fpm.batch import DeviceBatch
+    from torch.profiler import profile, ProfilerActivity
+    dev = torch.device("cuda", 0)
+    B, n = 64, 256
+    bt = DeviceBatch.from_pairs(synth.make_batch(3, B, n), dev)
+    gt = torch.zeros(B, n, n, device=dev)
+    gt[:, torch.arange(n), torch.arange(n)] = 1.0
+    label = (torch.arange(B, device=dev) % 2).float()
+    net = fpm.Net(regression=True, backbone=False, dtype="bf16")
+    net.load_state_dict(params.init_params(1))
+    net.to(dev).train()
+    ns = [bt.n_host[0], bt.n_host[1]]
+
+    def step():
+        out = net({"fpm_batch": bt, "gt_perm_mat": gt, "label": label})
+        loss = train.permutation_loss(out["ds_mat"], gt, ns[0], ns[1]) + out["ks_loss"] + out["cls_loss"]
+        loss.backward()
+        net.zero_grad(set_to_none=True)
+
+    step()
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+        step()
+        torch.cuda.synchronize()
+    rows = {}
+    for e in prof.events():
+        if e.key in ("aten::copy_", "aten::sum", "aten::fill_", "aten::add", "aten::add_") and e.self_device_time_total > 0:
+            st = [fr for fr in (e.stack or []) if "fingerprint" in fr or "fpm" in fr][:3]
+            k = (e.key, tuple(st))
+            c, t = rows.get(k, (0, 0.0))
+            rows[k] = (c + 1, t + e.self_device_time_total)
+    for (name, st), (c, t) in sorted(rows.items(), key=lambda kv: -kv[1][1])[:25]:
+        print("%-12s calls %4d  self dev %8.1f us  %s" % (name, c, t, " <- ".join(s.split("/")[-1] for s in st)))
+
+
+if __name__ == "__main__":
+    main()
