@@ -102,6 +102,13 @@ SIGNATURES = {
     "fpm_spline_conv_bwd_data_scatter": (I, [I, P, P, P, L, L, I, P, P, P, I, P, P, P, P, P, P, I, P]),
     "fpm_kron_agg": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, I, P, P]),
     "fpm_kron_gnn_layer_bwd_point": (I, [P, I, I, I, I, P, P, P, P, P, P, P]),
+    "fpm_kron_gnn_layer_fwd_f64": (I, [P, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P]),
+    "fpm_sinkhorn_log_fwd_f64": (I, [P, I, L, L, L, P, L, L, L, P, L, L, L, P, P, I, I, I, I, ctypes.c_double, I, P]),
+    "fpm_node_classifier_f64": (I, [P, I, I, I, P, P, P, P, P]),
+    "fpm_crossset_attn_row_f64": (I, [P, L, L, I, I, I, P, P, I, P, P, P, P, P, P]),
+    "fpm_gemm_f64": (I, [P, I, P, I, P, P, I, I, I, I, I, P]),
+    "fpm_instnorm_f64": (I, [P, P, I, I, I, P, P, P, P, ctypes.c_double, P, P, P]),
+    "fpm_afau_head_f64": (I, [P, P, P, I, I, P, P, P, P, P, P, P, P, P, P]),
     "fpm_profile_enable": (I, [I]),
     "fpm_profile_enabled": (I, []),
     "fpm_profile_read": (I, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),

@@ -199,6 +199,14 @@ class Net(nn.Module):
         # fp32 reference's own deviation (tools/kprob_yround.py), so the bf16 mode keeps them for the
         # large graphs where they pay (C3: n = 256) and stays near-fp32 below.
         self.sc_f32_nmax = int(os.environ.get("FPM_SC_F32_NMAX", "64"))
+        # the k chain in fp64 (csrc/precise.hip): batches whose padded box is at most FPM_K_F64_NMAX
+        # (64, at most 128) keypoints run everything after Kp -- the three GNN layers with their
+        # Sinkhorns, the readout, the final Sinkhorn and the AFA-U regressor -- in fp64, both modes,
+        # inference only.  On image-derived pairs of that size k_prob is ill-conditioned: the fp32
+        # rounding of any one stage after Kp moves it by up to ~6e-5 and the fp32 reference sits up
+        # to 2e-4 from its own fp64 value (tools/kprob_arith.py); in fp64 the device lands within
+        # ~5e-6 of it.  0 = off.
+        self.k_f64_nmax = min(128, int(os.environ.get("FPM_K_F64_NMAX", "64")))
         # FPM_PROLOGUE_GRAPH: the eager forward's prologue (coefficients, casts, AFA-U column block,
         # spline plans: ~15 small launches whose Python enqueue left the GPU idle ~0.5 ms at the start
         # of a 128-pair forward) replayed from a HIP graph captured on the batch's first forward.
@@ -252,7 +260,7 @@ class Net(nn.Module):
                             sd[pre + ".root"].to(device).t()[None]]).contiguous().float()
             d["W%d" % l] = wf.to(op)
             # fp32 copies for the bf16 mode's small-graph SplineConv (_sc_f32)
-            d["W%df" % l] = wf if op == torch.float32 else (wf if self.sc_f32_nmax > 0 else None)
+            d["W%df" % l] = wf
             d["bias%d" % l] = g(pre + ".bias")
         d["aff_w"] = g("vertex_affinity.A.weight")          # [768][1024] = N x K
         d["aff_wT"] = d["aff_w"].t().contiguous()          # [1024][768] for fpm_coef_tanh
@@ -316,6 +324,26 @@ class Net(nn.Module):
             d["mc_sh" + tag] = (gb - rm * sc).float().to(device)
         d["mc_fcw"] = g("match_cls.fc.weight").reshape(-1).contiguous()
         d["mc_fcb"] = g("match_cls.fc.bias")
+        # fp64 copies of the AFA-U weights for the fp64 k chain (the GNN packs are read as fp32 and
+        # widened in the kernel)
+        g64 = lambda k: sd[k].to(device=device, dtype=torch.float64).contiguous()
+        f = {}
+        for blk in ("row", "col"):
+            pre = "encoder_k.layers.0.%s_encoding_block" % blk
+            for k, name in (("Wv", ".Wv.weight"), ("mix1w", ".mixed_score_MHA.mix1_weight"),
+                            ("mix1b", ".mixed_score_MHA.mix1_bias"), ("mix2w", ".mixed_score_MHA.mix2_weight"),
+                            ("mix2b", ".mixed_score_MHA.mix2_bias"), ("Wc", ".multi_head_combine.weight"),
+                            ("bc", ".multi_head_combine.bias"), ("W1", ".feed_forward.W1.weight"),
+                            ("b1", ".feed_forward.W1.bias"), ("W2", ".feed_forward.W2.weight"),
+                            ("b2", ".feed_forward.W2.bias"), ("n1w", ".add_n_normalization_1.norm.weight"),
+                            ("n1b", ".add_n_normalization_1.norm.bias"), ("n2w", ".add_n_normalization_2.norm.weight"),
+                            ("n2b", ".add_n_normalization_2.norm.bias")):
+                f[blk + "_" + k] = g64(pre + name).reshape(-1).contiguous() if k.startswith("mix") else g64(pre + name)
+        for h in ("final_row", "final_col"):
+            for i in (0, 2):
+                f["%s%dw" % (h, i)] = g64("%s.%d.weight" % (h, i)).reshape(-1).contiguous()
+                f["%s%db" % (h, i)] = g64("%s.%d.bias" % (h, i))
+        d["f64"] = f
         self._pack, self._pack_key = d, key
         self._pack_gen += 1
         return d
@@ -360,6 +388,10 @@ class Net(nn.Module):
         """SplineConv products (and the vertex affinity) in fp32 for this batch: the fp32 mode, and the
         bf16 mode on batches whose padded box is at most ``sc_f32_nmax`` keypoints."""
         return self.dtype_mode != "bf16" or max(bt.nmax) <= self.sc_f32_nmax
+
+    def _k_f64(self, bt):
+        """The fp64 k chain for this batch (inference forwards on boxes of at most k_f64_nmax keypoints)."""
+        return (not self.training) and self.k_f64_nmax > 0 and max(bt.nmax) <= self.k_f64_nmax
 
     def _kp_split(self, side, bt):
         """Split-operand pattern of side ``side``'s affinity operand rows (0: plain rows)."""
@@ -529,6 +561,58 @@ class Net(nn.Module):
                       wp["final_row2b"], wp["final_col0w"], wp["final_col0b"], wp["final_col2w"], wp["final_col2b"], ks)
         return ks
 
+    def _afau_f64(self, wp, ss64, bt):
+        """AFA-U k regression (ngm.py:386-412) in fp64 from the fp64 ss (the fp64 k chain) -> ks (B,)
+        fp32.  Row block: attention, combine, norm, FFN, norm + max-pool; col block (independent of
+        ss: one-hot rows + the combine bias) once per distinct n2, gathered per pair."""
+        f = wp["f64"]
+        dev = ss64.device
+        B, n1max, n2max = bt.B, bt.n1max, bt.n2max
+        E, HD = C.AFAU_EMB, C.AFAU_HEADS * C.AFAU_QKV
+        if max(n1max, n2max) > self.univ_size:
+            raise AssertionError("UNIV_SIZE cap: n1max/n2max must be <= %d (ngm.py:387-389)" % self.univ_size)
+        f64 = dict(device=dev, dtype=torch.float64)
+        att = torch.empty(B * n1max, HD, **f64)
+        ops.crossset_attn_row_f64(ss64, bt.n2, f["row_Wv"], f["row_mix1w"], f["row_mix1b"], f["row_mix2w"],
+                                  f["row_mix2b"], att)
+        mh = ops.gemm_f64(att, f["row_Wc"], f["row_bc"])
+        o1 = torch.empty_like(mh)
+        ops.instnorm_f64(mh, B, n1max, E, f["row_n1w"], f["row_n1b"], out=o1)
+        ff = ops.gemm_f64(ops.gemm_f64(o1, f["row_W1"], f["row_b1"], relu=True), f["row_W2"], f["row_b2"])
+        g_row = torch.empty(B, E, **f64)
+        ops.instnorm_f64(o1, B, n1max, E, f["row_n2w"], f["row_n2b"], in2=ff, gmax=g_row)
+        n2u, n2u_d, inv = self._afau_col_index(bt)
+        U = len(n2u)
+        o1c = torch.empty(U * n2max, E, **f64)
+        ops.instnorm_f64(None, U, n2max, E, f["col_n1w"], f["col_n1b"], nvalid=n2u_d, onehot_bias=f["col_bc"], out=o1c)
+        ffc = ops.gemm_f64(ops.gemm_f64(o1c, f["col_W1"], f["col_b1"], relu=True), f["col_W2"], f["col_b2"])
+        g_col = torch.empty(U, E, **f64)
+        ops.instnorm_f64(o1c, U, n2max, E, f["col_n2w"], f["col_n2b"], in2=ffc, gmax=g_col)
+        ks = torch.empty(B, device=dev, dtype=torch.float32)
+        ops.afau_head_f64(g_row, g_col, None if inv is None else inv.to(torch.int32), B, E, f["final_row0w"],
+                          f["final_row0b"], f["final_row2w"], f["final_row2b"], f["final_col0w"], f["final_col0b"],
+                          f["final_col2w"], f["final_col2b"], ks)
+        return ks
+
+    def _gnn_chain_f64(self, wp, bt, Kp, csr1, csr2, s, ss, ss64):
+        """The three GNN layers (+ their Sinkhorns), the readout and the final Sinkhorn in fp64
+        (csrc/precise.hip) from the fp32 Kp: writes s / ss (fp32 copies) and ss64."""
+        dev = bt.device
+        B, n1max, n2max = bt.B, bt.n1max, bt.n2max
+        f64 = dict(device=dev, dtype=torch.float64)
+        X, Cin = Kp, 1
+        zbuf = torch.empty(B, n2max, n1max, **f64)
+        for l in range(C.GNN_LAYER):
+            Xn = torch.empty(B, 17, n2max, n1max, **f64)
+            ops.gnn_layer_f64(X, Cin, B, n1max, n2max, csr1, csr2, bt.n1, bt.n2, wp["gnn%d" % l], Xn, zbuf)
+            ops.sinkhorn_f64(zbuf.transpose(1, 2), bt.n1, bt.n2, C.GNN_SK_ITER, self.tau, True,
+                             out=Xn[:, 16].transpose(1, 2))
+            X, Cin = Xn, 17
+            self._mark("gnn%d" % l)
+        s64 = torch.empty(B, n1max, n2max, **f64)
+        ops.node_classifier_f64(X, B, n1max, n2max, wp["cls_w"], wp["cls_b"], s64, s)
+        ops.sinkhorn_f64(s64, bt.n1, bt.n2, C.SK_ITER_NUM, self.tau, True, out=ss64, out32=ss)
+
     def _mark(self, name):
         """Diagnostic stage timing (FPM_STAGE_TIMING=1): synchronises, so never in timed runs.
         FPM_STAGE_EVENTS=1: a timing event on the current stream per mark instead (no sync; for
@@ -578,11 +662,12 @@ class Net(nn.Module):
         ops.coef_tanh(gw, wp["aff_wT"], wp["aff_b"], coef)
         return gw, coef
 
-    def run_gpu_stage(self, bt, keep_feats=False, s_out=None, ss_out=None, gc=None, x_ops=(None, None), plans=None):
+    def run_gpu_stage(self, bt, keep_feats=False, s_out=None, ss_out=None, gc=None, x_ops=(None, None), plans=None,
+                      ss64_out=None):
         """Everything up to ss on the GPU.  Returns a dict of device tensors.  ``gc``: this
         batch's rows of global_coef() when computed for a parent batch; ``x_ops``: its rows of the
         parent's bf16 operand copies of the node features (cast once per forward); ``plans``:
-        plans(bt) when already computed."""
+        plans(bt) when already computed; ``ss64_out``: the fp64 ss of the fp64 k chain (_k_f64)."""
         keep_feats = keep_feats or self.compute_ke
         self._keep_feats = keep_feats
         if self._stage_timing:
@@ -611,6 +696,18 @@ class Net(nn.Module):
         self._mark("affinity")
         csr1 = ops.plan_csr(plan0, bt.E[0], B * n1max)
         csr2 = ops.plan_csr(plan1, bt.E[1], B * n2max)
+        if self._k_f64(bt):
+            s = s_out if s_out is not None else torch.empty(B, n1max, n2max, device=dev, dtype=torch.float32)
+            ss = ss_out if ss_out is not None else torch.empty(B, n1max, n2max, device=dev, dtype=torch.float32)
+            ss64 = ss64_out if ss64_out is not None else torch.empty(B, n1max, n2max, device=dev, dtype=torch.float64)
+            self._gnn_chain_f64(wp, bt, Kp, csr1, csr2, s, ss, ss64)
+            self._mark("final_sinkhorn")
+            out = dict(s=s, ss=ss, ss64=ss64, Kp=Kp[:, 0].transpose(1, 2), coef=coef)
+            if keep_feats:
+                out["feat0"], out["feat1"] = f1, f2
+            if Ke is not None:
+                out["Ke"] = Ke
+            return out
         zbuf = torch.empty(B, n2max, n1max, device=dev, dtype=torch.float32)
         vpart = torch.empty(B, n2max, n1max, device=dev, dtype=torch.float32)
         Cin = 1
@@ -695,7 +792,8 @@ class Net(nn.Module):
         x_ops = tuple(None if t is None else t[b0 * part.nmax[s]:b1 * part.nmax[s]]
                       for s, t in enumerate(xop or (None, None)))
         r = self.run_gpu_stage(part, keep_feats, s_out=o["s"][b0:b1], ss_out=o["ss"][b0:b1],
-                               gc=(gc[0][b0:b1], gc[1][b0:b1]), x_ops=x_ops, plans=plans)
+                               gc=(gc[0][b0:b1], gc[1][b0:b1]), x_ops=x_ops, plans=plans,
+                               ss64_out=o["ss64"][b0:b1] if "ss64" in o else None)
         if tail is None:
             self._stage_tail(part, b0, b1, o, gt_ks, min_pt, col, host=self._pinned[b0:b1] if zc else None)
             return r
@@ -727,7 +825,9 @@ class Net(nn.Module):
         the pinned rows of the host Hungarian, written by the soft top-k kernel itself (zero-copy)."""
         dev = part.device
         ks = o["k_prob"][b0:b1]
-        if self.regression:
+        if self.regression and "ss64" in o:
+            ks.copy_(self._afau_f64(self.packed(dev), o["ss64"][b0:b1], part))
+        elif self.regression:
             ks.copy_(self._afau(self.packed(dev), o["ss"][b0:b1], part, col=col, b0=b0))
         else:
             ks.copy_(gt_ks[b0:b1] / min_pt[b0:b1])
@@ -788,9 +888,11 @@ class Net(nn.Module):
         return dt
 
     @staticmethod
-    def _alloc_outputs(B, n1max, n2max, dev):
+    def _alloc_outputs(B, n1max, n2max, dev, k_f64=False):
         f32 = dict(device=dev, dtype=torch.float32)
         o = {k: torch.empty(B, n1max, n2max, **f32) for k in ("s", "ss", "ds_mat", "perm_mat", "lsa")}
+        if k_f64:
+            o["ss64"] = torch.empty(B, n1max, n2max, device=dev, dtype=torch.float64)
         o.update({k: torch.empty(B, **f32) for k in ("k_prob", "cls_logits", "cls_prob", "_kk")})
         o["sk_steps"] = torch.empty(B, device=dev, dtype=torch.int32)
         o["_lsa_status"] = torch.zeros(B, device=dev, dtype=torch.int32)
@@ -859,7 +961,7 @@ class Net(nn.Module):
         # the fused-norm switch and the kernel-variant switches (ops.set_tuning)
         key = (len(parts), tuple(rng), self.dtype_mode, self.afau_mode, self.kp_x3, self.regression,
                self.n_streams, self._pack_gen, str(dev), float(self.tau), self.afau_fuse_norm,
-               ops.tuning_generation())
+               ops.tuning_generation(), self.sc_f32_nmax, self.k_f64_nmax)
         g = self._gstate
         if g is not None and g["bt"]() is bt and g["key"] == key:
             return g
@@ -914,7 +1016,7 @@ class Net(nn.Module):
         self.packed(dev)                      # (re)packed weights outside any capture; sets _pack_gen
         rng = tuple((0, bt.B) if p is bt else p.pair_range for p in parts)
         key = (len(parts), rng, self.dtype_mode, self.afau_mode, self.kp_x3, self.regression, self._pack_gen,
-               str(dev), self.afau_fuse_norm, ops.tuning_generation())
+               str(dev), self.afau_fuse_norm, ops.tuning_generation(), self.sc_f32_nmax, self.k_f64_nmax)
         g = self._pgstate
         if g is None or g["bt"]() is not bt or g["key"] != key:
             import weakref
@@ -940,7 +1042,8 @@ class Net(nn.Module):
 
     def _graphed(self, parts, keep_feats=False):
         return (self.use_graphs and not keep_feats and self.lsa_mode != "device" and not self.compute_ke
-                and not self.training and not self._stage_timing and not self._stage_events and not ops.profiling())
+                and not self.training and not self._stage_timing and not self._stage_events and not ops.profiling()
+                and not self._k_f64(parts[0]))
 
     def stage_events(self, reset=True, absolute=False):
         """FPM_STAGE_EVENTS=1: [(stage, ms since the previous mark)] of the marks recorded so far
@@ -997,7 +1100,7 @@ class Net(nn.Module):
             gs = self._graph_state(bt, parts, dev)
             o, min_pt, gt_ks = gs["o"], gs["min_pt"], gs["gt_ks"]
         else:
-            o = self._alloc_outputs(B, n1max, n2max, dev)
+            o = self._alloc_outputs(B, n1max, n2max, dev, k_f64=self._k_f64(bt))
             min_pt = torch.minimum(bt.n1, bt.n2).to(torch.float32)
             gt_ks = min_pt.clone()
         if gt_perm is not None:

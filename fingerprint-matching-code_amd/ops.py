@@ -482,6 +482,122 @@ def afau_head(gr, gc, B, E, r0w, r0b, r2w, r2b, c0w, c0b, c2w, c2b, ks):
               _p(c2w), _p(c2b), _p(ks), _stream(gr))
 
 
+# ---- fp64 k chain (csrc/precise.hip): Kp -> GNN layers -> readout -> final Sinkhorn -> AFA-U -------
+def _f64(*ts):
+    for t in ts:
+        if t is not None and t.dtype != torch.float64:
+            raise _lib.FpmError("fp64 k-chain op: float64 tensor expected, got %s" % t.dtype)
+
+
+def gnn_layer_f64(X, C, B, n1max, n2max, csr1, csr2, n1, n2, params, Xout, zbuf):
+    """PYGNNLayer in fp64: X (B, C, n2max, n1max) fp32 Kp for C = 1, the fp64 state for C = 17 ->
+    Xout[:, 0:16] (fp64) and zbuf (B, n2max, n1max) fp64 (fpm_kron_gnn_layer_fwd_f64)."""
+    _dev(X, n1, n2, params, Xout, zbuf)
+    _shape(X, (B, C, n2max, n1max), "gnn_layer_f64 X")
+    _shape(Xout, (B, 17, n2max, n1max), "gnn_layer_f64 Xout")
+    _shape(zbuf, (B, n2max, n1max), "gnn_layer_f64 zbuf")
+    _f64(Xout, zbuf)
+    if not (X.is_contiguous() and Xout.is_contiguous() and zbuf.is_contiguous()):
+        raise _lib.FpmError("gnn_layer_f64: contiguous tensors expected")
+    x64 = X.dtype == torch.float64
+    if x64 != (C == 17) or (not x64 and X.dtype != torch.float32):
+        raise _lib.FpmError("gnn_layer_f64: layer 0 reads fp32 Kp (C = 1), later layers the fp64 state (C = 17)")
+    _lib.call("fpm_kron_gnn_layer_fwd_f64", _p(X), int(x64), C, B, n1max, n2max, ctypes.c_void_p(csr1[0]),
+              ctypes.c_void_p(csr1[1]), ctypes.c_void_p(csr2[0]), ctypes.c_void_p(csr2[1]), _p(n1), _p(n2),
+              _p(params), _p(Xout), _p(zbuf), _stream(X))
+
+
+def sinkhorn_f64(s, n1, n2, iters, tau, dummy_row=True, out=None, out32=None):
+    """pygm log Sinkhorn in fp64 on each pair's valid block of the (n1max, n2max) box: ``s`` any
+    strided fp32 / fp64 3-D view, ``out`` an fp64 view (allocated when None and ``out32`` is None),
+    ``out32`` an optional fp32 copy.  Boxes up to 128 x 128."""
+    _dev(s, n1, n2, out, out32)
+    B, n1max, n2max = s.shape
+    if out is None and out32 is None:
+        out = torch.empty(B, n1max, n2max, device=s.device, dtype=torch.float64)
+    _shape(out, (B, n1max, n2max), "sinkhorn_f64 out")
+    _shape(out32, (B, n1max, n2max), "sinkhorn_f64 out32")
+    _shape(n1, (B,), "sinkhorn_f64 n1")
+    _shape(n2, (B,), "sinkhorn_f64 n2")
+    _f64(out)
+    if out32 is not None and out32.dtype != torch.float32:
+        raise _lib.FpmError("sinkhorn_f64: out32 must be float32")
+    if s.dtype not in (torch.float32, torch.float64):
+        raise _lib.FpmError("sinkhorn_f64: s must be float32 or float64")
+    st = lambda t: (t.stride(0), t.stride(1), t.stride(2)) if t is not None else (0, 0, 0)
+    _lib.call("fpm_sinkhorn_log_fwd_f64", _p(s), int(s.dtype == torch.float64), *st(s), _p(out), *st(out), _p(out32),
+              *st(out32), _p(n1), _p(n2), B, n1max, n2max, int(iters), float(tau), int(bool(dummy_row)), _stream(s))
+    return out
+
+
+def node_classifier_f64(X, B, n1max, n2max, w, b, s64, s32=None):
+    """s = classifier(emb) (ngm.py:368-369) from the fp64 state: s64 (B, n1max, n2max) fp64 and
+    optionally its fp32 copy."""
+    _dev(X, w, b, s64, s32)
+    _shape(X, (B, 17, n2max, n1max), "node_classifier_f64 X")
+    _shape(s64, (B, n1max, n2max), "node_classifier_f64 s64")
+    _shape(s32, (B, n1max, n2max), "node_classifier_f64 s32")
+    _f64(X, s64)
+    for t in (X, s64, s32):
+        if t is not None and not t.is_contiguous():
+            raise _lib.FpmError("node_classifier_f64: contiguous tensors expected")
+    _lib.call("fpm_node_classifier_f64", _p(X), B, n1max, n2max, _p(w), _p(b), _p(s64), _p(s32), _stream(X))
+
+
+def crossset_attn_row_f64(cost, n2, Wv, mix1w, mix1b, mix2w, mix2b, out):
+    """The AFA-U row block's cross-set attention (R0 = 0) in fp64: cost (B, n1max, n2max) fp64 with
+    unit column stride -> out (B * n1max, 256) fp64."""
+    _dev(cost, n2, Wv, out)
+    _f64(cost, Wv, mix1w, mix1b, mix2w, mix2b, out)
+    B, n1max, n2max = cost.shape
+    _shape(out, (B * n1max, 256), "crossset_attn_row_f64 out")
+    if cost.stride(2) != 1 or not Wv.is_contiguous() or not out.is_contiguous():
+        raise _lib.FpmError("crossset_attn_row_f64: unit-stride cost rows, contiguous Wv / out expected")
+    _lib.call("fpm_crossset_attn_row_f64", _p(cost), cost.stride(0), cost.stride(1), B, n1max, n2max, _p(n2), _p(Wv),
+              Wv.shape[1], _p(mix1w), _p(mix1b), _p(mix2w), _p(mix2b), _p(out), _stream(cost))
+
+
+def gemm_f64(A, W, bias=None, relu=False, out=None):
+    """out = act(A @ W^T + bias) in fp64 (fpm_gemm_f64): A (M, K), W (N, K)."""
+    _dev(A, W, bias, out)
+    _f64(A, W, bias, out)
+    M, K = A.shape
+    N = W.shape[0]
+    if W.shape[1] != K or A.stride(1) != 1 or W.stride(1) != 1:
+        raise _lib.FpmError("gemm_f64: A (M, K), W (N, K) with unit column stride expected")
+    if out is None:
+        out = torch.empty(M, N, device=A.device, dtype=torch.float64)
+    _shape(out, (M, N), "gemm_f64 out")
+    _lib.call("fpm_gemm_f64", _p(A), A.stride(0), _p(W), W.stride(0), _p(bias), _p(out), out.stride(0), M, N, K,
+              int(bool(relu)), _stream(A))
+    return out
+
+
+def instnorm_f64(in1, B, P, Cn, w, b, in2=None, nvalid=None, onehot_bias=None, out=None, gmax=None, eps=1e-5):
+    """AddAndInstanceNormalization (afau.py:154-176) in fp64 over each pair's P rows of Cn channels:
+    x = in1 (+ in2), or the col block's one-hot + bias; out (B * P, Cn) and/or gmax (B, Cn)."""
+    ref = in1 if in1 is not None else w
+    _dev(ref, in2, nvalid, onehot_bias, w, b, out, gmax)
+    _f64(in1, in2, onehot_bias, w, b, out, gmax)
+    for t in (in1, in2, out):
+        _shape(t, (B * P, Cn), "instnorm_f64 rows")
+    _shape(gmax, (B, Cn), "instnorm_f64 gmax")
+    _lib.call("fpm_instnorm_f64", _p(in1), _p(in2), B, P, Cn, _p(nvalid), _p(onehot_bias), _p(w), _p(b), float(eps),
+              _p(out), _p(gmax), _stream(ref))
+
+
+def afau_head_f64(gr, gc, cidx, B, E, r0w, r0b, r2w, r2b, c0w, c0b, c2w, c2b, ks):
+    """ks = sigmoid((final_row(gr) + final_col(gc[cidx])) / 2) from fp64 pooled rows -> ks fp32."""
+    _dev(gr, gc, cidx, ks)
+    _f64(gr, gc, r0w, r0b, r2w, r2b, c0w, c0b, c2w, c2b)
+    _shape(gr, (B, E), "afau_head_f64 gr")
+    _shape(ks, (B,), "afau_head_f64 ks")
+    if cidx is not None and (cidx.dtype != torch.int32 or tuple(cidx.shape) != (B,)):
+        raise _lib.FpmError("afau_head_f64: cidx must be int32 (B,)")
+    _lib.call("fpm_afau_head_f64", _p(gr), _p(gc), _p(cidx), B, E, _p(r0w), _p(r0b), _p(r2w), _p(r2b), _p(c0w),
+              _p(c0b), _p(c2w), _p(c2b), _p(ks), _stream(gr))
+
+
 def match_cls(s, perm, w1, b1, bn1_sc, bn1_sh, w2, b2, bn2_sc, bn2_sh, fcw, fcb, logits=None, prob=None, dtype=F32):
     _dev(s, perm)
     if not (s.is_contiguous() and perm.is_contiguous()):

@@ -265,6 +265,43 @@ int fpm_afau_head(const float* gr, const float* gc, int B, int E, const float* r
                   const float* r2w, const float* r2b, const float* c0w, const float* c0b, const float* c2w,
                   const float* c2b, float* ks, void* stream);
 
+/* ---- fp64 k chain (csrc/precise.hip) ----------------------------------------------------------
+ * Everything after the vertex affinity Kp in double precision, for small boxes where k_prob is
+ * ill-conditioned (Net.k_f64_nmax): the same algebra as the fp32 entry points above.
+ * fpm_kron_gnn_layer_fwd_f64: PYGNNLayer (gnn.py:207-226); X is fp32 Kp (x_f64 = 0, C = 1) or the
+ *   fp64 state (x_f64 = 1, C = 17); params as fpm_kron_gnn_layer_fwd; Xout channels 0..15 and zbuf
+ *   fp64; n1max <= 1024 and C x n1max doubles within LDS.
+ * fpm_sinkhorn_log_fwd_f64: pygm sinkhorn (sinkhorn.py:85-87) in fp64 on fp32 (s_f64 = 0) or fp64
+ *   input, any strides; o64 (fp64) and / or o32 (fp32 copy) outputs; boxes up to 128 x 128.
+ * fpm_node_classifier_f64: s = classifier(emb) (ngm.py:368-369) -> s64 (+ optional fp32 s32).
+ * fpm_crossset_attn_row_f64: the AFA-U row block's attention with R0 = 0 (afau.py:231-300), out
+ *   (B x n1max) x 256 fp64.
+ * fpm_gemm_f64: C = act(A W^T + bias), relu = 1 for ReLU (the AFA-U projections and FFN).
+ * fpm_instnorm_f64: AddAndInstanceNormalization (afau.py:154-176) over P positions; in1 (+ in2) or
+ *   (in1 NULL) the col block's one-hot + onehot_bias; out and / or gmax (max over positions).
+ * fpm_afau_head_f64: ks[b] = sigmoid((final_row(gr[b]) + final_col(gc[cidx[b]])) / 2) (ngm.py:401-412),
+ *   cidx NULL = b; ks fp32. */
+int fpm_kron_gnn_layer_fwd_f64(const void* X, int x_f64, int C, int B, int n1max, int n2max, const int* ptr1,
+                               const int* nbr1, const int* ptr2, const int* nbr2, const int* n1, const int* n2,
+                               const float* params, double* Xout, double* zbuf, void* stream);
+int fpm_sinkhorn_log_fwd_f64(const void* s, int s_f64, long s_sb, long s_si, long s_sj, double* o64, long o_sb,
+                             long o_si, long o_sj, float* o32, long f_sb, long f_si, long f_sj, const int* n1,
+                             const int* n2, int B, int n1max, int n2max, int iters, double tau, int dummy_row,
+                             void* stream);
+int fpm_node_classifier_f64(const double* X, int B, int n1max, int n2max, const float* w, const float* bias,
+                            double* s64, float* s32, void* stream);
+int fpm_crossset_attn_row_f64(const double* cost, long c_sb, long c_ld, int B, int n1max, int n2max, const int* n2,
+                              const double* Wv, int emb, const double* mix1w, const double* mix1b,
+                              const double* mix2w, const double* mix2b, double* out, void* stream);
+int fpm_gemm_f64(const double* A, int lda, const double* W, int ldw, const double* bias, double* C, int ldc, int M,
+                 int N, int K, int relu, void* stream);
+int fpm_instnorm_f64(const double* in1, const double* in2, int B, int P, int Cn, const int* nvalid,
+                     const double* onehot_bias, const double* w, const double* bias, double eps, double* out,
+                     double* gmax, void* stream);
+int fpm_afau_head_f64(const double* gr, const double* gc, const int* cidx, int B, int E, const double* r0w,
+                      const double* r0b, const double* r2w, const double* r2b, const double* c0w, const double* c0b,
+                      const double* c2w, const double* c2b, float* ks, void* stream);
+
 /* ---- AFA-U backward (training, src/model/afau.py:54-300 through ks_loss, training_loop.py:60) ---
  * fpm_afau_head_bwd: ks = sigmoid((final_row(gr) + final_col(gc)) / 2) -> dgr, dgc (B x E) and
  *   per-pair parameter partials part[b] = 2 x [dW0 (8 x E) | db0 (8) | dw2 (8) | db2] (row, col).

@@ -11,7 +11,7 @@ tools/kprob_sources.py's bf16src probe rounded the operands only.  Here the orac
 and reports, per pair, |k - k64| beyond the fp32 oracle's own |k32 - k64| (the image-path gate's
 "excess"), on the test's image seeds (tests/test_frontend.py::_image_batch, CPU backbone).
 
-    python tools/kprob_yround.py [--seeds 8,9,10,11,12,13]
+    python tools/kprob_yround.py [--seeds 8,9,10,11,12,13] [--n 32]
 """
 import argparse
 import os
@@ -27,6 +27,7 @@ sys.path.insert(0, os.path.join(REPO, "tools"))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seeds", default="8,9,10,11,12,13")
+    ap.add_argument("--n", type=int, default=32)
     args = ap.parse_args()
     import oracle as O
     from oracle import ngm_oracle as NO
@@ -67,7 +68,7 @@ def main():
                 "ops+Y1": (True, True, (0,))}
     worst = {v: 0.0 for v in variants}
     for seed in map(int, args.seeds.split(",")):
-        pairs = image_pairs(3, 32, seed)
+        pairs = image_pairs(3, args.n, seed)
         k32 = O.forward(pairs, sd)["k_prob"].double()
         k64 = O.forward(pairs, sd, dtype=torch.float64)["k_prob"]
         floor = (k32 - k64).abs()
