@@ -552,7 +552,7 @@ class Net(nn.Module):
             ops.gemm(att, wp["row_Wc"], B * n1max, E, kc, att.shape[1], att.shape[1], bias=wp["row_bc"], out_f=mh,
                      ldc=E)
             g_row = self._afau_block(wp, "row", B, n1max, mh=mh)
-        if col is None or col[2] != n2max:
+        if col is None or isinstance(col[0], str) or col[2] != n2max:
             col, b0 = self._afau_col(wp, bt), 0
         n2u, gm_u, _, inv = col
         g_col = gm_u if inv is None else gm_u.index_select(0, inv[b0:b0 + B])
@@ -561,10 +561,26 @@ class Net(nn.Module):
                       wp["final_row2b"], wp["final_col0w"], wp["final_col0b"], wp["final_col2w"], wp["final_col2b"], ks)
         return ks
 
-    def _afau_f64(self, wp, ss64, bt):
+    def _afau_col_f64(self, wp, bt, idx=None):
+        """The AFA-U column block in fp64 (independent of ss: one-hot rows + the combine bias) once per
+        distinct n2 of the batch -> ("f64", pooled rows (U, E) fp64, n2max, int32 gather index or
+        None); ``idx`` = _afau_col_index(bt) (computed before any graph capture)."""
+        f = wp["f64"]
+        n2u, n2u_d, inv = idx if idx is not None else self._afau_col_index(bt)
+        U, n2max, E = len(n2u), bt.n2max, C.AFAU_EMB
+        f64 = dict(device=bt.device, dtype=torch.float64)
+        o1c = torch.empty(U * n2max, E, **f64)
+        ops.instnorm_f64(None, U, n2max, E, f["col_n1w"], f["col_n1b"], nvalid=n2u_d, onehot_bias=f["col_bc"], out=o1c)
+        ffc = ops.gemm_f64(ops.gemm_f64(o1c, f["col_W1"], f["col_b1"], relu=True), f["col_W2"], f["col_b2"])
+        g_col = torch.empty(U, E, **f64)
+        ops.instnorm_f64(o1c, U, n2max, E, f["col_n2w"], f["col_n2b"], in2=ffc, gmax=g_col)
+        return "f64", g_col, n2max, None if inv is None else inv.to(torch.int32)
+
+    def _afau_f64(self, wp, ss64, bt, col=None, b0=0):
         """AFA-U k regression (ngm.py:386-412) in fp64 from the fp64 ss (the fp64 k chain) -> ks (B,)
-        fp32.  Row block: attention, combine, norm, FFN, norm + max-pool; col block (independent of
-        ss: one-hot rows + the combine bias) once per distinct n2, gathered per pair."""
+        fp32.  Row block: attention, combine, norm, FFN, norm + max-pool; col block: ``col`` =
+        _afau_col_f64 of the forward's batch, whose pairs [b0, b0 + B) this (sub-)batch is (computed
+        here when None)."""
         f = wp["f64"]
         dev = ss64.device
         B, n1max, n2max = bt.B, bt.n1max, bt.n2max
@@ -581,15 +597,11 @@ class Net(nn.Module):
         ff = ops.gemm_f64(ops.gemm_f64(o1, f["row_W1"], f["row_b1"], relu=True), f["row_W2"], f["row_b2"])
         g_row = torch.empty(B, E, **f64)
         ops.instnorm_f64(o1, B, n1max, E, f["row_n2w"], f["row_n2b"], in2=ff, gmax=g_row)
-        n2u, n2u_d, inv = self._afau_col_index(bt)
-        U = len(n2u)
-        o1c = torch.empty(U * n2max, E, **f64)
-        ops.instnorm_f64(None, U, n2max, E, f["col_n1w"], f["col_n1b"], nvalid=n2u_d, onehot_bias=f["col_bc"], out=o1c)
-        ffc = ops.gemm_f64(ops.gemm_f64(o1c, f["col_W1"], f["col_b1"], relu=True), f["col_W2"], f["col_b2"])
-        g_col = torch.empty(U, E, **f64)
-        ops.instnorm_f64(o1c, U, n2max, E, f["col_n2w"], f["col_n2b"], in2=ffc, gmax=g_col)
+        if col is None or not isinstance(col[0], str) or col[2] != n2max:
+            col, b0 = self._afau_col_f64(wp, bt), 0
+        _, g_col, _, inv = col
         ks = torch.empty(B, device=dev, dtype=torch.float32)
-        ops.afau_head_f64(g_row, g_col, None if inv is None else inv.to(torch.int32), B, E, f["final_row0w"],
+        ops.afau_head_f64(g_row, g_col, None if inv is None else inv[b0:b0 + B], B, E, f["final_row0w"],
                           f["final_row0b"], f["final_row2w"], f["final_row2b"], f["final_col0w"], f["final_col0b"],
                           f["final_col2w"], f["final_col2b"], ks)
         return ks
@@ -826,7 +838,7 @@ class Net(nn.Module):
         dev = part.device
         ks = o["k_prob"][b0:b1]
         if self.regression and "ss64" in o:
-            ks.copy_(self._afau_f64(self.packed(dev), o["ss64"][b0:b1], part))
+            ks.copy_(self._afau_f64(self.packed(dev), o["ss64"][b0:b1], part, col=col, b0=b0))
         elif self.regression:
             ks.copy_(self._afau(self.packed(dev), o["ss"][b0:b1], part, col=col, b0=b0))
         else:
@@ -922,7 +934,9 @@ class Net(nn.Module):
             if not self._sc_f32(bt) and cast:
                 xop_ = tuple(None if (s == 0 and bt.shared0) else ops.cast_bf16(bt.x[s]) for s in range(2))
             self._mark("pro_cast")
-            col_ = self._afau_col(self.packed(dev), bt, col_idx) if self.regression else None
+            col_ = None
+            if self.regression:
+                col_ = (self._afau_col_f64 if self._k_f64(bt) else self._afau_col)(self.packed(dev), bt, col_idx)
             return xop_, col_
         if side is not None:
             with torch.cuda.stream(side):
@@ -970,7 +984,7 @@ class Net(nn.Module):
         import weakref
         B, n1max, n2max = bt.B, bt.n1max, bt.n2max
         g = {"bt": weakref.ref(bt), "key": key}
-        o = self._alloc_outputs(B, n1max, n2max, dev)
+        o = self._alloc_outputs(B, n1max, n2max, dev, k_f64=self._k_f64(bt))
         g["o"] = o
         g["min_pt"] = torch.minimum(bt.n1, bt.n2).to(torch.float32)
         g["gt_ks"] = g["min_pt"].clone()
@@ -1042,8 +1056,7 @@ class Net(nn.Module):
 
     def _graphed(self, parts, keep_feats=False):
         return (self.use_graphs and not keep_feats and self.lsa_mode != "device" and not self.compute_ke
-                and not self.training and not self._stage_timing and not self._stage_events and not ops.profiling()
-                and not self._k_f64(parts[0]))
+                and not self.training and not self._stage_timing and not self._stage_events and not ops.profiling())
 
     def stage_events(self, reset=True, absolute=False):
         """FPM_STAGE_EVENTS=1: [(stage, ms since the previous mark)] of the marks recorded so far
