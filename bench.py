@@ -53,7 +53,7 @@ def shard(config, rank, world, batch, gallery):
     replicated); otherwise ``batch`` pairs per rank (weak scaling).  No data-path collective."""
     if config == "c4":
         share = (gallery + world - 1) // world
-        first = rank * share
+        first = min(rank * share, gallery)          # ranks past the end: empty shards at the end
         return first, max(0, min(share, gallery - first))
     return rank * batch, batch
 
@@ -115,7 +115,7 @@ def parity_vs_oracle(pairs, ref, sd, dev, dtypes):
         d["perm_pairs_identical"] = float(np.mean([torch.equal(P[b], R[b]) for b in range(P.shape[0])]))
         # pair-by-pair class of every perm_mat difference (oracle.compare: select tie with the same
         # assignment, LSA near-tie whose assignment is optimal under the oracle's ds_mat within
-        # m * 1e-6, eps-optimal assignment within 2 m delta, k* rounding crossing, or mismatch); every
+        # m * 1e-6, eps-optimal assignment within 2 m delta (bf16 modes only), k* rounding crossing, or mismatch); every
         # differing pair carries its assignment gap under the oracle's ds_mat and the bound it met.
         # k* rounding crossings are judged against the mode's own k_prob bound (1e-4: the gate)
         gated = dt == "f32" or net.afau_mode == "bf16x3"
@@ -448,6 +448,11 @@ def main():
 
     if world > 1:
         dist.init_process_group("gloo")
+    # several ranks on the node: each rank's host Hungarian pool on its own slice of the CPUs
+    from fpm.model import pin_rank_cpus, host_cpu_share
+    pinned = pin_rank_cpus()
+    if pinned is not None:
+        log("rank %d pinned to %d CPUs (%d..%d)" % (rank, len(pinned), pinned[0], pinned[-1]))
     # one GPU per rank; with fewer visible GPUs than ranks (a rehearsal of the N-rank path on a
     # smaller box) ranks share devices round-robin and say so in the JSON
     ndev = torch.cuda.device_count()
@@ -688,6 +693,8 @@ def main():
             "share128_line": share_line,
             "tuning": tuning or None,
             "ranks_share_devices": shared_devices,
+            "host_cpus_per_rank": host_cpu_share(),
+            "ranks_pinned": pinned is not None,
             "input_gen_s": t_gen,
             "graph_build": graph_build,
         }

@@ -33,19 +33,50 @@ from . import params as P
 from .batch import DeviceBatch
 
 
+def rank_cpu_set(local_rank, local_world, aff=None):
+    """The CPUs of the node-local rank ``local_rank`` of ``local_world``: a contiguous, disjoint slice
+    of the (sorted) affinity mask, at least one CPU each (ranks share CPUs round-robin only when the
+    mask has fewer CPUs than ranks)."""
+    cpus = sorted(aff if aff is not None else os.sched_getaffinity(0))
+    local_world = max(1, int(local_world))
+    if len(cpus) < local_world:
+        return [cpus[int(local_rank) % len(cpus)]]
+    k = len(cpus) // local_world
+    return cpus[int(local_rank) * k:(int(local_rank) + 1) * k]
+
+
+def pin_rank_cpus():
+    """Under torch.distributed.run with several ranks on the node: restrict this process to its own
+    slice of the affinity mask (rank_cpu_set), so the ranks' host Hungarian pools do not compete for
+    the same cores (FPM_PIN_RANKS=0: off).  Returns the CPU list or None."""
+    lws = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+    if lws <= 1 or os.environ.get("FPM_PIN_RANKS", "1") == "0" or os.environ.get("FPM_RANK_PINNED") == "1":
+        return None
+    cpus = rank_cpu_set(int(os.environ.get("LOCAL_RANK", "0")), lws)
+    os.sched_setaffinity(0, cpus)
+    os.environ["FPM_RANK_PINNED"] = "1"
+    return cpus
+
+
 def host_cpu_share():
     """CPUs this process may use for the host Hungarian pool.  ``FPM_CPU_SHARE`` sets it explicitly
     (``FPM_LSA_THREADS`` sets the pool size itself, default 2 per CPU of the share).  Otherwise:
     OMP_NUM_THREADS (16 per GPU on the pool) capped by the affinity mask; under
-    torch.distributed.run (LOCAL_WORLD_SIZE present), whose launcher exports OMP_NUM_THREADS=1 when
-    the variable was unset, a share of 1 is read as that default and replaced by the affinity mask
-    split over the node's ranks (at most 16 each) -- set FPM_CPU_SHARE=1 to really run on one CPU."""
+    torch.distributed.run (LOCAL_WORLD_SIZE > 1) the cap is this rank's slice of the mask
+    (rank_cpu_set; after pin_rank_cpus the mask IS the slice), and a share of 1 is read as the
+    launcher's OMP_NUM_THREADS=1 default (it exports it when the variable was unset) and replaced
+    by the slice (at most 16) -- set FPM_CPU_SHARE=1 to really run on one CPU."""
     n_aff = len(os.sched_getaffinity(0))
     if os.environ.get("FPM_CPU_SHARE"):
         return max(1, min(int(os.environ["FPM_CPU_SHARE"]), n_aff))
     omp = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
-    if omp <= 1 and "LOCAL_WORLD_SIZE" in os.environ:
-        omp = min(16, n_aff // max(1, int(os.environ["LOCAL_WORLD_SIZE"])))
+    lws = int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1) if "LOCAL_WORLD_SIZE" in os.environ else 0
+    if lws >= 1:
+        cap = n_aff if os.environ.get("FPM_RANK_PINNED") == "1" else len(
+            rank_cpu_set(int(os.environ.get("LOCAL_RANK", "0")), lws))
+        if omp <= 1:
+            omp = 16
+        return max(1, min(omp, cap))
     return max(1, min(omp, n_aff))
 
 

@@ -57,15 +57,18 @@ def _worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_two_rank_sharding(tmp_path):
-    world = 2
+@pytest.mark.parametrize("world", [2, 8])
+def test_rank_sharding(tmp_path, world):
+    """World size 2 and 8 (the 8-GPU node's rank count): shard bounds cover every pair once in
+    rank order, the gathered per-rank Hungarian results equal the single-process ones, and the
+    max-over-ranks timing reduction."""
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     with open(os.path.join(tmp_path, "res.json")) as f:
         d = json.load(f)
     res, t = d["res"], d["t"]
-    assert t == [2.0, 10.0]
+    assert t == [float(world), 10.0]
     from fpm import ops
-    for cfg, total in (("c3", 12), ("c4", 13)):
+    for cfg, total in (("c3", 6 * world), ("c4", 13)):
         parts = sorted(res[cfg], key=lambda p: p[0])
         assert parts[0][0] == 0 and sum(p[1] for p in parts) == total
         assert all(a[0] + a[1] == b[0] for a, b in zip(parts, parts[1:]))
@@ -92,3 +95,36 @@ def test_host_cpu_share_under_torchrun(monkeypatch):
     assert host_cpu_share() == 1
     monkeypatch.setenv("FPM_CPU_SHARE", "3")
     assert host_cpu_share() == min(3, n_aff)
+
+
+def _cpu_worker(rank, world, port, out_dir):
+    """One torchrun-like rank: LOCAL_RANK / LOCAL_WORLD_SIZE set, OMP_NUM_THREADS=1 (the launcher's
+    default), pins itself (bench.py's pin_rank_cpus) and reports its CPU set and pool share."""
+    os.environ.update(LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world), OMP_NUM_THREADS="1")
+    for k in ("FPM_CPU_SHARE", "FPM_RANK_PINNED", "FPM_PIN_RANKS"):
+        os.environ.pop(k, None)
+    from fpm.model import host_cpu_share, pin_rank_cpus
+    before = host_cpu_share()
+    cpus = pin_rank_cpus()
+    after = host_cpu_share()
+    with open(os.path.join(out_dir, "cpu%d.json" % rank), "w") as f:
+        json.dump({"cpus": cpus, "mask": sorted(os.sched_getaffinity(0)), "before": before, "after": after}, f)
+
+
+def test_eight_rank_cpu_split(tmp_path):
+    """8 ranks on one node: every rank's host Hungarian pool gets its own non-empty slice of the
+    affinity mask (disjoint when the mask has >= 8 CPUs), and its pool share equals the slice (at
+    most 16 CPUs) before and after pinning."""
+    world = 8
+    mp.spawn(_cpu_worker, args=(world, 0, str(tmp_path)), nprocs=world, join=True)
+    n_aff = len(os.sched_getaffinity(0))
+    sets = []
+    for r in range(world):
+        with open(os.path.join(tmp_path, "cpu%d.json" % r)) as f:
+            d = json.load(f)
+        assert d["cpus"] and d["mask"] == sorted(d["cpus"])
+        assert d["before"] == d["after"] == min(16, len(d["cpus"])) >= 1
+        sets.append(set(d["cpus"]))
+    if n_aff >= world:
+        assert all(not (a & b) for i, a in enumerate(sets) for b in sets[i + 1:])
+        assert all(len(s) == n_aff // world for s in sets)
