@@ -206,6 +206,49 @@ def survey_flops_per_pair(n1, n2, E1, E2, d=768):
     return float(f)
 
 
+def exec_flops_per_pair(n1, n2, E1, E2, spline_rows, dtype, afau_mode="bf16x3", kp_x3=True, d=768):
+    """FLOPs the device kernels EXECUTE per pair (the deduplicated (node, cell) product rows measured by
+    fpm_profile_read, split-operand K where the bf16 mode runs near-fp32 products), by precision:
+    -> ({stage: flops}, seconds per pair at the peaks of the precisions used).  bf16 MFMA stages are
+    priced at 2.5 PF, everything else (fp32 MFMA / VALU) at 157.3 TF, so
+    exec_frac = pairs/s x that time is the fraction of the step the kernels would need at peak (<= 1)."""
+    N = n1 * n2
+    bf = dtype == "bf16"
+    x3 = bf and afau_mode == "bf16x3"
+    f_bf, f_32 = {}, {}
+    (f_bf if bf else f_32)["spline_product_gemm"] = 2.0 * spline_rows * d * d
+    f_32["spline_combine"] = 2.0 * 2 * (2 * (4 * E1 + n1) * d + 2 * (4 * E2 + n2) * d)
+    f_32["coef"] = 2.0 * 1024 * d
+    (f_bf if bf else f_32)["vertex_affinity"] = 2.0 * N * d * (3 if (bf and kp_x3) else 1)
+    f_32["gnn_layers"] = float(N * (640 + 2 * 2176) + (E1 * E2 + N) * (1 + 17 + 17))
+    f_32["sinkhorns"] = 5.0 * 70 * N + 2 * 17 * N
+    f_32["afau_attention"] = 16.0 * N * 99
+    k = 3 if x3 else 1
+    (f_bf if bf and afau_mode != "f32" else f_32)["afau_gemms"] = 2.0 * n1 * (256 * k * 600 + 640 * k * 256
+                                                                              + 256 * k * 600)
+    f_32["afau_norms"] = 2.0 * 20 * n1 * 600
+    f_32["soft_topk"] = 120.0 * N
+    f_32["match_classifier"] = 2.0 * (N * 144 + (N / 4) * 4608)
+    t = sum(f_bf.values()) / 2.5e15 + sum(f_32.values()) / 157.3e12
+    return {**f_bf, **f_32}, t, sum(f_bf.values()), sum(f_32.values())
+
+
+def profiled_spline_rows(net, bt, pairs):
+    """Product-GEMM rows per pair of one forward of ``bt`` (fpm_profile_read's FLOPs / 2 x 768^2)."""
+    import ctypes
+    import torch
+    from fpm import _lib
+    lib = _lib.load()
+    lib.fpm_profile_read(None, None, None)
+    lib.fpm_profile_enable(1)
+    net.run(bt)
+    torch.cuda.synchronize()
+    lib.fpm_profile_enable(0)
+    ms, fl, cnt = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+    _lib.call("fpm_profile_read", ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(cnt))
+    return fl.value / (2.0 * 768 * 768) / pairs
+
+
 def spline_flops_per_graph(n, E, d=768):
     return float(2 * 2 * (4 * E + n) * d * d)
 
@@ -259,6 +302,11 @@ def config_line(cfg, args, dev, sd, steps=5, warmup=2):
     else:
         f_pair = survey_flops_per_pair(n, n, E_pair, E_pair)
     peak = 2500.0 if dtype == "bf16" else 157.3
+    rows = profiled_spline_rows(net, bt, B)
+    if cfg == "c4":
+        ex, t_ex, ex_bf, ex_32 = exec_flops_per_pair(n, n, 0, E_pair, rows, dtype, net.afau_mode, net.kp_x3)
+    else:
+        ex, t_ex, ex_bf, ex_32 = exec_flops_per_pair(n, n, E_pair, E_pair, rows, dtype, net.afau_mode, net.kp_x3)
     # the device on the CPU sample against the fp32 oracle: the gate (ss / ds_mat / k_prob 1e-4) and
     # perm classes with their recorded assignment gaps
     sbt = (DeviceBatch.from_probe_gallery(sample[0][0], [p[1] for p in sample], dev) if cfg == "c4"
@@ -277,7 +325,12 @@ def config_line(cfg, args, dev, sd, steps=5, warmup=2):
             "ms_per_step": el / steps * 1e3, "gpu_stage_pairs_per_s": B * steps / g_s if g_s > 0 else None,
             "pairs_per_step": B, "n_keypoints": n, "edges_per_graph": E_pair,
             "afau_mode": net.afau_mode,
-            "forward_frac_8d": value * f_pair / (peak * 1e12),
+            # hardware fraction: executed FLOPs at the peaks of the precisions they run in (<= 1)
+            "exec_frac": value * t_ex, "exec_tflops": value * (ex_bf + ex_32) / 1e12,
+            "exec_flops_per_pair": {"bf16_mfma": ex_bf, "fp32": ex_32, "spline_rows_per_pair": rows},
+            # SURVEY §8(d)'s per-edge accounting: a rate in TFLOP/s, NOT a hardware fraction (the kernels
+            # compute deduplicated (node, cell) rows, ~2.5x fewer FLOPs than the per-edge form)
+            "rate_8d_tflops": value * f_pair / 1e12,
             "flops_per_pair_8d": f_pair, "peak_tflops": peak,
             "parity_gate": {"tolerance": 1e-4, "outputs": ["ss", "ds_mat", "k_prob"], "mode": dtype,
                             "passed": all(d[k] < 1e-4 for k in ("ss", "ds_mat", "k_prob"))
@@ -550,6 +603,11 @@ def main():
     value = pairs_total / elapsed
     peak = 2500.0 if args.dtype == "bf16" else 157.3
     achieved = (fl.value / (ms.value / 1e3)) / 1e12 if ms.value > 0 else 0.0
+    # executed FLOPs per pair from the profiled steps' product rows (bench.exec_flops_per_pair)
+    rows_pp = fl.value / (2.0 * 768 * 768) / max(pairs_total / world, 1)
+    Eg = E_tot / (2.0 * args.batch)
+    ex_f, ex_t, ex_bf, ex_32 = exec_flops_per_pair(args.n, args.n, 0 if args.config == "c4" else Eg, Eg, rows_pp,
+                                                   args.dtype, net.afau_mode, net.kp_x3)
 
     # the fp32 (parity) mode on the same C3 batch beside the bf16 headline
     f32_line = None
@@ -560,8 +618,11 @@ def main():
         k32 = max(1, min(args.steps, 3))
         e32, g32, _ = timed(net32, bt, k32, "f32")
         e32, g32 = reduce_max([e32, g32], world)
-        f32_line = {"value": args.batch * world * k32 / e32, "unit": "pairs/s", "dtype": "f32", "steps": k32,
-                    "ms_per_step": e32 / k32 * 1e3, "gpu_stage_pairs_per_s": args.batch * world * k32 / g32}
+        _, t32, b32, s32 = exec_flops_per_pair(args.n, args.n, Eg, Eg, rows_pp, "f32", "f32", False)
+        v32 = args.batch * world * k32 / e32
+        f32_line = {"value": v32, "unit": "pairs/s", "dtype": "f32", "steps": k32,
+                    "ms_per_step": e32 / k32 * 1e3, "gpu_stage_pairs_per_s": args.batch * world * k32 / g32,
+                    "exec_frac": v32 / world * t32, "exec_tflops": v32 * (b32 + s32) / 1e12}
         del net32
         torch.cuda.empty_cache()
 
@@ -631,6 +692,7 @@ def main():
             config_lines["train_line"] = train_line(args, dev)
             log("train line: %s" % json.dumps(config_lines["train_line"]))
         f8d = survey_flops_per_pair(args.n, args.n, E_tot / (2.0 * args.batch), E_tot / (2.0 * args.batch))
+
         res = {
             "metric": "graph-match pairs/sec @ n=256 kpts, batch=1024, 1 & 8 GPU",
             "value": value,
@@ -671,9 +733,15 @@ def main():
                          "algorithmic_flops_per_launch": fl.value / max(cnt.value, 1),
                          "isolated_achieved": (iso_fl.value / (iso_ms.value / 1e3)) / 1e12 if iso_ms.value > 0 else 0.0,
                          "isolated_avg_launch_ms": iso_ms.value / max(iso_cnt.value, 1),
-                         # SURVEY §8(d)'s whole-forward figure: pairs/s x algorithmic FLOPs per pair
-                         # (the reference's per-edge form, Ke excluded) / peak
-                         "forward_frac_8d": None if args.config == "c4" else value * f8d / (peak * 1e12),
+                         # the whole forward's hardware fraction: executed FLOPs (deduplicated product
+                         # rows from this run's profile, split-operand K) at the peaks of the precisions
+                         # they run in (bench.exec_flops_per_pair), <= 1
+                         "exec_frac": value / world * ex_t, "exec_tflops": value * (ex_bf + ex_32) / 1e12,
+                         "exec_flops_per_pair": {"bf16_mfma": ex_bf, "fp32": ex_32, "spline_rows_per_pair": rows_pp,
+                                                 "by_stage": ex_f},
+                         # SURVEY §8(d)'s per-edge accounting as a rate (TFLOP/s): NOT a hardware
+                         # fraction (the reference's per-edge form, ~2.5x the executed FLOPs)
+                         "rate_8d_tflops": None if args.config == "c4" else value * f8d / 1e12,
                          "flops_per_pair_8d": None if args.config == "c4" else f8d},
             "value_profiled": pairs_total / elapsed_prof,
             "cpu_baseline": cpu,

@@ -2,6 +2,7 @@
 // Used by: SplineConv root term, global-weight coefficient (affinity_layer.py:13), vertex
 // affinity Kp (affinity_layer.py:15-18), AFA-U projections/FFN (afau.py:99-103,188-199).
 #include "gemm_phase.h"
+#include "gemm_pp.h"
 #include <cstdlib>
 #include <cstring>
 
@@ -67,6 +68,15 @@ extern "C" int fpm_gemm(int dtype, const void* A, long lda, long sA, const int* 
 }
 
 namespace fpm {
+// FPM_GEMM_PP: the product GEMM on the two-workgroups-per-CU 256 x 128 kernel (gemm_pp.h)
+int& gemm_pp_flag() {
+    static int on = [] {
+        const char* e = getenv("FPM_GEMM_PP");
+        return e ? atoi(e) : 0;
+    }();
+    return on;
+}
+
 int& gemm_phase_flag() {
     static int on = [] {
         const char* e = getenv("FPM_GEMM_PHASE");
@@ -238,6 +248,7 @@ int& afau_head_split_flag();
 extern "C" int fpm_set_tuning(const char* key, int value) {
     int* f = nullptr;
     if (key && !strcmp(key, "gemm_phase")) f = &fpm::gemm_phase_flag();
+    else if (key && !strcmp(key, "gemm_pp")) f = &fpm::gemm_pp_flag();
     else if (key && !strcmp(key, "plan_graph")) f = &plan_graph_flag();
     else if (key && !strcmp(key, "combine_npb")) f = &combine_npb_flag();
     else if (key && !strcmp(key, "sinkhorn_bwd_reg")) f = &sinkhorn_bwd_reg_flag();

@@ -982,22 +982,26 @@ Queue& queue() {
 extern "C" {
 
 // s: (B, n1max, n2max) host float32, row stride ld2 (>= n2max) and batch stride sb.
-// assign: (B, n1max) int32 output, -1 = unassigned row.  Returns 0, or the first failing pair+1.
+// assign: (B, n1max) int32 output, -1 = unassigned row.  Returns 0, or the lowest failing pair + 1
+// (an atomic min over the workers, as the asynchronous queue keeps it: the same pair is named whatever
+// the threads' timing or the FPM_LSA_X2 grouping).
 int fpm_lsa_batch_host(const float* s, long sb, long ld, const int* n1, const int* n2, int B, int n1max, int* assign,
                        int nthreads) {
     if (B <= 0) return 0;
     const int grp = lsa_group(), ntasks = (B + grp - 1) / grp;
     if (nthreads < 1) nthreads = 1;
     if (nthreads > ntasks) nthreads = ntasks;
-    std::atomic<int> fail(0);
+    std::atomic<int> fail(0);                     // 0 = none, else lowest failing pair + 1
     std::function<void(int)> work = [&](int t) {
         const int b = t * grp, b2 = grp == 2 && b + 1 < B ? b + 1 : -1;
         int rc[2];
         lsa_two(s, sb, ld, n1, n2, n1max, assign, b, b2, rc);
         for (int k = 0; k < 2; ++k)
             if (rc[k]) {
-                int expect = 0;
-                fail.compare_exchange_strong(expect, (k ? b2 : b) + 1);
+                const int mine = (k ? b2 : b) + 1;
+                int cur = fail.load();
+                while ((cur == 0 || mine < cur) && !fail.compare_exchange_weak(cur, mine)) {
+                }
             }
     };
     if (nthreads == 1) {

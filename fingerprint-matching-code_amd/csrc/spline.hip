@@ -14,6 +14,7 @@
 // per-edge GEMM, and the message tensor is never materialised.  The plan (dst CSR included) is
 // built on device once per side and shared by both layers and the GNN layers.
 #include "gemm_phase.h"
+#include "gemm_pp.h"
 
 #include <vector>
 
@@ -1292,7 +1293,9 @@ extern "C" int fpm_spline_conv_fwd_argmax(int dtype, const void* x_op, const voi
         p.store_sc1 = gemm_store_sc1_flag();
         p.remap_mtiles = (int)(dtype == 0 ? L.max_tiles : L.max_tiles2);
         if (dtype == 1) p.tile_info = (const int*)(w + L.tile_info2);
-        dim3 grid(dtype == 0 ? remap_grid(D, p.remap_mtiles) : remap_grid256(D, p.remap_mtiles), 1, 1);
+        const bool pp = dtype == 1 && use_gemm_pp(D);
+        dim3 grid(dtype == 0 ? remap_grid(D, p.remap_mtiles) : pp ? pp_grid(D, p.remap_mtiles)
+                                                                  : remap_grid256(D, p.remap_mtiles), 1, 1);
         ProfRec rec = {nullptr, nullptr, (int)g_prof.size()};
         if (g_prof_on && !g_prof_rows) (void)hipMalloc(&g_prof_rows, PROF_MAX * sizeof(int));
         if (g_prof_on && g_prof_rows && rec.slot < PROF_MAX) {
@@ -1303,6 +1306,7 @@ extern "C" int fpm_spline_conv_fwd_argmax(int dtype, const void* x_op, const voi
             (void)hipEventRecord(rec.a, st);
         }
         if (dtype == 0) hipLaunchKernelGGL((gemm_kernel<float, false>), grid, dim3(GTHREADS), 0, st, p);
+        else if (pp) hipLaunchKernelGGL((gemm_pp_kernel<EPI_STORE>), grid, dim3(PP_THREADS), 0, st, p);
         else if (use_gemm_phase(D)) hipLaunchKernelGGL((gemm_phase_kernel<EPI_STORE, false>), grid, dim3(G2_THREADS), 0, st, p);
         else hipLaunchKernelGGL((gemm_big_kernel<256, EPI_STORE, false>), grid, dim3(G2_THREADS), 0, st, p);
         if (g_prof_on && g_prof_rows && rec.slot < PROF_MAX) {

@@ -418,25 +418,54 @@ def affinity(X1, X2, w, A_w, A_b, n1, n2, half=False, out=None):
     return out
 
 
-def perm_loss_fwd(ds, gt, n1, n2, check_range=True):
+_RANGE = {"bad": None, "calls": 0}
+
+
+def _range_every():
+    import os
+    return int(os.environ.get("FPM_LOSS_CHECK_EVERY", "1"))
+
+
+def perm_loss_fwd(ds, gt, n1, n2, check_range=None):
     """PermutationLoss (src/loss_func.py:26-59) of device ds / gt (B, n1max, n2max views with unit
     column stride), n1 / n2 (B,) int32 device -> 0-d fp32 device tensor (fpm_perm_loss_fwd).  Each
-    pair's block is clamped to the padded box like the reference's slice.  ``check_range``: raise
-    like the reference's assert (loss_func.py:42-47) when a ds or gt entry of a valid block lies
-    outside [0, 1] or is NaN (one small device-to-host read)."""
+    pair's block is clamped to the padded box like the reference's slice.
+
+    Range check (the reference asserts 0 <= x <= 1 on both tensors, loss_func.py:42-47): entries of
+    each pair's VALID block outside [0, 1] or NaN raise FpmError (the padding, which the reference's
+    assert also covers, is not read: the device ds_mat is 0 there by construction).  The reference's
+    assert reads the device on every call; here ``check_range`` (None: FPM_LOSS_CHECK_EVERY, default
+    1) = 1 does the same, N > 1 accumulates the per-pair flags on the device and reads them every N-th
+    call (the error names the calls since the last read), 0 / False skips the check."""
     _dev(ds, gt, n1, n2)
     B, n1max, n2max = ds.shape
     if ds.stride(2) != 1 or gt.stride(2) != 1 or tuple(gt.shape) != tuple(ds.shape):
         raise _lib.FpmError("perm_loss: ds / gt (B, n1max, n2max) with unit column stride expected")
+    every = _range_every() if check_range is None else int(check_range)
     ws = torch.empty(B, device=ds.device, dtype=torch.float32)
-    bad = torch.zeros(B, device=ds.device, dtype=torch.int32) if check_range else None
+    bad = torch.zeros(B, device=ds.device, dtype=torch.int32) if every > 0 else None
     out = torch.empty((), device=ds.device, dtype=torch.float32)
     _lib.call("fpm_perm_loss_fwd", _p(ds), ds.stride(0), ds.stride(1), _p(gt), gt.stride(0), gt.stride(1), _p(n1), _p(n2),
               B, n1max, n2max, _p(ws), _p(bad), _p(out), _stream(ds))
-    if check_range and int(bad.sum()):
-        pairs = bad.nonzero().view(-1).tolist()
-        raise _lib.FpmError("perm_loss: ds_mat / gt_perm_mat entries outside [0, 1] (or NaN) in pair(s) %s "
-                            "(the reference asserts 0 <= x <= 1, loss_func.py:42-47)" % pairs[:8])
+    if every <= 0:
+        return out
+    if every == 1:
+        if int(bad.sum()):
+            pairs = bad.nonzero().view(-1).tolist()
+            raise _lib.FpmError("perm_loss: ds_mat / gt_perm_mat entries outside [0, 1] (or NaN) in pair(s) %s "
+                                "(the reference asserts 0 <= x <= 1, loss_func.py:42-47)" % pairs[:8])
+        return out
+    acc = _RANGE["bad"]
+    tot = bad.sum()
+    _RANGE["bad"] = tot if acc is None or acc.device != tot.device else acc + tot
+    _RANGE["calls"] += 1
+    if _RANGE["calls"] >= every:
+        n, calls = int(_RANGE["bad"]), _RANGE["calls"]
+        _RANGE["bad"], _RANGE["calls"] = None, 0
+        if n:
+            raise _lib.FpmError("perm_loss: %d pair(s) with ds_mat / gt_perm_mat entries outside [0, 1] (or NaN) "
+                                "in the last %d loss calls (the reference asserts 0 <= x <= 1, "
+                                "loss_func.py:42-47)" % (n, calls))
     return out
 
 

@@ -843,3 +843,11 @@ def test_perm_loss_kernel_clamps_sizes_and_checks_range():
     d2 = ds.clone()
     d2[2, 6, 6] = 7.0                       # outside pair 2's 4 x 7 block: ignored
     ops.perm_loss_fwd(d2, gt, clamped, n2c)
+    # check_range = N accumulates the flags on the device and reads them every N-th call
+    d2 = ds.clone()
+    d2[0, 0, 0] = 2.0
+    ops.perm_loss_fwd(d2, gt, clamped, n2c, check_range=3)
+    ops.perm_loss_fwd(ds, gt, clamped, n2c, check_range=3)
+    with pytest.raises(FpmError, match="1 pair"):
+        ops.perm_loss_fwd(ds, gt, clamped, n2c, check_range=3)
+    ops.perm_loss_fwd(d2, gt, clamped, n2c, check_range=0)      # off

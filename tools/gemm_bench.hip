@@ -3,6 +3,7 @@
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I fingerprint-matching-code_amd/csrc tools/gemm_bench.hip
 // (-DGP_PROBE: also the phase kernel's per-workgroup phase split from shader-clock stamps)
 #include "gemm_phase.h"
+#include "gemm_pp.h"
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -11,6 +12,7 @@
 #include <cstring>
 
 namespace fpm {
+int& gemm_pp_flag() { static int v = 1; return v; }
 void set_error(const char*, ...) {}
 int check_launch(const char*) { return 0; }
 }
@@ -136,10 +138,11 @@ int main(int argc, char** argv) {
     };
     auto t128 = table(128), t256 = table(256);
     printf("rows %d  tiles128 %zu tiles256 %zu\n", rows, t128.size() / 2, t256.size() / 2);
-    uint16_t *dx, *dw, *c1, *c2, *c3;
+    uint16_t *dx, *dw, *c1, *c2, *c3, *c4;
     int *darows, *dgoff, *dt128, *dt256;
     CK(hipMalloc(&dx, hx.size() * 2)); CK(hipMalloc(&dw, hw.size() * 2));
     CK(hipMalloc(&c1, (size_t)rows * D * 2)); CK(hipMalloc(&c2, (size_t)rows * D * 2)); CK(hipMalloc(&c3, (size_t)rows * D * 2));
+    CK(hipMalloc(&c4, (size_t)rows * D * 2));
     CK(hipMalloc(&darows, arows.size() * 4)); CK(hipMalloc(&dgoff, goff.size() * 4));
     CK(hipMalloc(&dt128, t128.size() * 4)); CK(hipMalloc(&dt256, t256.size() * 4));
     CK(hipMemcpy(dx, hx.data(), hx.size() * 2, hipMemcpyHostToDevice));
@@ -155,35 +158,38 @@ int main(int argc, char** argv) {
     p1.tile_info = dt128; p1.Ct = c1; p1.remap_mtiles = (int)t128.size() / 2;
     p2.tile_info = dt256; p2.Ct = c2; p2.remap_mtiles = (int)t256.size() / 2;
     p3 = p2; p3.Ct = c3;
-    dim3 g1(remap_grid(D, p1.remap_mtiles)), g2(remap_grid256(D, p2.remap_mtiles));
+    GemmParams p4 = p2; p4.Ct = c4;
+    dim3 g1(remap_grid(D, p1.remap_mtiles)), g2(remap_grid256(D, p2.remap_mtiles)), g4(pp_grid(D, p4.remap_mtiles));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     const double flops = 2.0 * rows * (double)D * D;
     const int reps = 20;
     for (int round = 0; round < 3; ++round) {
-        for (int v = 0; v < 3; ++v) {
+        for (int v = 0; v < 4; ++v) {
             CK(hipEventRecord(e0));
             for (int r = 0; r < reps; ++r) {
                 if (v == 0) hipLaunchKernelGGL((gemm_kernel<bf16_t, false>), g1, dim3(GTHREADS), 0, 0, p1);
                 else if (v == 1) hipLaunchKernelGGL((gemm_big_kernel<256, EPI_STORE, false>), g2, dim3(G2_THREADS), 0, 0, p2);
-                else hipLaunchKernelGGL((gemm_phase_kernel<EPI_STORE, false>), g2, dim3(G2_THREADS), 0, 0, p3);
+                else if (v == 2) hipLaunchKernelGGL((gemm_phase_kernel<EPI_STORE, false>), g2, dim3(G2_THREADS), 0, 0, p3);
+                else hipLaunchKernelGGL((gemm_pp_kernel<EPI_STORE>), g4, dim3(PP_THREADS), 0, 0, p4);
             }
             CK(hipEventRecord(e1));
             CK(hipEventSynchronize(e1));
             float ms; CK(hipEventElapsedTime(&ms, e0, e1));
             ms /= reps;
-            printf("round %d %-10s %.4f ms  %.1f TF/s\n", round, v == 2 ? "phase256" : v ? "256x256" : "128x128", ms, flops / ms / 1e9);
+            printf("round %d %-10s %.4f ms  %.1f TF/s\n", round, v == 3 ? "pp256x128" : v == 2 ? "phase256" : v ? "256x256" : "128x128", ms, flops / ms / 1e9);
         }
     }
 #ifdef GP_PROBE
     for (int r = 0; r < 3; ++r) probe_report(p3, g2);
 #endif
-    std::vector<uint16_t> h1((size_t)rows * D), h2((size_t)rows * D), h3((size_t)rows * D);
+    std::vector<uint16_t> h1((size_t)rows * D), h2((size_t)rows * D), h3((size_t)rows * D), h4((size_t)rows * D);
     CK(hipMemcpy(h1.data(), c1, h1.size() * 2, hipMemcpyDeviceToHost));
     CK(hipMemcpy(h2.data(), c2, h2.size() * 2, hipMemcpyDeviceToHost));
     CK(hipMemcpy(h3.data(), c3, h3.size() * 2, hipMemcpyDeviceToHost));
-    size_t diff = 0, diff3 = 0;
-    for (size_t i = 0; i < h1.size(); ++i) { diff += h1[i] != h2[i]; diff3 += h3[i] != h2[i]; }
-    printf("mismatching elements 128 vs 256: %zu, phase vs 256: %zu of %zu\n", diff, diff3, h1.size());
-    return diff != 0 || diff3 != 0;
+    CK(hipMemcpy(h4.data(), c4, h4.size() * 2, hipMemcpyDeviceToHost));
+    size_t diff = 0, diff3 = 0, diff4 = 0;
+    for (size_t i = 0; i < h1.size(); ++i) { diff += h1[i] != h2[i]; diff3 += h3[i] != h2[i]; diff4 += h4[i] != h2[i]; }
+    printf("mismatching elements 128 vs 256: %zu, phase vs 256: %zu, pp vs 256: %zu of %zu\n", diff, diff3, diff4, h1.size());
+    return diff != 0 || diff3 != 0 || diff4 != 0;
 }
