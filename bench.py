@@ -656,7 +656,7 @@ def main():
     # WRITE_SIZE, separate passes; tools/pmc_gemm.sh -> profiles/r01_pmc_product_gemm.json)
     traffic = None
     pdir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
-    pmc_name = next((f for f in ("r05zz2_pmc_product_gemm.json", "r05z2_pmc_product_gemm.json", "r04v_pmc_product_gemm.json", "r04_pmc_product_gemm.json", "r03_pmc_product_gemm.json", "r02_pmc_product_gemm.json",
+    pmc_name = next((f for f in ("r06_pmc_product_gemm.json", "r05zz2_pmc_product_gemm.json", "r05z2_pmc_product_gemm.json", "r04v_pmc_product_gemm.json", "r04_pmc_product_gemm.json", "r03_pmc_product_gemm.json", "r02_pmc_product_gemm.json",
                                          "r01_pmc_product_gemm.json")
                      if os.path.exists(os.path.join(pdir, f))), None)
     if args.dtype == "bf16" and args.config == "c3" and pmc_name:

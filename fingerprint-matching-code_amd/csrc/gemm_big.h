@@ -46,8 +46,8 @@ template <int BN> struct G2Cfg {
     static constexpr int SMEM = g2_max(NST * STAGE, g2_max(G2_BM * (2 * BN + 16), 128 * (4 * BN + 16)));
 };
 
-inline unsigned remap_grid_big(int N, int BN, int mtiles) {
-    long nt = (N + BN - 1) / BN, chunk = 4 * nt;
+inline unsigned remap_grid_big(int N, int BN, int mtiles, int cm = 4) {
+    long nt = (N + BN - 1) / BN, chunk = (long)cm * nt;
     long t = nt * mtiles;
     if (mtiles < REMAP_MIN) return (unsigned)t;
     return (unsigned)((t + 8 * chunk - 1) / (8 * chunk) * (8 * chunk));

@@ -60,6 +60,7 @@ struct GemmParams {
                              // [hi | lo | hi] with segment stride split (ops.split_bf16x3 layout)
     int store_sc1;           // bf16 output tiles of the phase kernel: sc1 stores (the lines leave
                              // the XCD's L2 instead of evicting the gathered A rows)
+    int remap_cm;            // phase kernel: row tiles per XCD chunk of the tile order (0 = 4)
 };
 
 // 1-D grid for the XCD-aware tile order: padded to whole rounds of 8 chunks so the remap is a
@@ -73,9 +74,9 @@ inline unsigned remap_grid(int N, int mtiles) {
     if (mtiles < REMAP_MIN) return (unsigned)t;
     return (unsigned)((t + 8 * chunk - 1) / (8 * chunk) * (8 * chunk));
 }
-__device__ __forceinline__ int remap_tile(int nt, int mtiles) {
+__device__ __forceinline__ int remap_tile(int nt, int mtiles, int cm = 4) {
     if (mtiles < REMAP_MIN) return blockIdx.x;
-    const int chunk = 4 * nt;
+    const int chunk = cm * nt;
     const int i = blockIdx.x >> 3;
     return ((i / chunk) * 8 + (blockIdx.x & 7)) * chunk + (i % chunk);
 }

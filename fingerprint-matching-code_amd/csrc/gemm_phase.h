@@ -59,7 +59,10 @@ __device__ unsigned long long* gp_probe_buf;
 #ifndef GP_PRIO
 #define GP_PRIO 1
 #endif
-template <int EPI, bool F32OUT>
+// DIRECT (bf16 output): the MFMAs run with swapped operands (weights as the first), so each lane's
+// accumulator holds 4 consecutive OUTPUT COLUMNS of one row, and the epilogue stores them straight
+// from registers (8 B per lane, no LDS image, no barrier)
+template <int EPI, bool F32OUT, bool DIRECT = false>
 __global__ __launch_bounds__(G2_THREADS, 1) void gemm_phase_kernel(GemmParams p) {
     constexpr int BN = 256;
     __shared__ __attribute__((aligned(16))) unsigned char smem[GP_SMEM];
@@ -68,7 +71,7 @@ __global__ __launch_bounds__(G2_THREADS, 1) void gemm_phase_kernel(GemmParams p)
     const int batch = blockIdx.z;
 
     const int nt = (p.N + BN - 1) / BN;
-    const int q = remap_tile(nt, p.remap_mtiles);
+    const int q = remap_tile(nt, p.remap_mtiles, p.remap_cm > 0 ? p.remap_cm : 4);
     const int mtile = q / nt, ntile = q - mtile * nt;
     if (mtile >= p.remap_mtiles) return;
     int group = 0, row0, row_end;
@@ -154,8 +157,12 @@ __global__ __launch_bounds__(G2_THREADS, 1) void gemm_phase_kernel(GemmParams p)
 #pragma unroll
             for (int fm = 0; fm < 4; ++fm)
 #pragma unroll
-                for (int fn = 0; fn < 2; ++fn)
-                    c[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kk][fm], bb[kk][fn], c[fm][fn], 0, 0, 0);
+                for (int fn = 0; fn < 2; ++fn) {
+                    if constexpr (DIRECT)
+                        c[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[kk][fn], a[kk][fm], c[fm][fn], 0, 0, 0);
+                    else
+                        c[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kk][fm], bb[kk][fn], c[fm][fn], 0, 0, 0);
+                }
         if (GP_PRIO) __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_s_barrier();
     };
@@ -227,6 +234,33 @@ __global__ __launch_bounds__(G2_THREADS, 1) void gemm_phase_kernel(GemmParams p)
     // epilogue through LDS (same images as gemm_big_kernel<256>)
     int n1b = 0, n2b = 0;
     if (EPI == EPI_AFFINITY) { n1b = p.n1[batch]; n2b = p.n2[batch]; }
+    if constexpr (DIRECT) {
+        static_assert(!F32OUT && EPI == EPI_STORE, "DIRECT: bf16 output, plain store");
+        // lane: output row  h*128 + wr*64 + fm*16 + (lane & 15), columns g*128 + wc*32 + fn*16 + 4*(lane >> 4) + [0, 4)
+        bf16_t* Ct = (bf16_t*)p.Ct + (long)batch * p.sC;
+        const int cl = wc * 32 + 4 * (lane >> 4);
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int fm = 0; fm < 4; ++fm) {
+                const int r = row0 + h * 128 + wr * 64 + fm * 16 + (lane & 15);
+                if (r >= row_end) continue;
+                bf16_t* rowp = Ct + (long)r * p.ldc + n0;
+#pragma unroll
+                for (int g = 0; g < 2; ++g)
+#pragma unroll
+                    for (int fn = 0; fn < 2; ++fn) {
+                        const int c = g * 128 + cl + fn * 16;
+                        if (n0 + c >= p.N) continue;
+                        const f32x4_t v = acc[h][g][fm][fn];
+                        uint2 o;
+                        o.x = f2bf2(v[0], v[1]);
+                        o.y = f2bf2(v[2], v[3]);
+                        *(uint2*)(rowp + c) = o;
+                    }
+            }
+        return;
+    }
     if (!F32OUT) {
         constexpr int ROW = BN * 2 + 16;
         // the bias test hoisted out of the image loop (a compile-time branch each; g2_epi)

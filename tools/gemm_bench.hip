@@ -159,27 +159,44 @@ int main(int argc, char** argv) {
     p2.tile_info = dt256; p2.Ct = c2; p2.remap_mtiles = (int)t256.size() / 2;
     p3 = p2; p3.Ct = c3;
     GemmParams p4 = p2; p4.Ct = c4;
+    uint16_t* c5;
+    CK(hipMalloc(&c5, (size_t)rows * D * 2));
+    GemmParams p5 = p2; p5.Ct = c5;
     dim3 g1(remap_grid(D, p1.remap_mtiles)), g2(remap_grid256(D, p2.remap_mtiles)), g4(pp_grid(D, p4.remap_mtiles));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     const double flops = 2.0 * rows * (double)D * D;
     const int reps = 20;
     for (int round = 0; round < 3; ++round) {
-        for (int v = 0; v < 4; ++v) {
+        for (int v = 0; v < 5; ++v) {
             CK(hipEventRecord(e0));
             for (int r = 0; r < reps; ++r) {
                 if (v == 0) hipLaunchKernelGGL((gemm_kernel<bf16_t, false>), g1, dim3(GTHREADS), 0, 0, p1);
                 else if (v == 1) hipLaunchKernelGGL((gemm_big_kernel<256, EPI_STORE, false>), g2, dim3(G2_THREADS), 0, 0, p2);
                 else if (v == 2) hipLaunchKernelGGL((gemm_phase_kernel<EPI_STORE, false>), g2, dim3(G2_THREADS), 0, 0, p3);
-                else hipLaunchKernelGGL((gemm_pp_kernel<EPI_STORE>), g4, dim3(PP_THREADS), 0, 0, p4);
+                else if (v == 3) hipLaunchKernelGGL((gemm_pp_kernel<EPI_STORE>), g4, dim3(PP_THREADS), 0, 0, p4);
+                else hipLaunchKernelGGL((gemm_phase_kernel<EPI_STORE, false, true>), g2, dim3(G2_THREADS), 0, 0, p5);
             }
             CK(hipEventRecord(e1));
             CK(hipEventSynchronize(e1));
             float ms; CK(hipEventElapsedTime(&ms, e0, e1));
             ms /= reps;
-            printf("round %d %-10s %.4f ms  %.1f TF/s\n", round, v == 3 ? "pp256x128" : v == 2 ? "phase256" : v ? "256x256" : "128x128", ms, flops / ms / 1e9);
+            printf("round %d %-10s %.4f ms  %.1f TF/s\n", round, v == 4 ? "direct256" : v == 3 ? "pp256x128" : v == 2 ? "phase256" : v ? "256x256" : "128x128", ms, flops / ms / 1e9);
         }
     }
+    // tile order: row tiles per XCD chunk (remap_cm), phase kernel
+    for (int round = 0; round < 2; ++round)
+        for (int cm : {1, 2, 4, 8, 16}) {
+            GemmParams pc = p3; pc.remap_cm = cm;
+            dim3 gc(remap_grid_big(D, 256, pc.remap_mtiles, cm));
+            CK(hipEventRecord(e0));
+            for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((gemm_phase_kernel<EPI_STORE, false>), gc, dim3(G2_THREADS), 0, 0, pc);
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+            ms /= reps;
+            printf("round %d phase256 chunk %2d m-tiles %.4f ms  %.1f TF/s\n", round, cm, ms, flops / ms / 1e9);
+        }
 #ifdef GP_PROBE
     for (int r = 0; r < 3; ++r) probe_report(p3, g2);
 #endif
@@ -188,8 +205,13 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(h2.data(), c2, h2.size() * 2, hipMemcpyDeviceToHost));
     CK(hipMemcpy(h3.data(), c3, h3.size() * 2, hipMemcpyDeviceToHost));
     CK(hipMemcpy(h4.data(), c4, h4.size() * 2, hipMemcpyDeviceToHost));
-    size_t diff = 0, diff3 = 0, diff4 = 0;
-    for (size_t i = 0; i < h1.size(); ++i) { diff += h1[i] != h2[i]; diff3 += h3[i] != h2[i]; diff4 += h4[i] != h2[i]; }
-    printf("mismatching elements 128 vs 256: %zu, phase vs 256: %zu, pp vs 256: %zu of %zu\n", diff, diff3, diff4, h1.size());
-    return diff != 0 || diff3 != 0 || diff4 != 0;
+    std::vector<uint16_t> h5((size_t)rows * D);
+    CK(hipMemcpy(h5.data(), c5, h5.size() * 2, hipMemcpyDeviceToHost));
+    size_t diff = 0, diff3 = 0, diff4 = 0, diff5 = 0;
+    for (size_t i = 0; i < h1.size(); ++i) {
+        diff += h1[i] != h2[i]; diff3 += h3[i] != h2[i]; diff4 += h4[i] != h2[i]; diff5 += h5[i] != h2[i];
+    }
+    printf("mismatching elements 128 vs 256: %zu, phase vs 256: %zu, pp vs 256: %zu, direct vs 256: %zu of %zu\n",
+           diff, diff3, diff4, diff5, h1.size());
+    return diff != 0 || diff3 != 0 || diff4 != 0 || diff5 != 0;
 }
