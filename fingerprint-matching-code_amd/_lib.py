@@ -109,6 +109,7 @@ SIGNATURES = {
     "fpm_gemm_f64": (I, [P, I, P, I, P, P, I, I, I, I, I, P]),
     "fpm_instnorm_f64": (I, [P, P, I, I, I, P, P, P, P, ctypes.c_double, P, P, P]),
     "fpm_afau_head_f64": (I, [P, P, P, I, I, P, P, P, P, P, P, P, P, P, P]),
+    "fpm_soft_topk_fwd_f64": (I, [P, L, L, P, P, P, I, I, I, I, ctypes.c_double, P, L, P, L, L, P, P, L, L, P]),
     "fpm_profile_enable": (I, [I]),
     "fpm_profile_enabled": (I, []),
     "fpm_profile_read": (I, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),

@@ -21,6 +21,7 @@
 //   gemm_f64_kernel        C = act(A W^T + bias): the AFA-U projections / FFN
 //   instnorm_f64_kernel    AddAndInstanceNormalization (+ max over positions)
 //   afau_head_f64_kernel   final_row / final_col + sigmoid(mean) (ngm.py:401-412)
+//   soft_topk_f64_kernel   soft top-k's 2-column Sinkhorn incl. the while loop -> ds_mat (fp32 out)
 #include "fpm_common.h"
 
 namespace {
@@ -355,7 +356,125 @@ __global__ __launch_bounds__(64) void afau_head_f64_kernel(const double* __restr
     ks[b] = (float)(1.0 / (1.0 + exp(-lg)));
 }
 
+// soft_topk + Sinkhorn_m.forward_log (soft_topk.py:8-53, 166-255, batched_operation=False) in fp64:
+// per pair the valid block's entries x_e (row-major, N = n1 n2) against the anchors [min, max] of the
+// block, L[e][c] = -|x_e - anchor_c| / tau; alternately L -= logsumexp over the 2 columns (+ log 1,
+// the row marginal) and L -= logsumexp over the N rows + log [N - k, k]; NaN -> -inf; ``iters`` steps,
+// then further steps while any L > 0 (the reference's while loop; capped at PK_MAX_STEPS so every
+// wave reaches the exit); ds[i][j] = exp(L[i n2 + j][1]) on the block, 0 elsewhere.  One workgroup
+// per pair, L in a global fp64 scratch (2 N doubles per pair, L2-resident), block reductions.
+constexpr int PK_MAX_STEPS = 100000;
+
+// op 0: sum, 1: max, 2: min; every thread gets the result (fixed order: wave butterfly, then waves
+// in order)
+__device__ __forceinline__ double block_reduce(double v, int op, double* red) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int o = 32; o > 0; o >>= 1) {
+        const double y = __shfl_xor(v, o);
+        v = op == 0 ? v + y : op == 1 ? fmax(v, y) : fmin(v, y);
+    }
+    __syncthreads();
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    double r = red[0];
+    for (int k = 1; k < (int)(blockDim.x >> 6); ++k) r = op == 0 ? r + red[k] : op == 1 ? fmax(r, red[k]) : fmin(r, red[k]);
+    return r;
+}
+
+__global__ __launch_bounds__(256) void soft_topk_f64_kernel(const double* __restrict__ ss, long s_sb, long s_ld,
+                                                            const int* __restrict__ n1, const int* __restrict__ n2,
+                                                            const float* __restrict__ kk, int n1max, int n2max,
+                                                            int iters, double tau, double* __restrict__ ws,
+                                                            float* __restrict__ out, long o_sb, long o_ld,
+                                                            int* __restrict__ steps_out, float* __restrict__ out2,
+                                                            long o2_sb, long o2_ld) {
+    __shared__ double red[4];
+    const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+    const int r = n1[b], c = n2[b];
+    const long N = (long)r * c;
+    const double NEG = -__builtin_inf();
+    const double* sb = ss + (long)b * s_sb;
+    double* L = ws + (long)b * 2 * n1max * n2max;
+    int st = 0;
+    if (N > 0) {
+        double mn = __builtin_inf(), mx = NEG;
+        for (long e = tid; e < N; e += nt) {
+            const double v = sb[(e / c) * s_ld + e % c];
+            mn = fmin(mn, v);
+            mx = fmax(mx, v);
+        }
+        mn = block_reduce(mn, 2, red);
+        mx = block_reduce(mx, 1, red);
+        for (long e = tid; e < N; e += nt) {
+            const double v = sb[(e / c) * s_ld + e % c];
+            L[2 * e] = -fabs(v - mn) / tau;
+            L[2 * e + 1] = -fabs(v - mx) / tau;
+        }
+        const double k = (double)kk[b];
+        const double lcp[2] = {log((double)N - k), log(k)};
+        auto fix = [&](double y) { return y != y ? NEG : y; };
+        auto step = [&](int i) {
+            __syncthreads();
+            if ((i & 1) == 0) {
+                for (long e = tid; e < N; e += nt) {
+                    const double a = L[2 * e], q = L[2 * e + 1];
+                    const double m = fmax(a, q);
+                    const double lse = m == NEG ? NEG : m + log(exp(a - m) + exp(q - m));
+                    L[2 * e] = fix(a - lse + 0.0);
+                    L[2 * e + 1] = fix(q - lse + 0.0);
+                }
+            } else {
+                double lse[2];
+                for (int cc = 0; cc < 2; ++cc) {
+                    double m = NEG;
+                    for (long e = tid; e < N; e += nt) m = fmax(m, L[2 * e + cc]);
+                    m = block_reduce(m, 1, red);
+                    double sum = 0.0;
+                    if (m != NEG)
+                        for (long e = tid; e < N; e += nt) sum += exp(L[2 * e + cc] - m);
+                    sum = block_reduce(sum, 0, red);
+                    lse[cc] = m == NEG ? NEG : m + log(sum);
+                }
+                for (long e = tid; e < N; e += nt) {
+                    L[2 * e] = fix(L[2 * e] - lse[0] + lcp[0]);
+                    L[2 * e + 1] = fix(L[2 * e + 1] - lse[1] + lcp[1]);
+                }
+            }
+        };
+        for (; st < iters; ++st) step(st);
+        for (;;) {
+            __syncthreads();
+            double pos = 0.0;
+            for (long e = tid; e < 2 * N; e += nt) pos = fmax(pos, L[e] > 0.0 ? 1.0 : 0.0);
+            pos = block_reduce(pos, 1, red);
+            if (pos == 0.0 || st >= PK_MAX_STEPS) break;
+            step(st);
+            ++st;
+        }
+        __syncthreads();
+    }
+    for (long q = tid; q < (long)n1max * n2max; q += nt) {
+        const int i = (int)(q / n2max), j = (int)(q % n2max);
+        const float v = (i < r && j < c) ? (float)exp(L[2 * ((long)i * c + j) + 1]) : 0.f;
+        out[(long)b * o_sb + (long)i * o_ld + j] = v;
+        if (out2) out2[(long)b * o2_sb + (long)i * o2_ld + j] = v;
+    }
+    if (steps_out && tid == 0) steps_out[b] = st;
+}
+
 }  // namespace
+
+extern "C" int fpm_soft_topk_fwd_f64(const double* ss, long s_sb, long s_ld, const int* n1, const int* n2,
+                                     const float* k, int B, int n1max, int n2max, int iters, double tau, double* ws,
+                                     long ws_doubles, float* out, long o_sb, long o_ld, int* steps_out, float* out2,
+                                     long o2_sb, long o2_ld, void* stream) {
+    if (B == 0) return 0;
+    FPM_CHECK_ARG(n1max > 0 && n2max > 0 && iters >= 0 && tau > 0.0, "soft_topk_f64: bad sizes / iters / tau");
+    FPM_CHECK_ARG(ws_doubles >= 2L * B * n1max * n2max, "soft_topk_f64: workspace of 2 B n1max n2max doubles needed");
+    hipLaunchKernelGGL(soft_topk_f64_kernel, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, ss, s_sb, s_ld, n1, n2,
+                       k, n1max, n2max, iters, tau, ws, out, o_sb, o_ld, steps_out, out2, o2_sb, o2_ld);
+    return fpm::check_launch("fpm_soft_topk_fwd_f64");
+}
 
 extern "C" int fpm_kron_gnn_layer_fwd_f64(const void* X, int x_f64, int C, int B, int n1max, int n2max, const int* ptr1,
                                           const int* nbr1, const int* ptr2, const int* nbr2, const int* n1,

@@ -876,8 +876,14 @@ class Net(nn.Module):
             ks.copy_(gt_ks[b0:b1] / min_pt[b0:b1])
         self._mark("afau")
         k_used = gt_ks[b0:b1] if self.training else ks * min_pt[b0:b1]
-        ops.soft_topk_fwd(o["ss"][b0:b1], part.n1, part.n2, k_used.contiguous(), C.SK_ITER_NUM, self.tau,
-                          out=o["ds_mat"][b0:b1], steps=o["sk_steps"][b0:b1], out_host=host)
+        if "ss64" in o:
+            # the fp64 k chain carries on through the soft top-k (its tau = 0.01 2-column Sinkhorn
+            # amplifies ss's fp32 rounding on small boxes as the final Sinkhorn does)
+            ops.soft_topk_f64(o["ss64"][b0:b1], part.n1, part.n2, k_used.contiguous(), C.SK_ITER_NUM, self.tau,
+                              out=o["ds_mat"][b0:b1], steps=o["sk_steps"][b0:b1], out_host=host)
+        else:
+            ops.soft_topk_fwd(o["ss"][b0:b1], part.n1, part.n2, k_used.contiguous(), C.SK_ITER_NUM, self.tau,
+                              out=o["ds_mat"][b0:b1], steps=o["sk_steps"][b0:b1], out_host=host)
         o["_kk"][b0:b1].copy_(ks * min_pt[b0:b1])
         self._mark("soft_topk")
 

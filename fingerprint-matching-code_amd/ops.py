@@ -627,6 +627,31 @@ def afau_head_f64(gr, gc, cidx, B, E, r0w, r0b, r2w, r2b, c0w, c0b, c2w, c2b, ks
               _p(c0b), _p(c2w), _p(c2b), _p(ks), _stream(gr))
 
 
+def soft_topk_f64(ss, n1, n2, k, iters=10, tau=0.01, out=None, steps=None, out_host=None):
+    """soft_topk(..., return_prob=True)[1] in fp64 from the fp64 ss (unit column stride) -> ds_mat
+    fp32 (B, n1max, n2max); ``steps``: (B,) int32 steps taken incl. the while loop; ``out_host``: a
+    pinned host copy written by the kernel too."""
+    _dev(ss, n1, n2, k, out, steps)
+    _f64(ss)
+    B, n1max, n2max = ss.shape
+    if ss.stride(2) != 1:
+        raise _lib.FpmError("soft_topk_f64: ss rows with unit column stride expected")
+    if out is None:
+        out = torch.empty(B, n1max, n2max, device=ss.device, dtype=torch.float32)
+    _shape(out, (B, n1max, n2max), "soft_topk_f64 out")
+    for t, w in ((n1, "n1"), (n2, "n2"), (k, "k"), (steps, "steps")):
+        _shape(t, (B,), "soft_topk_f64 " + w)
+    if out.stride(2) != 1 or (out_host is not None and (out_host.is_cuda or not out_host.is_pinned()
+                                                       or tuple(out_host.shape) != (B, n1max, n2max))):
+        raise _lib.FpmError("soft_topk_f64: out with unit column stride, out_host pinned (B, n1max, n2max)")
+    ws = torch.empty(2 * B * n1max * n2max, device=ss.device, dtype=torch.float64)
+    _lib.call("fpm_soft_topk_fwd_f64", _p(ss), ss.stride(0), ss.stride(1), _p(n1), _p(n2), _p(k), B, n1max, n2max,
+              int(iters), float(tau), _p(ws), ws.numel(), _p(out), out.stride(0), out.stride(1), _p(steps),
+              _p(out_host), out_host.stride(0) if out_host is not None else 0,
+              out_host.stride(1) if out_host is not None else 0, _stream(ss))
+    return out
+
+
 def match_cls(s, perm, w1, b1, bn1_sc, bn1_sh, w2, b2, bn2_sc, bn2_sh, fcw, fcb, logits=None, prob=None, dtype=F32):
     _dev(s, perm)
     if not (s.is_contiguous() and perm.is_contiguous()):

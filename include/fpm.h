@@ -280,7 +280,10 @@ int fpm_afau_head(const float* gr, const float* gc, int B, int E, const float* r
  * fpm_instnorm_f64: AddAndInstanceNormalization (afau.py:154-176) over P positions; in1 (+ in2) or
  *   (in1 NULL) the col block's one-hot + onehot_bias; out and / or gmax (max over positions).
  * fpm_afau_head_f64: ks[b] = sigmoid((final_row(gr[b]) + final_col(gc[cidx[b]])) / 2) (ngm.py:401-412),
- *   cidx NULL = b; ks fp32. */
+ *   cidx NULL = b; ks fp32.
+ * fpm_soft_topk_fwd_f64: soft_topk (soft_topk.py:8-53, 166-255) incl. the while loop in fp64 from the
+ *   fp64 ss -> ds_mat fp32 (and an optional second, e.g. pinned host, copy); ws >= 2 B n1max n2max
+ *   doubles; steps_out (optional) = steps taken. */
 int fpm_kron_gnn_layer_fwd_f64(const void* X, int x_f64, int C, int B, int n1max, int n2max, const int* ptr1,
                                const int* nbr1, const int* ptr2, const int* nbr2, const int* n1, const int* n2,
                                const float* params, double* Xout, double* zbuf, void* stream);
@@ -301,6 +304,9 @@ int fpm_instnorm_f64(const double* in1, const double* in2, int B, int P, int Cn,
 int fpm_afau_head_f64(const double* gr, const double* gc, const int* cidx, int B, int E, const double* r0w,
                       const double* r0b, const double* r2w, const double* r2b, const double* c0w, const double* c0b,
                       const double* c2w, const double* c2b, float* ks, void* stream);
+int fpm_soft_topk_fwd_f64(const double* ss, long s_sb, long s_ld, const int* n1, const int* n2, const float* k, int B,
+                          int n1max, int n2max, int iters, double tau, double* ws, long ws_doubles, float* out,
+                          long o_sb, long o_ld, int* steps_out, float* out2, long o2_sb, long o2_ld, void* stream);
 
 /* ---- AFA-U backward (training, src/model/afau.py:54-300 through ks_loss, training_loop.py:60) ---
  * fpm_afau_head_bwd: ks = sigmoid((final_row(gr) + final_col(gc)) / 2) -> dgr, dgc (B x E) and

@@ -177,3 +177,56 @@ def test_k_f64_off_above_threshold(sd):
     r32 = O.forward(pairs, sd)
     for k in ("ss", "ds_mat", "k_prob"):
         assert float((res[k].cpu() - r32[k]).abs().max()) < 1e-4, k
+
+
+@pytest.mark.parametrize("k_f64", [64, 0])
+def test_forward_tiny_and_lopsided_pairs(sd, k_f64):
+    """Edge sizes the reference handles (build_graphs.py:77-100: fewer than 3 points -> fully
+    connected): a 1-keypoint graph (no edges: every SplineConv max over an empty in-edge set is 0,
+    torch_scatter's rule), 2- and 3-keypoint graphs, and lopsided pairs (1 x 5, 3 x 40, 40 x 3:
+    dummy rows, transposed Sinkhorns, k = round(ks * 1)).  Both k chains (fp64 on the 40-keypoint
+    box, and the fp32 chain with k_f64_nmax = 0) against the oracle: ss / k_prob / cls_prob within
+    1e-4 of the fp32 oracle, perm_mat identical or a proven tie class.  ds_mat is gated like the
+    image path's k (anchored at the fp64 oracle): on the 2- and 7-keypoint pairs the fp32 oracle's
+    own ds_mat sits 2.3e-4 / 1.1e-4 from its fp64 value (its ss 1.2e-5 from it: the tau = 0.01 soft
+    top-k amplifies), so per pair |ds_dev - ds_64| <= |ds_32 - ds_64| + 1e-4."""
+    pairs = synth.make_batch(5, 5, [1, 2, 3, 40, 7], n2=[5, 2, 40, 3, 7])
+    assert pairs[0][0]["edge_index"].shape[1] == 0 and pairs[1][0]["edge_index"].shape[1] == 2
+    res = _forward(pairs, sd, "f32", k_f64=k_f64)
+    ref = O.forward(pairs, sd)
+    r64 = O.forward(pairs, sd, dtype=torch.float64)
+    for k in ("ss", "k_prob", "cls_prob"):
+        assert float((res[k].cpu() - ref[k]).abs().max()) < 1e-4, k
+    for b in range(len(pairs)):
+        d_dev = float((res["ds_mat"][b].cpu().double() - r64["ds_mat"][b]).abs().max())
+        d_ref = float((ref["ds_mat"][b].double() - r64["ds_mat"][b]).abs().max())
+        print("pair %d ds_mat: device %.2e, fp32 oracle %.2e from fp64" % (b, d_dev, d_ref))
+        assert d_dev <= d_ref + 1e-4, (b, d_dev, d_ref)
+    rep = O.compare.perm_report(res, ref, [p[0]["n"] for p in pairs], [p[1]["n"] for p in pairs])
+    assert rep["counts"]["mismatch"] == 0, rep
+    if k_f64:
+        assert float((res["k_prob"].cpu().double() - r64["k_prob"]).abs().max()) < 2e-5
+
+
+@pytest.mark.parametrize("n1s,n2s,kfrac", [
+    ((8, 8, 8), (8, 8, 8), (0.5, 0.2, 0.9)),
+    ((32, 20, 32), (32, 32, 17), (0.55, 0.7, 0.35)),
+    ((64, 41), (50, 64), (0.61, 0.48)),
+])
+def test_soft_topk_f64_vs_oracle(n1s, n2s, kfrac):
+    """soft top-k in fp64 (csrc/precise.hip; the 2-column Sinkhorn_m incl. its while loop) against
+    ngm_oracle.soft_topk in float64 on the same fp64 ss: within 1e-6 (the fp32 cast of an fp64
+    evaluation); the padding zero; the pinned host copy identical."""
+    g = torch.Generator().manual_seed(sum(n1s) + 3)
+    B, n1max, n2max = len(n1s), max(n1s), max(n2s)
+    s = torch.randn(B, n1max, n2max, generator=g, dtype=torch.float64) * 0.02
+    ss = O.pygm_sinkhorn(s, n1s, n2s, dummy_row=True, max_iter=10, tau=0.01)
+    k = torch.tensor([f * min(a, b) for f, a, b in zip(kfrac, n1s, n2s)], dtype=torch.float32)
+    ref = O.soft_topk(ss, k.double(), list(n1s), list(n2s))
+    steps = torch.zeros(B, dtype=torch.int32, device=DEV)
+    host = torch.zeros(B, n1max, n2max).pin_memory()
+    out = ops.soft_topk_f64(ss.to(DEV), _i32(n1s), _i32(n2s), k.to(DEV), 10, 0.01, steps=steps, out_host=host)
+    torch.cuda.synchronize()
+    assert float((out.cpu().double() - ref).abs().max()) < 1e-6
+    assert torch.equal(host, out.cpu())
+    assert int(steps.min()) >= 10
