@@ -28,6 +28,7 @@ struct SinkArgs {
     int dummy_row;
     int contig_j;  // 1: j (column) is the unit-stride dimension of in/out
     int fast;      // shifted single-pass lse after the first step (sinkhorn_reg_kernel)
+    int rw;        // streaming kernel: rows per wave in the row step's fast path (> 1: multi-row form)
     // backward (sinkhorn_reg_kernel<.., true>): dP view, dS out (contiguous B x n1max x n2max),
     // potential history (B x iters x H floats; slot H - 1: the dummy rows' potential)
     const float* dp;
@@ -981,6 +982,91 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
     // potA[ia] = lse_c(val - potC[c]) (+ nd * exp(DUMMY - ud)): one wave per ia, lanes along c
     auto along_c = [&](bool add_dummy, bool fast) {
         const float ud = ud_sh;
+        auto multi_rows = [&](auto rwc, bool shifted) {
+            // SK_RW rows per wave at once (rows wv + 16 t): their 16-B loads in flight together, the
+            // row sums reduced on DPP / v_permlane (fpm::wave_sum_dpp) instead of six ds_bpermute
+            // round trips each; a row whose shifted sum leaves [2^-30, 2^30] takes the online form
+            // below.  (The single-row loop was load- and shuffle-latency bound: ~16 GB/s per CU.)
+            constexpr int RW = decltype(rwc)::value;
+            const int nrow = limA > wv ? (limA - wv + 15) / 16 : 0;
+            for (int t0 = 0; t0 < nrow; t0 += RW) {
+                float sh[RW], sm[RW];
+                const float* rp[RW];
+#pragma unroll
+                for (int r = 0; r < RW; ++r) {
+                    const int ia = wv + 16 * (t0 + r < nrow ? t0 + r : t0);
+                    sh[r] = potA[ia];
+                    sm[r] = 0.f;
+                    rp[r] = in + (long)ia * sA;
+                }
+                if (!shifted) {
+                    // first step (no previous potential to shift by): the row max of val - potC in
+                    // a pass of its own, then the max-shifted sum -- two vector passes instead of
+                    // the online rescale on scalar loads
+#pragma unroll
+                    for (int r = 0; r < RW; ++r) sh[r] = -INFINITY;
+                    for (int ic = 4 * lane; ic < limC; ic += 256) {
+                        const float4 pc = *(const float4*)&potC[ic];
+#pragma unroll
+                        for (int r = 0; r < RW; ++r) {
+                            const float4 v = *(const float4*)(rp[r] + ic);
+                            sh[r] = fmaxf(fmaxf(fmaxf(sh[r], v.x * vscale - pc.x), fmaxf(v.y * vscale - pc.y,
+                                          v.z * vscale - pc.z)), v.w * vscale - pc.w);
+                        }
+                    }
+#pragma unroll
+                    for (int r = 0; r < RW; ++r) sh[r] = fpm::warp_max(sh[r]);
+                }
+                for (int ic = 4 * lane; ic < limC; ic += 256) {
+                    const float4 pc = *(const float4*)&potC[ic];
+                    float4 v[RW];
+#pragma unroll
+                    for (int r = 0; r < RW; ++r) v[r] = *(const float4*)(rp[r] + ic);
+#pragma unroll
+                    for (int r = 0; r < RW; ++r) sm[r] += e4(v[r], pc, sh[r] == -INFINITY ? 0.f : sh[r]);
+                }
+#pragma unroll
+                for (int r = 0; r < RW; ++r) {
+                    if (t0 + r >= nrow) break;
+                    const int ia = wv + 16 * (t0 + r);
+                    if (!shifted) {
+                        float m = sh[r], s2 = fpm::wave_sum_dpp(sm[r]);
+                        if (m == -INFINITY) s2 = 0.f;
+                        if (add_dummy) lse_combine(m, s2, DUMMY - ud, (float)nd);
+                        if (lane == 0) potA[ia] = (m == -INFINITY) ? 0.f : m + fpm::fast_log2(s2);
+                        continue;
+                    }
+                    float sr = fpm::wave_sum_dpp(sm[r]);
+                    if (add_dummy) sr += (float)nd * fpm::fast_exp2(DUMMY - ud - sh[r]);
+                    if (ok_s(sr)) {
+                        if (lane == 0) potA[ia] = sh[r] + fpm::fast_log2(sr);
+                        continue;
+                    }
+                    // out of range (wave-uniform): this row's exact max, then the max-shifted sum,
+                    // both on 16-B loads
+                    float m = -INFINITY, s2 = 0.f;
+                    for (int ic = 4 * lane; ic < limC; ic += 256) {
+                        const float4 pc = *(const float4*)&potC[ic];
+                        const float4 v = *(const float4*)(rp[r] + ic);
+                        m = fmaxf(fmaxf(fmaxf(m, v.x * vscale - pc.x), fmaxf(v.y * vscale - pc.y, v.z * vscale - pc.z)),
+                                  v.w * vscale - pc.w);
+                    }
+                    m = fpm::warp_max(m);
+                    for (int ic = 4 * lane; ic < limC; ic += 256)
+                        s2 += e4(*(const float4*)(rp[r] + ic), *(const float4*)&potC[ic], m == -INFINITY ? 0.f : m);
+                    s2 = m == -INFINITY ? 0.f : fpm::wave_sum_dpp(s2);
+                    if (add_dummy) lse_combine(m, s2, DUMMY - ud, (float)nd);
+                    if (lane == 0) potA[ia] = (m == -INFINITY) ? 0.f : m + fpm::fast_log2(s2);
+                }
+            }
+        };
+        if (vec && a.rw > 1 && (fast || a.fast)) {
+            if (a.rw >= 8) multi_rows(std::integral_constant<int, 8>{}, fast);
+            else if (a.rw >= 4) multi_rows(std::integral_constant<int, 4>{}, fast);
+            else multi_rows(std::integral_constant<int, 2>{}, fast);
+            __syncthreads();
+            return;
+        }
         for (int ia = wv; ia < limA; ia += 16) {
             if (fast && vec) {
                 const float sh = potA[ia];
@@ -1038,6 +1124,70 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
         const float ud = ud_sh;
         const int cpad = (limC + 63) / 64 * 64;
         const int groups = cpad >= 1024 ? 1 : 1024 / cpad;
+        if (!fast && vec && a.rw > 1 && a.fast) {
+            // first step: per column quad the max over the rows of val - potA, then the max-shifted
+            // sum (two vector passes; row groups combined through LDS), as in along_c's first step
+            const int nq = limC >> 2, qpad = (nq + 63) / 64 * 64;
+            const int groups4 = qpad >= 1024 ? 1 : 1024 / qpad;
+            for (int q0 = 0; q0 < nq; q0 += 1024) {
+                const int q = q0 + (groups4 == 1 ? tid : tid % qpad), grp = groups4 == 1 ? 0 : tid / qpad;
+                const int ic = 4 * q;
+                const bool act = q < nq && grp < groups4;
+                float4 mx = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+                if (act)
+#pragma unroll 8
+                    for (int ia = grp; ia < limA; ia += groups4) {
+                        const float4 v = *(const float4*)(in + (long)ia * sA + ic);
+                        const float pa = potA[ia];
+                        mx.x = fmaxf(mx.x, v.x * vscale - pa);
+                        mx.y = fmaxf(mx.y, v.y * vscale - pa);
+                        mx.z = fmaxf(mx.z, v.z * vscale - pa);
+                        mx.w = fmaxf(mx.w, v.w * vscale - pa);
+                    }
+                red4[tid] = mx;
+                __syncthreads();
+                if (q < nq) {
+                    const int t0 = groups4 == 1 ? tid : tid % qpad;
+                    for (int g = 0; g < groups4; ++g) {
+                        const float4 o = red4[t0 + g * qpad];
+                        mx.x = fmaxf(mx.x, o.x); mx.y = fmaxf(mx.y, o.y); mx.z = fmaxf(mx.z, o.z); mx.w = fmaxf(mx.w, o.w);
+                    }
+                }
+                __syncthreads();
+                const float4 sh = make_float4(mx.x == -INFINITY ? 0.f : mx.x, mx.y == -INFINITY ? 0.f : mx.y,
+                                              mx.z == -INFINITY ? 0.f : mx.z, mx.w == -INFINITY ? 0.f : mx.w);
+                float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (act)
+#pragma unroll 8
+                    for (int ia = grp; ia < limA; ia += groups4) {
+                        const float4 v = *(const float4*)(in + (long)ia * sA + ic);
+                        const float pa = potA[ia];
+                        acc.x += fpm::fast_exp2(v.x * vscale - pa - sh.x);
+                        acc.y += fpm::fast_exp2(v.y * vscale - pa - sh.y);
+                        acc.z += fpm::fast_exp2(v.z * vscale - pa - sh.z);
+                        acc.w += fpm::fast_exp2(v.w * vscale - pa - sh.w);
+                    }
+                red4[tid] = acc;
+                __syncthreads();
+                if (grp == 0 && q < nq) {
+                    for (int g = 1; g < groups4; ++g) {
+                        const float4 o = red4[tid + g * qpad];
+                        acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
+                    }
+                    const float mv[4] = {mx.x, mx.y, mx.z, mx.w}, sv[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        float m = mv[k], sk = m == -INFINITY ? 0.f : sv[k];
+                        if (add_dummy) lse_combine(m, sk, DUMMY - ud, (float)nd);
+                        newC[ic + k] = (m == -INFINITY) ? 0.f : m + fpm::fast_log2(sk);
+                    }
+                }
+                __syncthreads();
+            }
+            for (int k = tid; k < limC; k += 1024) potC[k] = newC[k];
+            __syncthreads();
+            return;
+        }
         if (fast && vec) {
             // thread = (column quad q, row group grp); float4 partial sums, combined over groups
             const int nq = limC >> 2, qpad = (nq + 63) / 64 * 64;
@@ -1048,7 +1198,7 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
                 float4 sh = make_float4(0.f, 0.f, 0.f, 0.f), acc = sh;
                 if (q < nq) sh = *(const float4*)&potC[ic];
                 if (q < nq && grp < groups4) {
-#pragma unroll 4
+#pragma unroll 8
                     for (int ia = grp; ia < limA; ia += groups4) {
                         const float4 v = *(const float4*)(in + (long)ia * sA + ic);
                         const float pa = potA[ia];
@@ -1158,6 +1308,22 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
 
     float* out = a.out + (long)b * a.out_sb;
     const long oA = a.contig_j ? a.out_si : a.out_sj, oC = a.contig_j ? a.out_sj : a.out_si;
+    if (vec && a.rw > 1 && oC == 1 && (oA & 3) == 0 && ((unsigned long)out & 15) == 0 && (boxC & 3) == 0) {
+        // 16-B loads and stores along c (limC % 4 == 0 under vec; the box's padding written as 0)
+        for (int ia = wv; ia < boxA; ia += 16)
+            for (int ic = 4 * lane; ic < boxC; ic += 256) {
+                float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (ia < limA && ic < limC) {
+                    const float4 v = *(const float4*)(in + (long)ia * sA + ic);
+                    const float4 pc = *(const float4*)&potC[ic];
+                    const float pa = potA[ia];
+                    o = make_float4(fpm::fast_exp2(v.x * vscale - pa - pc.x), fpm::fast_exp2(v.y * vscale - pa - pc.y),
+                                    fpm::fast_exp2(v.z * vscale - pa - pc.z), fpm::fast_exp2(v.w * vscale - pa - pc.w));
+                }
+                *(float4*)(out + ia * oA + ic) = o;
+            }
+        return;
+    }
     for (int ia = wv; ia < boxA; ia += 16)
         for (int ic = lane; ic < boxC; ic += 64) {
             float v = 0.f;
@@ -1180,6 +1346,15 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
 // entries per thread measured 0.578 ms and was dropped).
 int& sinkhorn_lform_flag() {
     static int v = 1;
+    return v;
+}
+
+// streaming kernel's row step: rows per wave processed together (1 = the single-row loop; A/B)
+int& stream_rows_flag() {
+    static int v = [] {
+        const char* e = getenv("FPM_SK_STREAM_RW");
+        return e ? atoi(e) : 4;
+    }();
     return v;
 }
 
@@ -1237,6 +1412,7 @@ extern "C" int fpm_sinkhorn_log_fwd(const float* s, long s_sb, long s_si, long s
     a.iters = iters; a.tau = tau; a.dummy_row = dummy_row;
     a.contig_j = (s_sj == 1) ? 1 : 0;
     a.fast = sinkhorn_fast_flag();
+    a.rw = stream_rows_flag();
     FPM_CHECK_ARG(s_sj == 1 || s_si == 1, "sinkhorn: one of the input's row/column strides must be 1");
     int nmax = n1max > n2max ? n1max : n2max;
     hipStream_t st = (hipStream_t)stream;
