@@ -15,11 +15,12 @@
 namespace {
 
 // log2-unit logsumexp of a row's two entries (one term is exp2(0) = 1 exactly, so u >= max and
-// L = a - u <= 0 after a row step, as in the reference)
+// L = a - u <= 0 after a row step, as in the reference).  The max term's exp2(0) = 1 is not
+// evaluated: 1 + exp2(min - max) is the same sum in either order (one exp, one log per entry).
 __device__ __forceinline__ float urow(float a0, float a1) {
-    float m = fmaxf(a0, a1);
+    const float m = fmaxf(a0, a1);
     if (m == -INFINITY) return INFINITY;
-    return m + fpm::fast_log2(fpm::fast_exp2(a0 - m) + fpm::fast_exp2(a1 - m));
+    return m + fpm::fast_log2(1.f + fpm::fast_exp2(fminf(a0, a1) - m));
 }
 
 // STREAM: blocks beyond 64 values per thread (n1*n2 > 65536, e.g. n = 512) re-read ss from
@@ -130,6 +131,9 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
     // reference's own operation order, so "L <= 0 after a row step" holds exactly as it does there.
     float vu0 = 0.f, vu1 = 0.f, lse0 = 0.f, lse1 = 0.f;
     int last = 0;   // 0: none, 1: row, 2: column
+    // maxima of the last reference-order column step's input (valid while last == 2 after it)
+    float cm0 = -INFINITY, cm1 = -INFINITY;
+    bool cm_ok = false;
 
     // opaque copies of the anchors: stops the compiler from hoisting the 2*NQ distances out of
     // the iteration loop (that would need 128 more VGPRs and spill)
@@ -157,6 +161,7 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
             vu1 = (lse1 == -INFINITY || t1 != t1) ? INFINITY : t1;
         }
         last = 1;
+        cm_ok = false;
     };
     // fast: one pass shifted by the column's log target instead of a max pass (every entry of a
     // row-normalised L is <= 0, and a column's sum stays within 2^+-30 of its target here; a sum
@@ -195,6 +200,7 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
                 lse0 = lcp0 + fpm::fast_log2(a0);
                 lse1 = lcp1 + fpm::fast_log2(a1);
                 last = 2;
+                cm_ok = false;
                 return;
             }
         }
@@ -231,8 +237,22 @@ __global__ __launch_bounds__(1024) void soft_topk_kernel(const float* __restrict
         lse0 = (m0 == -INFINITY) ? -INFINITY : m0 + fpm::fast_log2(a0);
         lse1 = (m1 == -INFINITY) ? -INFINITY : m1 + fpm::fast_log2(a1);
         last = 2;
+        cm0 = m0;
+        cm1 = m1;
+        cm_ok = true;
     };
+    // any(L > 0) (soft_topk.py:232).  After a row step (or none) every L = a - u <= 0 exactly (u >=
+    // max(a_0, a_1) in rounded arithmetic): false without a pass.  After a reference-order column
+    // step L_c = (x - lse_c) + lcp_c is monotone in x (rounding is monotone), so its maximum is the
+    // one at x = the step's own maximum cm_c: the test is two scalar comparisons, the same verdict
+    // as the pass over every entry.
     auto any_pos = [&]() -> bool {
+        if (last != 2) return false;
+        if (cm_ok) {
+            const bool p0 = cm0 != -INFINITY && ((cm0 - lse0) + lcp0) > 0.f;
+            const bool p1 = cm1 != -INFINITY && ((cm1 - lse1) + lcp1) > 0.f;
+            return p0 || p1;
+        }
         float mnl, mxl;
         anchors(mnl, mxl);
         int flag = 0;

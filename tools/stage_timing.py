@@ -1,6 +1,6 @@
 import os, sys, time
 os.environ["FPM_STAGE_TIMING"] = "1"
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 t0 = time.perf_counter()
 def log(*a): print("[%.1fs]" % (time.perf_counter() - t0), *a, flush=True)
 B = int(sys.argv[1]); n = int(sys.argv[2]); dt = sys.argv[3]
