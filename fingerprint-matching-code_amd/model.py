@@ -60,7 +60,7 @@ def pin_rank_cpus():
 
 def host_cpu_share():
     """CPUs this process may use for the host Hungarian pool.  ``FPM_CPU_SHARE`` sets it explicitly
-    (``FPM_LSA_THREADS`` sets the pool size itself, default 2 per CPU of the share).  Otherwise:
+    (``FPM_LSA_THREADS`` sets the pool size itself, default 4 per CPU of the share).  Otherwise:
     OMP_NUM_THREADS (16 per GPU on the pool) capped by the affinity mask; under
     torch.distributed.run (LOCAL_WORLD_SIZE > 1) the cap is this rank's slice of the mask
     (rank_cpu_set; after pin_rank_cpus the mask IS the slice), and a share of 1 is read as the
@@ -159,13 +159,15 @@ class Net(nn.Module):
         self.afau_mode = "f32" if dtype == "f32" else (afau or os.environ.get("FPM_AFAU_DTYPE", "bf16x3"))
         if self.afau_mode not in ("f32", "bf16", "bf16s", "bf16x3"):
             raise ValueError("afau / FPM_AFAU_DTYPE must be f32, bf16, bf16s or bf16x3")
-        # Hungarian pool: 2 threads per CPU of the process's share (FPM_LSA_THREADS overrides).  Measured
+        # Hungarian pool: 4 threads per CPU of the process's share (FPM_LSA_THREADS overrides).  Measured
         # on the 16-CPU box share: 16 / 32 / 48 threads -> 29-44 / 17-22 / 17-18 ms per 1024 pairs
-        # (the pairs of a chunk differ in cost; idle stragglers at each chunk's join dominate at 1x);
-        # round 5: 48 vs 32 threads equal at C3 (31.5 vs 31.6 K pairs/s) and +2-6 % on the 128-pair
-        # forward -- kept at 2x so the pool stays near the box's CPU share (FPM_LSA_THREADS=48 to use it)
+        # (the pairs of a chunk differ in cost; idle stragglers at each chunk's join dominate at 1x).
+        # The threads stay inside the share (its affinity mask); more threads than CPUs only let a
+        # tail group's pairs all start at once and share the cores evenly, so the group ends when its
+        # total work does rather than behind a straggler.  Round 6 (profiles/r06_lsa_threads_ab.txt):
+        # 64 vs 32 threads +5 % on the 128-pair forward (21.8-22.0 vs 20.2-21.0 K), C3 equal.
         share = host_cpu_share()
-        self.lsa_threads = lsa_threads or int(os.environ.get("FPM_LSA_THREADS", str(2 * share)))
+        self.lsa_threads = lsa_threads or int(os.environ.get("FPM_LSA_THREADS", str(4 * share)))
         self.chunks = chunks
         # quadratic (edge) affinity Ke (ngm.py:282-289): dead for every output, off by default
         self.compute_ke = compute_ke
