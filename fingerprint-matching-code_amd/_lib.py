@@ -21,6 +21,8 @@ SIGNATURES = {
     "fpm_version": (I, []),
     "fpm_device_sync": (I, []),
     "fpm_sinkhorn_log_fwd": (I, [P, L, L, L, P, L, L, L, P, P, I, I, I, I, F, I, P]),
+    "fpm_sinkhorn_ws_bytes": (L, [I, I, I]),
+    "fpm_sinkhorn_log_fwd_ws": (I, [P, L, L, L, P, L, L, L, P, P, I, I, I, I, F, I, P, L, P]),
     "fpm_soft_topk_fwd": (I, [P, L, L, P, P, P, I, I, I, I, F, P, L, L, P, P, L, L, P]),
     "fpm_topk_select": (I, [P, L, L, P, L, P, I, I, I, P, L, L, P, L, L, P]),
     "fpm_greedy_perm": (I, [P, L, I, P, I, I, I, P, L, L, P]),

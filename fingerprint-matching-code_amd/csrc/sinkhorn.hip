@@ -29,6 +29,12 @@ struct SinkArgs {
     int contig_j;  // 1: j (column) is the unit-stride dimension of in/out
     int fast;      // shifted single-pass lse after the first step (sinkhorn_reg_kernel)
     int rw;        // streaming kernel: rows per wave in the row step's fast path (> 1: multi-row form)
+    // streaming kernel, pairs split over `split` workgroups along a (1 = one workgroup per pair):
+    // B pairs, per-pair arrival counters (zeroed before the launch), exchange slots of xslot floats
+    int B, split;
+    int* xcnt;
+    float* xbuf;
+    long xslot;
     // backward (sinkhorn_reg_kernel<.., true>): dP view, dS out (contiguous B x n1max x n2max),
     // potential history (B x iters x H floats; slot H - 1: the dummy rows' potential)
     const float* dp;
@@ -939,14 +945,27 @@ __device__ __forceinline__ void lse_push(float& m, float& s, float x) {
     }
 }
 
+typedef unsigned int sk_u32x4 __attribute__((ext_vector_type(4)));
+
 __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
     __shared__ __attribute__((aligned(16))) float potA[SK_MAXN], potC[SK_MAXN];
     __shared__ float4 red4[1024];
     __shared__ float red_m[1024], red_s[1024];
     __shared__ float ud_sh;
-    __shared__ float newC[SK_MAXN];
-    __shared__ int redo_sh;
-    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    __shared__ __attribute__((aligned(16))) float newC[SK_MAXN], xmax[SK_MAXN];
+    __shared__ int redo_sh, xfail_sh;
+    // split launches: XCD x = block % 8 takes pairs x, x + 8, ...; a pair's G sibling workgroups are
+    // consecutive in that XCD's dispatch order (its exchanges stay in one L2, and a waiting sibling
+    // only ever waits for workgroups dispatched before or right after it)
+    const int G = a.split > 1 ? a.split : 1;
+    int b = blockIdx.x, j = 0;
+    if (G > 1) {
+        const int x = blockIdx.x & 7, k = blockIdx.x >> 3;
+        b = (k / G) * 8 + x;
+        j = k % G;
+        if (b >= a.B) return;
+    }
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int n1b = a.n1[b], n2b = a.n2[b];
     const bool transposed = n1b > n2b;
     const int R = transposed ? n2b : n1b, C = transposed ? n1b : n2b;
@@ -969,9 +988,68 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
                fpm::fast_exp2(v.z * vscale - p.z - sh) + fpm::fast_exp2(v.w * vscale - p.w - sh);
     };
     (void)scale;
+    // Split pairs (G > 1; square or dummy-free pairs on the 16-B path, >= 64 lines per workgroup):
+    // sibling j owns the a-lines [a_lo, a_hi) -- their row potentials, their share of every column
+    // sum, their output rows -- and keeps the whole column-potential vector.  A column step
+    // exchanges the G partial column sums (or (max, sum) pairs) through global memory; every
+    // sibling combines them in sibling order, so all hold the same potentials and take the same
+    // fallback decisions.  Other pairs run whole on sibling 0 (the rest return).
+    // (a pair with fewer than 64 G lines uses floor(lines / 64) siblings: its own size decides)
+    const int gcap = limA / 64 < G ? limA / 64 : G;
+    const bool split = G > 1 && vec && a.rw > 1 && nd == 0 && gcap >= 2;
+    if (G > 1 && (!split || j >= gcap) && j != 0) return;
+    const int GP = split ? gcap : 1, jj = split ? j : 0;
+    const int a_lo = (int)((long)limA * jj / GP), a_hi = (int)((long)limA * (jj + 1) / GP);
+    int xr = 0;   // exchange rounds so far (the same count in every sibling)
     for (int k = tid; k < SK_MAXN; k += 1024) { potA[k] = 0.f; potC[k] = 0.f; }
-    if (tid == 0) { ud_sh = 0.f; redo_sh = 0; }
+    if (tid == 0) { ud_sh = 0.f; redo_sh = 0; xfail_sh = 0; }
     __syncthreads();
+
+    // One exchange round (cdna_hip_programming.md Guideline 16, R1 form with the acquire kept):
+    // the partial sums newC[0, limC) (and the partial maxima xmax when `two`) leave as 16-B sc1
+    // stores into this sibling's slot, every wave drains its stores, a barrier, then ONE lane adds
+    // to the pair's arrival counter (agent scope) and polls it (relaxed loads, bounded: a missing
+    // sibling sets xfail and the outputs become NaN instead of the launch hanging), ONE agent
+    // acquire, a barrier; the slots are then read with plain vector loads.  Slots alternate
+    // between two buffers: a sibling's round r + 2 store can only follow every sibling's round
+    // r + 1 arrival, which follows its reads of round r.
+    auto slot_of = [&](int g, int r) { return a.xbuf + (((long)b * G + g) * 2 + (r & 1)) * a.xslot; };
+    auto exchange = [&](bool two) {
+        float* slot = slot_of(j, xr);
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)slot, (short)0, (int)(a.xslot * 4), 0x00020000);
+        const int nq = limC >> 2;
+        for (int q = tid; q < nq; q += 1024) {
+            const float4 v = *(const float4*)&newC[4 * q];
+            __builtin_amdgcn_raw_buffer_store_b128(
+                (sk_u32x4){__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)},
+                rs, 16 * q, 0, 16);
+            if (two) {
+                const float4 m = *(const float4*)&xmax[4 * q];
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    (sk_u32x4){__float_as_uint(m.x), __float_as_uint(m.y), __float_as_uint(m.z), __float_as_uint(m.w)},
+                    rs, (int)(a.xslot / 2) * 4 + 16 * q, 0, 16);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            __hip_atomic_fetch_add(a.xcnt + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int target = GP * (xr + 1);
+            unsigned spins = 0;
+            while (__hip_atomic_load(a.xcnt + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > (1u << 24)) {
+                    xfail_sh = 1;
+                    break;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        ++xr;
+    };
 
     // Shifted single-pass lse (fast, every step after the first; as in sinkhorn_reg_kernel): after
     // a normalisation along one axis every entry is <= 0, so the other axis' lse is shifted by the
@@ -988,13 +1066,14 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
             // round trips each; a row whose shifted sum leaves [2^-30, 2^30] takes the online form
             // below.  (The single-row loop was load- and shuffle-latency bound: ~16 GB/s per CU.)
             constexpr int RW = decltype(rwc)::value;
-            const int nrow = limA > wv ? (limA - wv + 15) / 16 : 0;
+            const int span = a_hi - a_lo;                   // this workgroup's a-lines
+            const int nrow = span > wv ? (span - wv + 15) / 16 : 0;
             for (int t0 = 0; t0 < nrow; t0 += RW) {
                 float sh[RW], sm[RW];
                 const float* rp[RW];
 #pragma unroll
                 for (int r = 0; r < RW; ++r) {
-                    const int ia = wv + 16 * (t0 + r < nrow ? t0 + r : t0);
+                    const int ia = a_lo + wv + 16 * (t0 + r < nrow ? t0 + r : t0);
                     sh[r] = potA[ia];
                     sm[r] = 0.f;
                     rp[r] = in + (long)ia * sA;
@@ -1028,7 +1107,7 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
 #pragma unroll
                 for (int r = 0; r < RW; ++r) {
                     if (t0 + r >= nrow) break;
-                    const int ia = wv + 16 * (t0 + r);
+                    const int ia = a_lo + wv + 16 * (t0 + r);
                     if (!shifted) {
                         float m = sh[r], s2 = fpm::wave_sum_dpp(sm[r]);
                         if (m == -INFINITY) s2 = 0.f;
@@ -1061,8 +1140,7 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
             }
         };
         if (vec && a.rw > 1 && (fast || a.fast)) {
-            if (a.rw >= 8) multi_rows(std::integral_constant<int, 8>{}, fast);
-            else if (a.rw >= 4) multi_rows(std::integral_constant<int, 4>{}, fast);
+            if (a.rw >= 4) multi_rows(std::integral_constant<int, 4>{}, fast);
             else multi_rows(std::integral_constant<int, 2>{}, fast);
             __syncthreads();
             return;
@@ -1124,6 +1202,139 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
         const float ud = ud_sh;
         const int cpad = (limC + 63) / 64 * 64;
         const int groups = cpad >= 1024 ? 1 : 1024 / cpad;
+        if (split) {
+            // this sibling's share of every column sum over its a-lines, exchanged and combined in
+            // sibling order (no dummy rows here: nd == 0)
+            const int nq = limC >> 2, qpad = (nq + 63) / 64 * 64;
+            const int groups4 = qpad >= 1024 ? 1 : 1024 / qpad;
+            if (fast) {
+                for (int q0 = 0; q0 < nq; q0 += 1024) {
+                    const int q = q0 + (groups4 == 1 ? tid : tid % qpad), grp = groups4 == 1 ? 0 : tid / qpad;
+                    const int ic = 4 * q;
+                    float4 sh = make_float4(0.f, 0.f, 0.f, 0.f), acc = sh;
+                    if (q < nq) sh = *(const float4*)&potC[ic];
+                    if (q < nq && grp < groups4) {
+#pragma unroll 8
+                        for (int ia = a_lo + grp; ia < a_hi; ia += groups4) {
+                            const float4 v = *(const float4*)(in + (long)ia * sA + ic);
+                            const float pa = potA[ia];
+                            acc.x += fpm::fast_exp2(v.x * vscale - pa - sh.x);
+                            acc.y += fpm::fast_exp2(v.y * vscale - pa - sh.y);
+                            acc.z += fpm::fast_exp2(v.z * vscale - pa - sh.z);
+                            acc.w += fpm::fast_exp2(v.w * vscale - pa - sh.w);
+                        }
+                    }
+                    red4[tid] = acc;
+                    __syncthreads();
+                    if (grp == 0 && q < nq) {
+                        for (int g = 1; g < groups4; ++g) {
+                            const float4 o = red4[tid + g * qpad];
+                            acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
+                        }
+                        *(float4*)&newC[ic] = acc;
+                    }
+                    __syncthreads();
+                }
+                exchange(false);
+                for (int q = tid; q < nq; q += 1024) {
+                    float4 t = *(const float4*)(slot_of(0, xr - 1) + 4 * q);
+                    for (int g = 1; g < GP; ++g) {
+                        const float4 o = *(const float4*)(slot_of(g, xr - 1) + 4 * q);
+                        t.x += o.x; t.y += o.y; t.z += o.z; t.w += o.w;
+                    }
+                    const float4 sh = *(const float4*)&potC[4 * q];
+                    const float sv[4] = {t.x, t.y, t.z, t.w}, hv[4] = {sh.x, sh.y, sh.z, sh.w};
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        if (ok_s(sv[k])) newC[4 * q + k] = hv[k] + fpm::fast_log2(sv[k]);
+                        else redo_sh = 1;
+                    }
+                }
+                __syncthreads();
+                const bool redo = redo_sh != 0;          // the same in every sibling (same totals)
+                __syncthreads();
+                if (!redo) {
+                    for (int k = tid; k < limC; k += 1024) potC[k] = newC[k];
+                    __syncthreads();
+                    return;
+                }
+                if (tid == 0) redo_sh = 0;
+            }
+            // exact form: each sibling's column max over its lines, the sum shifted by it; combined
+            // as (max, sum) pairs in sibling order
+            for (int q0 = 0; q0 < nq; q0 += 1024) {
+                const int q = q0 + (groups4 == 1 ? tid : tid % qpad), grp = groups4 == 1 ? 0 : tid / qpad;
+                const int ic = 4 * q;
+                const bool act = q < nq && grp < groups4;
+                float4 mx = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+                if (act)
+#pragma unroll 8
+                    for (int ia = a_lo + grp; ia < a_hi; ia += groups4) {
+                        const float4 v = *(const float4*)(in + (long)ia * sA + ic);
+                        const float pa = potA[ia];
+                        mx.x = fmaxf(mx.x, v.x * vscale - pa);
+                        mx.y = fmaxf(mx.y, v.y * vscale - pa);
+                        mx.z = fmaxf(mx.z, v.z * vscale - pa);
+                        mx.w = fmaxf(mx.w, v.w * vscale - pa);
+                    }
+                red4[tid] = mx;
+                __syncthreads();
+                if (q < nq) {
+                    const int t0 = groups4 == 1 ? tid : tid % qpad;
+                    for (int g = 0; g < groups4; ++g) {
+                        const float4 o = red4[t0 + g * qpad];
+                        mx.x = fmaxf(mx.x, o.x); mx.y = fmaxf(mx.y, o.y); mx.z = fmaxf(mx.z, o.z); mx.w = fmaxf(mx.w, o.w);
+                    }
+                }
+                __syncthreads();
+                const float4 sh = make_float4(mx.x == -INFINITY ? 0.f : mx.x, mx.y == -INFINITY ? 0.f : mx.y,
+                                              mx.z == -INFINITY ? 0.f : mx.z, mx.w == -INFINITY ? 0.f : mx.w);
+                float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (act)
+#pragma unroll 8
+                    for (int ia = a_lo + grp; ia < a_hi; ia += groups4) {
+                        const float4 v = *(const float4*)(in + (long)ia * sA + ic);
+                        const float pa = potA[ia];
+                        acc.x += fpm::fast_exp2(v.x * vscale - pa - sh.x);
+                        acc.y += fpm::fast_exp2(v.y * vscale - pa - sh.y);
+                        acc.z += fpm::fast_exp2(v.z * vscale - pa - sh.z);
+                        acc.w += fpm::fast_exp2(v.w * vscale - pa - sh.w);
+                    }
+                red4[tid] = acc;
+                __syncthreads();
+                if (grp == 0 && q < nq) {
+                    for (int g = 1; g < groups4; ++g) {
+                        const float4 o = red4[tid + g * qpad];
+                        acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
+                    }
+                    *(float4*)&newC[ic] = acc;
+                    *(float4*)&xmax[ic] = mx;
+                }
+                __syncthreads();
+            }
+            exchange(true);
+            for (int q = tid; q < nq; q += 1024) {
+                const float* s0 = slot_of(0, xr - 1);
+                float4 t = *(const float4*)(s0 + 4 * q), m4 = *(const float4*)(s0 + a.xslot / 2 + 4 * q);
+                float sv[4] = {t.x, t.y, t.z, t.w}, mv[4] = {m4.x, m4.y, m4.z, m4.w};
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (mv[k] == -INFINITY) sv[k] = 0.f;
+                for (int g = 1; g < GP; ++g) {
+                    const float* sg = slot_of(g, xr - 1);
+                    const float4 to = *(const float4*)(sg + 4 * q), mo = *(const float4*)(sg + a.xslot / 2 + 4 * q);
+                    const float so[4] = {to.x, to.y, to.z, to.w}, mov[4] = {mo.x, mo.y, mo.z, mo.w};
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) lse_combine(mv[k], sv[k], mov[k], mov[k] == -INFINITY ? 0.f : so[k]);
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) newC[4 * q + k] = (mv[k] == -INFINITY) ? 0.f : mv[k] + fpm::fast_log2(sv[k]);
+            }
+            __syncthreads();
+            for (int k = tid; k < limC; k += 1024) potC[k] = newC[k];
+            __syncthreads();
+            return;
+        }
         if (!fast && vec && a.rw > 1 && a.fast) {
             // first step: per column quad the max over the rows of val - potA, then the max-shifted
             // sum (two vector passes; row groups combined through LDS), as in along_c's first step
@@ -1306,11 +1517,17 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
         }
     }
 
+    if (split && xfail_sh) {                          // a sibling never arrived: fail loudly (NaN)
+        for (int k = tid; k < limC; k += 1024) potC[k] = NAN;
+        __syncthreads();
+    }
+    // output rows: this workgroup's a-lines; the last sibling also zeroes the box's padding lines
+    const int o_lo = a_lo, o_hi = jj == GP - 1 ? boxA : a_hi;
     float* out = a.out + (long)b * a.out_sb;
     const long oA = a.contig_j ? a.out_si : a.out_sj, oC = a.contig_j ? a.out_sj : a.out_si;
     if (vec && a.rw > 1 && oC == 1 && (oA & 3) == 0 && ((unsigned long)out & 15) == 0 && (boxC & 3) == 0) {
         // 16-B loads and stores along c (limC % 4 == 0 under vec; the box's padding written as 0)
-        for (int ia = wv; ia < boxA; ia += 16)
+        for (int ia = o_lo + wv; ia < o_hi; ia += 16)
             for (int ic = 4 * lane; ic < boxC; ic += 256) {
                 float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
                 if (ia < limA && ic < limC) {
@@ -1324,7 +1541,7 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
             }
         return;
     }
-    for (int ia = wv; ia < boxA; ia += 16)
+    for (int ia = o_lo + wv; ia < o_hi; ia += 16)
         for (int ic = lane; ic < boxC; ic += 64) {
             float v = 0.f;
             if (ia < limA && ic < limC) v = fpm::fast_exp2(val(ia, ic) - potA[ia] - potC[ic]);
@@ -1397,15 +1614,39 @@ bool sinkhorn_reg_bwd(const float* s, long s_sb, long s_si, long s_sj, const flo
     return true;
 }
 
-extern "C" int fpm_sinkhorn_log_fwd(const float* s, long s_sb, long s_si, long s_sj, float* out,
-                                    long o_sb, long o_si, long o_sj, const int* n1, const int* n2,
-                                    int B, int n1max, int n2max, int iters, float tau, int dummy_row,
-                                    void* stream) {
+// streaming kernel (boxes over 256): workgroups per pair (FPM_SK_SPLIT, default 2; 1 = one per pair).
+// Used only with a caller-provided workspace (fpm_sinkhorn_log_fwd_ws); a pair's result depends on
+// this count (the column sums' fp32 summation order), not on the batch it comes in.
+int& stream_split_flag() {
+    static int v = [] {
+        const char* e = getenv("FPM_SK_SPLIT");
+        int g = e ? atoi(e) : 2;
+        return g < 1 ? 1 : (g > 8 ? 8 : g);
+    }();
+    return v;
+}
+
+namespace {
+long sk_cnt_bytes(int B) { return ((long)B * 4 + 15) / 16 * 16; }
+long sk_xslot(int n1max, int n2max) { return 2 * (long)((((n1max > n2max ? n1max : n2max) + 3) / 4) * 4); }
+}  // namespace
+
+extern "C" long fpm_sinkhorn_ws_bytes(int B, int n1max, int n2max) {
+    const int nmax = n1max > n2max ? n1max : n2max;
+    const int G = stream_split_flag();
+    if (B <= 0 || nmax <= 256 || G <= 1) return 0;
+    return sk_cnt_bytes(B) + (long)B * G * 2 * sk_xslot(n1max, n2max) * 4;
+}
+
+extern "C" int fpm_sinkhorn_log_fwd_ws(const float* s, long s_sb, long s_si, long s_sj, float* out, long o_sb,
+                                       long o_si, long o_sj, const int* n1, const int* n2, int B, int n1max,
+                                       int n2max, int iters, float tau, int dummy_row, void* ws, long ws_bytes,
+                                       void* stream) {
     FPM_CHECK_ARG(B >= 0 && n1max > 0 && n2max > 0, "sinkhorn: bad sizes");
     FPM_CHECK_ARG(n1max <= SK_MAXN && n2max <= SK_MAXN, "sinkhorn: n1max/n2max > %d not supported (%d,%d)",
                   SK_MAXN, n1max, n2max);
     if (B == 0) return 0;
-    SinkArgs a;
+    SinkArgs a = {};
     a.in = s; a.in_sb = s_sb; a.in_si = s_si; a.in_sj = s_sj;
     a.out = out; a.out_sb = o_sb; a.out_si = o_si; a.out_sj = o_sj;
     a.n1 = n1; a.n2 = n2; a.n1max = n1max; a.n2max = n2max;
@@ -1413,6 +1654,8 @@ extern "C" int fpm_sinkhorn_log_fwd(const float* s, long s_sb, long s_si, long s
     a.contig_j = (s_sj == 1) ? 1 : 0;
     a.fast = sinkhorn_fast_flag();
     a.rw = stream_rows_flag();
+    a.B = B;
+    a.split = 1;
     FPM_CHECK_ARG(s_sj == 1 || s_si == 1, "sinkhorn: one of the input's row/column strides must be 1");
     int nmax = n1max > n2max ? n1max : n2max;
     hipStream_t st = (hipStream_t)stream;
@@ -1428,9 +1671,32 @@ extern "C" int fpm_sinkhorn_log_fwd(const float* s, long s_sb, long s_si, long s
         else if (nmax <= 128) k = sinkhorn_reg_kernel<4, 4>;
         else if (nmax <= 256) k = sinkhorn_reg_kernel<8, 8>;
     }
-    if (k)
+    if (k) {
         hipLaunchKernelGGL(k, dim3(B), dim3(1024), 0, st, a);
-    else
-        hipLaunchKernelGGL(sinkhorn_stream_kernel, dim3(B), dim3(1024), 0, st, a);
+        return fpm::check_launch("fpm_sinkhorn_log_fwd");
+    }
+    const long need = fpm_sinkhorn_ws_bytes(B, n1max, n2max);
+    unsigned grid = (unsigned)B;
+    if (ws && need > 0) {
+        FPM_CHECK_ARG(ws_bytes >= need, "sinkhorn: workspace %ld B < %ld B (fpm_sinkhorn_ws_bytes)", ws_bytes, need);
+        FPM_CHECK_ARG(((uintptr_t)ws & 15) == 0, "sinkhorn: workspace not 16-B aligned");
+        a.split = stream_split_flag();
+        a.xcnt = (int*)ws;
+        a.xbuf = (float*)((char*)ws + sk_cnt_bytes(B));
+        a.xslot = sk_xslot(n1max, n2max);
+        // arrival counters zeroed on the stream before every launch (a memset node under capture)
+        FPM_CHECK_ARG(hipMemsetAsync(ws, 0, (size_t)sk_cnt_bytes(B), st) == hipSuccess, "sinkhorn: counter memset failed");
+        grid = (unsigned)(((B + 7) / 8) * 8 * a.split);
+    }
+    hipLaunchKernelGGL(sinkhorn_stream_kernel, dim3(grid), dim3(1024), 0, st, a);
     return fpm::check_launch("fpm_sinkhorn_log_fwd");
+}
+
+// Without a workspace the streaming kernel runs one workgroup per pair.
+extern "C" int fpm_sinkhorn_log_fwd(const float* s, long s_sb, long s_si, long s_sj, float* out,
+                                    long o_sb, long o_si, long o_sj, const int* n1, const int* n2,
+                                    int B, int n1max, int n2max, int iters, float tau, int dummy_row,
+                                    void* stream) {
+    return fpm_sinkhorn_log_fwd_ws(s, s_sb, s_si, s_sj, out, o_sb, o_si, o_sj, n1, n2, B, n1max, n2max, iters, tau,
+                                   dummy_row, nullptr, 0, stream);
 }

@@ -56,9 +56,13 @@ def sinkhorn(s, n1, n2, iters, tau, dummy_row=True, out=None, n1max=None, n2max=
     _shape(out, (B, n1max, n2max), "sinkhorn out")
     _shape(n1, (B,), "sinkhorn n1")
     _shape(n2, (B,), "sinkhorn n2")
-    _lib.call("fpm_sinkhorn_log_fwd", _p(s), s.stride(0), s.stride(1), s.stride(2), _p(out), out.stride(0),
+    # boxes over 256: the streaming kernel's split form needs a workspace of its own per call (exchange
+    # slots + arrival counters; allocated on the caller's stream, so concurrent streams never share one)
+    wsb = int(_lib.load().fpm_sinkhorn_ws_bytes(B, n1max, n2max)) if max(n1max, n2max) > 256 else 0
+    ws = torch.empty(wsb, device=s.device, dtype=torch.uint8) if wsb > 0 else None
+    _lib.call("fpm_sinkhorn_log_fwd_ws", _p(s), s.stride(0), s.stride(1), s.stride(2), _p(out), out.stride(0),
               out.stride(1), out.stride(2), _p(n1), _p(n2), B, n1max, n2max, int(iters), float(tau),
-              int(bool(dummy_row)), _stream(s))
+              int(bool(dummy_row)), _p(ws), wsb, _stream(s))
     return out
 
 

@@ -36,6 +36,15 @@ int fpm_device_sync(void);
 int fpm_sinkhorn_log_fwd(const float* s, long s_sb, long s_si, long s_sj, float* out, long o_sb, long o_si,
                          long o_sj, const int* n1, const int* n2, int B, int n1max, int n2max, int iters,
                          float tau, int dummy_row, void* stream);
+/* The same with a caller-provided device workspace of fpm_sinkhorn_ws_bytes(B, n1max, n2max) bytes
+ * (16-B aligned; 0 = none needed): boxes over 256 then run each pair on FPM_SK_SPLIT (default 2)
+ * workgroups that exchange their partial column sums through it, instead of one workgroup per pair
+ * (fp32 summation order of the column sums differs; both forms within the oracle's tolerance).
+ * Concurrent calls need separate workspaces. */
+long fpm_sinkhorn_ws_bytes(int B, int n1max, int n2max);
+int fpm_sinkhorn_log_fwd_ws(const float* s, long s_sb, long s_si, long s_sj, float* out, long o_sb, long o_si,
+                            long o_sj, const int* n1, const int* n2, int B, int n1max, int n2max, int iters,
+                            float tau, int dummy_row, void* ws, long ws_bytes, void* stream);
 
 /* ---- soft top-k -------------------------------------------------------------------------------
  * Replaces soft_topk(..., return_prob=True)[1] (src/model/soft_topk.py:8-53) incl. Sinkhorn_m's

@@ -11,7 +11,7 @@ import pytest
 import torch
 
 import fpm
-from fpm import ops, params, synth
+from fpm import _lib, ops, params, synth
 from fpm.batch import DeviceBatch
 import oracle as O
 
@@ -769,6 +769,42 @@ def test_sinkhorn_stream_ragged_vs_oracle(n1s, n2s, tau):
     ref = O.pygm_sinkhorn(s.double(), n1s, n2s, dummy_row=True, max_iter=10, tau=tau)
     out = ops.sinkhorn(s.to(DEV), _i32(n1s), _i32(n2s), 10, tau, True).cpu()
     assert (out.double() - ref).abs().max() < 1e-4
+
+
+@pytest.mark.parametrize("tau", [0.01, 0.0005])
+def test_sinkhorn_stream_split_vs_oracle(tau):
+    """Boxes over 256 through ops.sinkhorn: square / dummy-free pairs run on FPM_SK_SPLIT workgroups
+    that exchange partial column sums (tau 0.0005 drives the shifted sums out of range: the exact
+    (max, sum) exchange); pairs with dummy rows run whole on one workgroup of the same launch.  Both
+    layouts; deterministic; a pair's result does not depend on the batch; and within 1e-5 of the
+    one-workgroup form (fpm_sinkhorn_log_fwd without a workspace)."""
+    g = torch.Generator().manual_seed(31)
+    n1s, n2s = (512, 400, 300, 512, 260, 256, 512), (512, 400, 512, 300, 260, 256, 497)
+    B, n1max, n2max = len(n1s), 512, 512
+    s = torch.randn(B, n1max, n2max, generator=g) * 0.3
+    # fp32 entries s / tau reach ~3e3 at tau = 0.0005: ~2e-4 of rounding in the log domain for any
+    # fp32 form (the one-workgroup kernel measures 1.06e-4 on the transposed layout); 1e-4 at 0.01
+    tol = 1e-4 if tau >= 0.01 else 2e-4
+    ref = O.pygm_sinkhorn(s.double(), n1s, n2s, dummy_row=True, max_iter=10, tau=tau)
+    sd, n1d, n2d = s.to(DEV), _i32(n1s), _i32(n2s)
+    out = ops.sinkhorn(sd, n1d, n2d, 10, tau, True)
+    assert (out.cpu().double() - ref).abs().max() < tol
+    assert torch.equal(out, ops.sinkhorn(sd, n1d, n2d, 10, tau, True))
+    solo = ops.sinkhorn(sd[:2].contiguous(), n1d[:2].contiguous(), n2d[:2].contiguous(), 10, tau, True)
+    assert torch.equal(solo, out[:2])
+    sT = s.transpose(1, 2).contiguous().to(DEV).transpose(1, 2)
+    o2 = torch.zeros(B, n2max, n1max, device=DEV).transpose(1, 2)
+    ops.sinkhorn(sT, n1d, n2d, 10, tau, True, out=o2)
+    assert (o2.cpu().double() - ref).abs().max() < tol
+    one = torch.empty_like(out)
+    _lib.call("fpm_sinkhorn_log_fwd", ops._p(sd), *sd.stride(), ops._p(one), *one.stride(), ops._p(n1d),
+              ops._p(n2d), B, n1max, n2max, 10, float(tau), 1, ops._stream(sd))
+    torch.cuda.synchronize()
+    assert (one - out).abs().max().item() < 1e-5
+    # dummy_row=False: rectangular pairs have no dummy rows, so they split as well
+    ref_nd = O.pygm_sinkhorn(s.double(), n1s, n2s, dummy_row=False, max_iter=10, tau=tau)
+    out_nd = ops.sinkhorn(sd, n1d, n2d, 10, tau, False)
+    assert (out_nd.cpu().double() - ref_nd).abs().max() < tol
 
 
 def test_soft_topk_stream_vs_oracle():

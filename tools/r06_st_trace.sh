@@ -4,7 +4,8 @@
 set -o pipefail
 export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
+N=${N:-256}
 for B in ${BS:-128 1024}; do
-  FPM_STREAMS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/st$B -o st --output-format csv -- python tools/stage_timing.py $B 256 bf16 > gpurun_out/st$B.log 2>&1 || { tail gpurun_out/st$B.log; exit 1; }
-  grep "iter 2" gpurun_out/st$B.log
+  FPM_STREAMS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/st${B}_$N -o st --output-format csv -- python tools/stage_timing.py $B $N bf16 > gpurun_out/st${B}_$N.log 2>&1 || { tail gpurun_out/st${B}_$N.log; exit 1; }
+  grep "iter 2" gpurun_out/st${B}_$N.log
 done
