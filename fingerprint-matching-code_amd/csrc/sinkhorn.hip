@@ -1037,12 +1037,10 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
             __hip_atomic_fetch_add(a.xcnt + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const int target = GP * (xr + 1);
             unsigned spins = 0;
-            while (__hip_atomic_load(a.xcnt + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            // bounded: ~2^20 polls (about a second); after one failure later rounds do not wait
+            while (!xfail_sh && __hip_atomic_load(a.xcnt + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
                 __builtin_amdgcn_s_sleep(1);
-                if (++spins > (1u << 24)) {
-                    xfail_sh = 1;
-                    break;
-                }
+                if (++spins > (1u << 20)) xfail_sh = 1;
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
