@@ -883,8 +883,9 @@ def test_match_cls_bf16_vs_f32(sd):
 def test_gnn_kernel_variants_bit_identical(sd):
     """Launch variants give bit-identical forwards: combine workgroup sizes, the global plan kernels,
     and the product GEMM on the 256 x 256 two-stage kernel (gemm_phase 0) instead of the phase
-    kernel."""
-    pairs = synth.make_batch(17, 3, 64)
+    kernel.  n = 96: above the fp64 k chain's 64-keypoint boxes, so the fp32 GNN layers and
+    Sinkhorns run."""
+    pairs = synth.make_batch(17, 3, 96)
     net = fpm.Net(regression=True, backbone=False, dtype="bf16")
     net.load_state_dict(sd)
     bt = DeviceBatch.from_pairs(pairs, DEV)
