@@ -39,6 +39,21 @@ def test_error_channel():
         _lib.call("fpm_sinkhorn_log_fwd", None, 0, 2, 2, None, 0, 0, 1, None, None, 1, 30, 30, 10, 0.01, 1, None)
 
 
+def test_sinkhorn_workspace_contract():
+    """fpm_sinkhorn_ws_bytes (host arithmetic only): no workspace for boxes <= 256 (register
+    kernels), a 16-B-multiple counter block + two exchange slots per sibling above; a too-small
+    workspace is refused before any launch."""
+    lib = _lib.load()
+    assert lib.fpm_sinkhorn_ws_bytes(64, 256, 256) == 0
+    assert lib.fpm_sinkhorn_ws_bytes(0, 512, 512) == 0
+    b1, b8 = lib.fpm_sinkhorn_ws_bytes(1, 512, 300), lib.fpm_sinkhorn_ws_bytes(8, 512, 300)
+    assert 0 < b1 < b8 and b1 % 16 == 0 and b8 % 16 == 0
+    assert lib.fpm_sinkhorn_ws_bytes(8, 300, 512) == b8               # the larger side sets the slot
+    with pytest.raises(_lib.FpmError, match="workspace"):
+        _lib.call("fpm_sinkhorn_log_fwd_ws", None, 0, 512, 1, None, 0, 512, 1, None, None, 8, 512, 300, 10,
+                  0.01, 1, ctypes.c_void_p(16), b8 - 16, None)
+
+
 def test_wrong_result_probe_gated(monkeypatch):
     """the 'gnn_mlp_off' timing probe (wrong GNN results) is refused by fpm_set_tuning
     unless FPM_TIMING_PROBES=1, and Net.run refuses to produce outputs while it is on."""
