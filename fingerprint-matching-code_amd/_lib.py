@@ -45,6 +45,7 @@ SIGNATURES = {
     "fpm_rows_bcast_scale": (I, [I, P, L, I, P, P, P, I, P]),
     "fpm_edge_diff_padded": (I, [P, P, P, P, P, P, L, I, P, P]),
     "fpm_kron_gnn_layer_fwd": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P]),
+    "fpm_kron_gnn_layer_fwd_ord": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P]),
     "fpm_gnn_param_count": (I, [I]),
     "fpm_node_classifier": (I, [P, I, I, I, P, P, P, P, P]),
     "fpm_crossset_attn_fwd": (I, [I, P, L, L, I, I, I, P, P, I, P, P, P, P, P, P, P]),

@@ -9,10 +9,45 @@ Per side g (0 = source graphs ``idx1``, 1 = target graphs ``idx2``):
   * w[g]      (B, 512) fp32          global feature (ngm.py:238).
 n1/n2 are per-pair node counts (int32, device + host copies); n1max/n2max the batch maxima.
 """
+import os
+
 import numpy as np
 import torch
 
 from . import config as C
+
+# graph-2 block order of the GNN layers (a schedule; results unchanged): boxes over this many
+# keypoints run their (pair, graph-2 node) workgroups in Hilbert-curve order of the keypoints, so the
+# workgroups in flight share neighbour rows in L2 (n = 512: -15 % per 17-channel layer, no effect at
+# n = 256 where a pair's state fits the L2 anyway; profiles/r06_gnn_order.txt)
+ORDER_MIN_NMAX = 256
+# FPM_GNN_ORDER=0: identity block order everywhere (A/B)
+ORDER_ON = os.environ.get("FPM_GNN_ORDER", "1") != "0"
+
+
+def hilbert_order(P, n, nmax):
+    """(B, nmax) int32 permutation per pair: valid keypoints P[b, :n[b]] (x in [0, 320), y in
+    [0, 240), the reference's frame) in Hilbert-curve order, then the padding slots in index order.
+    Vectorised torch on P's device."""
+    P = torch.as_tensor(P, dtype=torch.float32)
+    B = P.shape[0]
+    n = torch.as_tensor(n, dtype=torch.int64, device=P.device).view(B, 1)
+    q = torch.stack([P[..., 0] / 320.0, P[..., 1] / 240.0], -1).clamp(0.0, 1.0) * 1023.0
+    x, y = q[..., 0].long(), q[..., 1].long()
+    d = torch.zeros_like(x)
+    s = 512
+    while s > 0:
+        rx, ry = (x & s) > 0, (y & s) > 0
+        d += s * s * ((3 * rx.long()) ^ ry.long())
+        m = ~ry
+        sw = m & rx
+        x = torch.where(sw, 1023 - x, x)
+        y = torch.where(sw, 1023 - y, y)
+        x, y = torch.where(m, y, x), torch.where(m, x, y)
+        s >>= 1
+    idx = torch.arange(nmax, device=P.device).view(1, nmax).expand(B, nmax)
+    key = torch.where(idx < n, d, (1 << 21) + idx)      # padding after every valid key, in index order
+    return torch.argsort(key, dim=1, stable=True).to(torch.int32).contiguous()
 
 
 class DeviceBatch:
@@ -31,6 +66,8 @@ class DeviceBatch:
         # per side, cumulative edge offsets per pair (host), for splitting into sub-batches
         self.edge_off = edge_off
         self._splits = {}
+        # optional (B, n2max) int32 graph-2 block order of the GNN layers (hilbert_order; None = identity)
+        self.ord2 = None
 
     def split(self, k, tail=0):
         """k contiguous sub-batches of pairs (views of x/w, renumbered edge copies); cached.
@@ -75,6 +112,7 @@ class DeviceBatch:
         sub = DeviceBatch(b1 - b0, self.n_host[0][b0:b1], self.n_host[1][b0:b1], xs, ws, ss, ds, ps, self.device,
                           nmax=self.nmax, edge_off=eo, shared0=self.shared0)
         sub.pair_range = (b0, b1)
+        sub.ord2 = None if self.ord2 is None else self.ord2[b0:b1]
         return sub
 
     def to(self, device, non_blocking=True):
@@ -88,6 +126,7 @@ class DeviceBatch:
                           mv(self.pseudo), device, nmax=self.nmax, edge_off=self.edge_off, shared0=self.shared0)
         if hasattr(self, "pair_range"):
             out.pair_range = self.pair_range
+        out.ord2 = None if self.ord2 is None else self.ord2.to(device, non_blocking=non_blocking)
         return out
 
     def max_graph_edges(self, side):
@@ -140,7 +179,13 @@ class DeviceBatch:
             srcs.append(torch.from_numpy(np.concatenate(s_l).astype(np.int32)).to(device))
             dsts.append(torch.from_numpy(np.concatenate(d_l).astype(np.int32)).to(device))
             pss.append(torch.from_numpy(np.concatenate(p_l).astype(np.float32)).to(device).contiguous())
-        return DeviceBatch(B, ns[0], ns[1], xs, ws, srcs, dsts, pss, device, edge_off=eoffs)
+        bt = DeviceBatch(B, ns[0], ns[1], xs, ws, srcs, dsts, pss, device, edge_off=eoffs)
+        if ORDER_ON and bt.nmax[1] > ORDER_MIN_NMAX and all("P" in p[1] for p in pairs):
+            P2 = np.zeros((B, bt.nmax[1], 2), np.float32)
+            for b, p in enumerate(pairs):
+                P2[b, :p[1]["n"]] = p[1]["P"]
+            bt.ord2 = hilbert_order(torch.from_numpy(P2), ns[1], bt.nmax[1]).to(device)
+        return bt
 
     @staticmethod
     def from_keypoints(P, n, x, w, device, stg="tri"):
@@ -162,6 +207,8 @@ class DeviceBatch:
             ns.append(torch.as_tensor(n[side], dtype=torch.int32).cpu())
         bt = DeviceBatch(B, ns[0], ns[1], [x[0], x[1]], [w[0], w[1]], srcs, dsts, pss, device,
                          nmax=[int(P[0].shape[1]), int(P[1].shape[1])], edge_off=eoffs)
+        if ORDER_ON and bt.nmax[1] > ORDER_MIN_NMAX:
+            bt.ord2 = hilbert_order(P[1].to(device), ns[1], bt.nmax[1])
         return bt
 
     @staticmethod

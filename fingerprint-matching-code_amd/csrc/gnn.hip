@@ -169,13 +169,16 @@ __global__ __launch_bounds__(1024) void gnn_layer_kernel(const float* __restrict
                                                          const int* __restrict__ n2, const float* __restrict__ W,
                                                          float* __restrict__ Xo, float* __restrict__ zbuf,
                                                          float* __restrict__ vpart, const float* __restrict__ cls_w,
-                                                         int B) {
+                                                         int B, const int* __restrict__ ord2) {
     // T[i][TS]: sum of graph-2 neighbour rows, node-major with 80-B rows (C = 17) so phase 2
     // reads a neighbour's 17 channels with 4 ds_read_b128 + 1 ds_read_b32
     constexpr int TS = C == 1 ? 1 : 20;
     extern __shared__ __attribute__((aligned(16))) float T[];
     int b, d;
     if (!pair_block(n2max, B, b, d)) return;
+    // ord2 (optional): the k-th block of a pair takes graph-2 node ord2[b][k] -- a schedule only (each
+    // node's work is unchanged), so that the blocks in flight share neighbour rows in L2
+    if (ord2) d = ord2[(long)b * n2max + d];
     const int i = threadIdx.x;
     const long N = (long)n1max * n2max;
     const float* Xb = X + (long)b * C * N;
@@ -327,10 +330,10 @@ int& gnn_mlp_off_flag() {
     return v;
 }
 
-extern "C" int fpm_kron_gnn_layer_fwd(const float* X, int C, int B, int n1max, int n2max, const int* ptr1,
-                                      const int* nbr1, const int* ptr2, const int* nbr2, const int* n1,
-                                      const int* n2, const float* params, float* Xout, float* zbuf,
-                                      float* vpart, const float* cls_w, void* stream) {
+extern "C" int fpm_kron_gnn_layer_fwd_ord(const float* X, int C, int B, int n1max, int n2max, const int* ptr1,
+                                          const int* nbr1, const int* ptr2, const int* nbr2, const int* n1,
+                                          const int* n2, const float* params, float* Xout, float* zbuf,
+                                          float* vpart, const float* cls_w, const int* ord2, void* stream) {
     FPM_CHECK_ARG(C == 1 || C == 17, "gnn_layer: C must be 1 or 17 (got %d)", C);
     FPM_CHECK_ARG(!vpart || cls_w, "gnn_layer: vpart needs cls_w");
     if (B == 0) return 0;
@@ -339,7 +342,7 @@ extern "C" int fpm_kron_gnn_layer_fwd(const float* X, int C, int B, int n1max, i
     const size_t sh = (size_t)(C == 1 ? 1 : 20) * n1max * 4;
     const int threads = (n1max + 63) / 64 * 64;
     void (*k)(const float*, int, int, const int*, const int*, const int*, const int*, const int*, const int*,
-              const float*, float*, float*, float*, const float*, int) =
+              const float*, float*, float*, float*, const float*, int, const int*) =
         (C == 17 && gnn_sweeps_flag() == 2 && !gnn_mlp_off_flag() && !gnn_store_sc1_flag()) ? gnn_layer_kernel<17, 0, true, 2>
         : (C == 17 && gnn_sweeps_flag() == 3 && !gnn_mlp_off_flag() && !gnn_store_sc1_flag()) ? gnn_layer_kernel<17, 0, true, 3>
         : gnn_mlp_off_flag() ? (C == 1 ? gnn_layer_kernel<1, 0, false> : gnn_layer_kernel<17, 0, false>)
@@ -347,8 +350,16 @@ extern "C" int fpm_kron_gnn_layer_fwd(const float* X, int C, int B, int n1max, i
                                : (C == 1 ? gnn_layer_kernel<1> : gnn_layer_kernel<17>);
     if (sh > 65536) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
     hipLaunchKernelGGL(k, dim3(pair_grid(n2max, B)), dim3(threads), sh, (hipStream_t)stream, X, n1max, n2max, ptr1,
-                       nbr1, ptr2, nbr2, n1, n2, params, Xout, zbuf, vpart, cls_w, B);
+                       nbr1, ptr2, nbr2, n1, n2, params, Xout, zbuf, vpart, cls_w, B, ord2);
     return fpm::check_launch("fpm_kron_gnn_layer_fwd");
+}
+
+extern "C" int fpm_kron_gnn_layer_fwd(const float* X, int C, int B, int n1max, int n2max, const int* ptr1,
+                                      const int* nbr1, const int* ptr2, const int* nbr2, const int* n1,
+                                      const int* n2, const float* params, float* Xout, float* zbuf,
+                                      float* vpart, const float* cls_w, void* stream) {
+    return fpm_kron_gnn_layer_fwd_ord(X, C, B, n1max, n2max, ptr1, nbr1, ptr2, nbr2, n1, n2, params, Xout, zbuf,
+                                      vpart, cls_w, nullptr, stream);
 }
 
 extern "C" int fpm_gnn_param_count(int C) { return C == 1 ? GnnPack<1>::total : GnnPack<17>::total; }

@@ -760,7 +760,8 @@ class Net(nn.Module):
             Xn = torch.empty(B, 17, n2max, n1max, device=dev, dtype=torch.float32)
             last = l == C.GNN_LAYER - 1      # fuse the final classifier's x1 part (ngm.py:368)
             ops.gnn_layer(X, Cin, B, n1max, n2max, csr1, csr2, bt.n1, bt.n2, wp["gnn%d" % l], Xn, zbuf,
-                          vpart=vpart if last else None, cls_w=wp["cls_w"] if last else None)
+                          vpart=vpart if last else None, cls_w=wp["cls_w"] if last else None,
+                          ord2=getattr(bt, "ord2", None))
             # Sinkhorn(20, tau) on Z[i][j] = z[j*n1max + i], written into channel 16 (gnn.py:217-222)
             ops.sinkhorn(zbuf.transpose(1, 2), bt.n1, bt.n2, C.GNN_SK_ITER, self.tau, True,
                          out=Xn[:, 16].transpose(1, 2))

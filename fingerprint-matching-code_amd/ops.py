@@ -332,15 +332,17 @@ def edge_diff_padded(x, src, dst, pair, row, nrows, cscale=None):
     return out
 
 
-def gnn_layer(X, C, B, n1max, n2max, csr1, csr2, n1, n2, params, Xout, zbuf, vpart=None, cls_w=None):
-    _dev(X, n1, n2, params, Xout, zbuf, vpart, cls_w)
+def gnn_layer(X, C, B, n1max, n2max, csr1, csr2, n1, n2, params, Xout, zbuf, vpart=None, cls_w=None, ord2=None):
+    """``ord2``: optional (B, n2max) int32 block order of the graph-2 nodes (a schedule; same results)."""
+    _dev(X, n1, n2, params, Xout, zbuf, vpart, cls_w, ord2)
     _shape(X, (B, C, n2max, n1max), "gnn_layer X")
     _shape(Xout, (B, 17, n2max, n1max), "gnn_layer Xout")
     _shape(zbuf, (B, n2max, n1max), "gnn_layer zbuf")
     _shape(vpart, (B, n2max, n1max), "gnn_layer vpart")
-    _lib.call("fpm_kron_gnn_layer_fwd", _p(X), C, B, n1max, n2max, ctypes.c_void_p(csr1[0]),
+    _shape(ord2, (B, n2max), "gnn_layer ord2")
+    _lib.call("fpm_kron_gnn_layer_fwd_ord", _p(X), C, B, n1max, n2max, ctypes.c_void_p(csr1[0]),
               ctypes.c_void_p(csr1[1]), ctypes.c_void_p(csr2[0]), ctypes.c_void_p(csr2[1]), _p(n1), _p(n2),
-              _p(params), _p(Xout), _p(zbuf), _p(vpart), _p(cls_w), _stream(X))
+              _p(params), _p(Xout), _p(zbuf), _p(vpart), _p(cls_w), _p(ord2), _stream(X))
 
 
 def node_classifier(X, B, n1max, n2max, w, b, out, vpart=None):

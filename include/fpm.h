@@ -253,6 +253,12 @@ int fpm_edge_diff_padded(const float* x, const int* src, const int* dst, const i
 int fpm_kron_gnn_layer_fwd(const float* X, int C, int B, int n1max, int n2max, const int* ptr1, const int* nbr1,
                            const int* ptr2, const int* nbr2, const int* n1, const int* n2, const float* params,
                            float* Xout, float* zbuf, float* vpart, const float* cls_w, void* stream);
+/* The same with a block order: the k-th workgroup of pair b takes graph-2 node ord2[b * n2max + k]
+ * (a permutation of 0..n2max-1 per pair; NULL = identity).  Same results (a schedule only). */
+int fpm_kron_gnn_layer_fwd_ord(const float* X, int C, int B, int n1max, int n2max, const int* ptr1,
+                               const int* nbr1, const int* ptr2, const int* nbr2, const int* n1, const int* n2,
+                               const float* params, float* Xout, float* zbuf, float* vpart, const float* cls_w,
+                               const int* ord2, void* stream);
 int fpm_gnn_param_count(int C);
 /* final classifier (ngm.py:368-369): s[b][i][j] = w . X[b][:, j, i] + bias; with vpart (NULL =
  * all 17 channels): s = vpart + w[16] X[b][16, j, i] + bias */

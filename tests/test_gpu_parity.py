@@ -807,6 +807,31 @@ def test_sinkhorn_stream_split_vs_oracle(tau):
     assert (out_nd.cpu().double() - ref_nd).abs().max() < tol
 
 
+def test_gnn_block_order_bit_identical(sd):
+    """Boxes over 256 run the GNN layers' (pair, graph-2 node) workgroups in Hilbert order of the
+    keypoints (DeviceBatch.ord2, a schedule only): the forward is bit-identical to the identity order,
+    and the batch carries a permutation per pair (padding slots last, in index order)."""
+    from fpm.batch import hilbert_order
+    pairs = synth.make_batch(41, 3, [300, 290, 270], [280, 300, 300])
+    bt = DeviceBatch.from_pairs(pairs, DEV)
+    assert bt.ord2 is not None and tuple(bt.ord2.shape) == (3, 300)
+    o = bt.ord2.cpu()
+    for b, p in enumerate(pairs):
+        assert sorted(o[b].tolist()) == list(range(300))
+        assert o[b, p[1]["n"]:].tolist() == list(range(p[1]["n"], 300))
+    assert torch.equal(hilbert_order(torch.zeros(1, 4, 2), [4], 4).cpu(), torch.arange(4, dtype=torch.int32)[None])
+    net = fpm.Net(regression=True, backbone=False, dtype="bf16")
+    net.load_state_dict(sd)
+    r1 = net.run(bt, chunks=1)
+    torch.cuda.synchronize()
+    bt2 = DeviceBatch.from_pairs(pairs, DEV)
+    bt2.ord2 = None
+    r2 = net.run(bt2, chunks=1)
+    torch.cuda.synchronize()
+    for k in ("s", "ss", "ds_mat", "k_prob", "perm_mat"):
+        assert torch.equal(r1[k], r2[k]), k
+
+
 def test_soft_topk_stream_vs_oracle():
     g = torch.Generator().manual_seed(22)
     B, n = 2, 512
