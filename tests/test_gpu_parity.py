@@ -807,6 +807,29 @@ def test_sinkhorn_stream_split_vs_oracle(tau):
     assert (out_nd.cpu().double() - ref_nd).abs().max() < tol
 
 
+def test_sinkhorn_max_box_and_empty_batch():
+    """The largest supported box (2048 x 2048, SK_MAXN) through both streaming forms (the split one
+    via ops.sinkhorn, one workgroup per pair via fpm_sinkhorn_log_fwd) against the fp64 oracle, a
+    ragged pair with dummy rows beside a square one; and B = 0 launches nothing."""
+    g = torch.Generator().manual_seed(37)
+    n1s, n2s = (2048, 1500), (2048, 2048)
+    B, nm = 2, 2048
+    s = torch.randn(B, nm, nm, generator=g) * 0.3
+    ref = O.pygm_sinkhorn(s.double(), n1s, n2s, dummy_row=True, max_iter=10, tau=0.01)
+    sd, n1d, n2d = s.to(DEV), _i32(n1s), _i32(n2s)
+    out = ops.sinkhorn(sd, n1d, n2d, 10, 0.01, True)
+    assert (out.cpu().double() - ref).abs().max() < 1e-4
+    one = torch.empty_like(out)
+    _lib.call("fpm_sinkhorn_log_fwd", ops._p(sd), *sd.stride(), ops._p(one), *one.stride(), ops._p(n1d),
+              ops._p(n2d), B, nm, nm, 10, 0.01, 1, ops._stream(sd))
+    torch.cuda.synchronize()
+    assert (one.cpu().double() - ref).abs().max() < 1e-4
+    e = torch.empty(0, 512, 512, device=DEV)
+    z = torch.empty(0, dtype=torch.int32, device=DEV)
+    assert ops.sinkhorn(e, z, z, 10, 0.01, True).shape == (0, 512, 512)
+    assert ops.soft_topk_fwd(e, z, z, torch.empty(0, device=DEV), 10, 0.01).shape == (0, 512, 512)
+
+
 def test_gnn_block_order_bit_identical(sd):
     """Boxes over 256 run the GNN layers' (pair, graph-2 node) workgroups in Hilbert order of the
     keypoints (DeviceBatch.ord2, a schedule only): the forward is bit-identical to the identity order,
