@@ -830,6 +830,19 @@ def test_sinkhorn_max_box_and_empty_batch():
     assert ops.soft_topk_fwd(e, z, z, torch.empty(0, device=DEV), 10, 0.01).shape == (0, 512, 512)
 
 
+def test_soft_topk_large_box_vs_oracle():
+    """Soft top-k on a 1024 x 1024 pair (the streaming form, 16 M-entry passes) and a ragged
+    1024 x 700 pair in the same box, against the oracle incl. its while loop."""
+    g = torch.Generator().manual_seed(43)
+    n1s, n2s = [1024, 1024], [1024, 700]
+    ss = torch.rand(2, 1024, 1024, generator=g) ** 8
+    ss[1, :, 700:] = 0
+    k = torch.tensor([600.5, 350.0])
+    ref = O.soft_topk(ss, k, n1s, n2s, 10, 0.01)
+    out = ops.soft_topk_fwd(ss.to(DEV), _i32(n1s), _i32(n2s), k.to(DEV), 10, 0.01).cpu()
+    assert (out - ref).abs().max() < 1e-4
+
+
 def test_gnn_block_order_bit_identical(sd):
     """Boxes over 256 run the GNN layers' (pair, graph-2 node) workgroups in Hilbert order of the
     keypoints (DeviceBatch.ord2, a schedule only): the forward is bit-identical to the identity order,
