@@ -886,6 +886,21 @@ def test_forward_n512_parity(sd):
     assert d["perm_equal"], d
 
 
+@pytest.mark.slow
+def test_forward_univ_size_cap(sd):
+    """The largest box the reference accepts (UNIV_SIZE = 600, ngm.py:387-389) end to end against
+    the oracle, a ragged partner in the same batch; one keypoint more is refused like the reference's
+    assertion."""
+    pairs = synth.make_batch(33, 1, [600], [571])
+    d = _compare_forward(pairs, sd)
+    assert d["ss"] < 1e-4 and d["ds_mat"] < 1e-4 and d["k_prob"] < 1e-4, d
+    assert d["perm_equal"], d
+    net = fpm.Net(regression=True, backbone=False, dtype="bf16")
+    net.load_state_dict(sd)
+    with pytest.raises(AssertionError, match="UNIV_SIZE"):
+        net.run(DeviceBatch.from_pairs(synth.make_batch(33, 1, [601], [64]), DEV))
+
+
 # ---------------------------------------------------------------------------------------- probe x gallery (C4)
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 def test_probe_gallery_shared_equals_per_pair(sd, dtype):
