@@ -101,7 +101,8 @@ extern "C" int fpm_gemm_norm_max(const void* A, long lda, const void* B, long ld
                                  const float* bias, const float* res, long ldres, const float* nw, const float* nb,
                                  float eps, int P, float* gmax, void* stream) {
     using namespace fpm;
-    FPM_CHECK_ARG(P == G2_BM, "gemm_norm_max: P=%d must be %d (one tile per pair)", P, G2_BM);
+    FPM_CHECK_ARG(P == G2_BM || 2 * P == G2_BM, "gemm_norm_max: P=%d must be %d or %d (one or two pairs per tile)", P,
+                  G2_BM, G2_BM / 2);
     FPM_CHECK_ARG(M >= 0 && M % P == 0 && N > 0 && K > 0 && K % G2_BK == 0, "gemm_norm_max: bad sizes M=%d N=%d K=%d",
                   M, N, K);
     FPM_CHECK_ARG(lda % 8 == 0 && ldb % 8 == 0 && ldres >= N, "gemm_norm_max: bad strides");
@@ -111,8 +112,8 @@ extern "C" int fpm_gemm_norm_max(const void* A, long lda, const void* B, long ld
     p.A = A; p.lda = lda; p.B = B; p.ldb = ldb;
     p.M = M; p.N = N; p.K = K; p.nseg = 1;
     p.epi = EPI_NORM_MAX; p.bias = bias; p.ldc = ldres;
-    p.res = res; p.nw = nw; p.nb = nb; p.eps = eps; p.gmax = gmax;
-    const int mt = M / G2_BM;
+    p.res = res; p.nw = nw; p.nb = nb; p.eps = eps; p.gmax = gmax; p.norm_p = P;
+    const int mt = (M + G2_BM - 1) / G2_BM;
     p.remap_mtiles = mt;
     dim3 grid(remap_grid_big(N, 128, mt), 1, 1);
     hipLaunchKernelGGL((gemm_big_kernel<128, EPI_NORM_MAX, true>), grid, dim3(G2_THREADS), 0, (hipStream_t)stream, p);
@@ -127,7 +128,8 @@ extern "C" int fpm_gemm_norm_out(const void* A, long lda, const void* B, long ld
                                  const float* bias, const float* nw, const float* nb, float eps, int P, float* out_f,
                                  long ldc, void* out_t, long ldt, void* stream) {
     using namespace fpm;
-    FPM_CHECK_ARG(P == G2_BM, "gemm_norm_out: P=%d must be %d (one tile per pair)", P, G2_BM);
+    FPM_CHECK_ARG(P == G2_BM || 2 * P == G2_BM, "gemm_norm_out: P=%d must be %d or %d (one or two pairs per tile)", P,
+                  G2_BM, G2_BM / 2);
     FPM_CHECK_ARG(M >= 0 && M % P == 0 && N > 0 && N % 4 == 0 && K > 0 && K % G2_BK == 0,
                   "gemm_norm_out: bad sizes M=%d N=%d K=%d", M, N, K);
     FPM_CHECK_ARG(lda % 8 == 0 && ldb % 8 == 0 && ldc >= N && ldc % 4 == 0 && (!out_t || (ldt >= N && ldt % 4 == 0 &&
@@ -138,8 +140,8 @@ extern "C" int fpm_gemm_norm_out(const void* A, long lda, const void* B, long ld
     p.A = A; p.lda = lda; p.B = B; p.ldb = ldb;
     p.M = M; p.N = N; p.K = K; p.nseg = 1;
     p.epi = EPI_NORM_OUT; p.bias = bias; p.Cf = out_f; p.ldc = ldc; p.Ct = out_t; p.ldt = ldt;
-    p.nw = nw; p.nb = nb; p.eps = eps;
-    const int mt = M / G2_BM;
+    p.nw = nw; p.nb = nb; p.eps = eps; p.norm_p = P;
+    const int mt = (M + G2_BM - 1) / G2_BM;
     p.remap_mtiles = mt;
     dim3 grid(remap_grid_big(N, 128, mt), 1, 1);
     hipLaunchKernelGGL((gemm_big_kernel<128, EPI_NORM_OUT, true>), grid, dim3(G2_THREADS), 0, (hipStream_t)stream, p);
@@ -163,14 +165,14 @@ extern "C" int fpm_gemm_x3out(const void* A, long lda, const void* B, long ldb, 
                   "gemm_x3out: segment Kp=%d must be in [N, N rounded up to 128], 4-aligned, ldt >= 3 Kp", Kp);
     FPM_CHECK_ARG(lda % 8 == 0 && ldb % 8 == 0 && (!out_f || (ldc >= N && ldc % 4 == 0)), "gemm_x3out: bad strides");
     FPM_CHECK_ARG(out_t3, "gemm_x3out: null out_t3");
-    FPM_CHECK_ARG(epi != EPI_NORM_OUT || (P == G2_BM && M % P == 0 && nw && nb && out_f),
-                  "gemm_x3out: the norm epilogue needs P = %d rows per pair, nw, nb and out_f", G2_BM);
+    FPM_CHECK_ARG(epi != EPI_NORM_OUT || ((P == G2_BM || 2 * P == G2_BM) && M % P == 0 && nw && nb && out_f),
+                  "gemm_x3out: the norm epilogue needs P = %d or %d rows per pair, nw, nb and out_f", G2_BM, G2_BM / 2);
     if (M == 0) return 0;
     GemmParams p = {};
     p.A = A; p.lda = lda; p.B = B; p.ldb = ldb;
     p.M = M; p.N = N; p.K = K; p.nseg = 1;
     p.epi = epi; p.bias = bias; p.Cf = out_f; p.ldc = ldc; p.Ct = out_t3; p.ldt = ldt; p.split = Kp;
-    p.nw = nw; p.nb = nb; p.eps = eps;
+    p.nw = nw; p.nb = nb; p.eps = eps; p.norm_p = epi == EPI_NORM_OUT ? P : 0;
     const int mt = (M + G2_BM - 1) / G2_BM;
     p.remap_mtiles = mt;
     dim3 grid(remap_grid_big(N, 128, mt), 1, 1);

@@ -204,7 +204,12 @@ __global__ __launch_bounds__(G2_THREADS, 1) void gemm_big_kernel(GemmParams p) {
         // the fp32 store path below (the block head).  Fixed reduction order.
         static_assert(BN == 128 && F32OUT, "norm epilogues: 256 x 128 fp32 tiles");
         float* red = (float*)smem;                         // [WM][BN]; the K loop's LDS is free
-        const int pair = row0 / G2_BM;
+        // P = 128 (norm_p): two pairs per tile, each over its WG = WM / 2 row waves; P = 256 is the
+        // one-pair form with the same reduction order as before
+        const int P = p.norm_p > 0 ? p.norm_p : G2_BM;
+        const int WG = Cfg::WM * P / G2_BM;               // row waves per pair
+        const int w0 = (wm / WG) * WG;                    // this wave's pair group
+        const int pair = (row0 + w0 * FM * 16) / P;
         float v[FM][FN][4];
 #pragma unroll
         for (int fm = 0; fm < FM; ++fm)
@@ -216,7 +221,10 @@ __global__ __launch_bounds__(G2_THREADS, 1) void gemm_big_kernel(GemmParams p) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int r = wm * FM * 16 + fm * 16 + (lane >> 4) * 4 + j;
-                    v[fm][fn][j] = EPI == EPI_NORM_MAX ? p.res[(long)(row0 + r) * p.ldc + n] + (acc[fm][fn][j] + bv)
+                    // rows past M (the empty second pair of an odd count's last tile): a valid row's
+                    // residual instead, their statistics are never written
+                    const int gr = row0 + r < p.M ? row0 + r : row0;
+                    v[fm][fn][j] = EPI == EPI_NORM_MAX ? p.res[(long)gr * p.ldc + n] + (acc[fm][fn][j] + bv)
                                                        : acc[fm][fn][j] + bv;
                 }
             }
@@ -235,9 +243,8 @@ __global__ __launch_bounds__(G2_THREADS, 1) void gemm_big_kernel(GemmParams p) {
 #pragma unroll
             for (int fn = 0; fn < FN; ++fn) {
                 const int c = wn * FN * 16 + fn * 16 + (lane & 15);
-                float x = red[c];
-#pragma unroll
-                for (int w = 1; w < Cfg::WM; ++w) x = is_max ? fmaxf(x, red[w * BN + c]) : x + red[w * BN + c];
+                float x = red[w0 * BN + c];
+                for (int w = w0 + 1; w < w0 + WG; ++w) x = is_max ? fmaxf(x, red[w * BN + c]) : x + red[w * BN + c];
                 t[fn] = x;
             }
             __syncthreads();
@@ -255,7 +262,7 @@ __global__ __launch_bounds__(G2_THREADS, 1) void gemm_big_kernel(GemmParams p) {
         colred(mean, false);
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn) {
-            mean[fn] /= (float)G2_BM;
+            mean[fn] /= (float)P;
             float s = 0.f;
 #pragma unroll
             for (int fm = 0; fm < FM; ++fm)
@@ -273,7 +280,7 @@ __global__ __launch_bounds__(G2_THREADS, 1) void gemm_big_kernel(GemmParams p) {
             for (int fn = 0; fn < FN; ++fn) {
                 const int c = wn * FN * 16 + fn * 16 + (lane & 15);
                 const int n = n0 + c < p.N ? n0 + c : p.N - 1;
-                const float rstd = 1.f / sqrtf(var[fn] / (float)G2_BM + p.eps);
+                const float rstd = 1.f / sqrtf(var[fn] / (float)P + p.eps);
                 const float ww = p.nw[n], bb = p.nb[n];
                 float m = -INFINITY;
 #pragma unroll
@@ -283,7 +290,7 @@ __global__ __launch_bounds__(G2_THREADS, 1) void gemm_big_kernel(GemmParams p) {
                 mx[fn] = m;
             }
             colred(mx, true);
-            if (wm == 0 && (lane >> 4) == 0) {
+            if (wm == w0 && (lane >> 4) == 0 && pair < p.M / P) {   // (an odd pair count's empty half: no write)
 #pragma unroll
                 for (int fn = 0; fn < FN; ++fn) {
                     const int c = wn * FN * 16 + fn * 16 + lane;
@@ -296,7 +303,7 @@ __global__ __launch_bounds__(G2_THREADS, 1) void gemm_big_kernel(GemmParams p) {
             for (int fn = 0; fn < FN; ++fn) {
                 const int c = wn * FN * 16 + fn * 16 + (lane & 15);
                 const int n = n0 + c < p.N ? n0 + c : p.N - 1;
-                const float rstd = 1.f / sqrtf(var[fn] / (float)G2_BM + p.eps);
+                const float rstd = 1.f / sqrtf(var[fn] / (float)P + p.eps);
                 const float ww = p.nw[n], bb = p.nb[n];
 #pragma unroll
                 for (int fm = 0; fm < FM; ++fm)

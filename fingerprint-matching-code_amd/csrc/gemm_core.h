@@ -57,6 +57,7 @@ struct GemmParams {
     float* gmax;
     long ldt;                // EPI_NORM_OUT / split: row stride of the bf16 copy Ct
     int split;               // > 0 (fp32-output 256-row kernels): Ct rows are split bf16 operands
+    int norm_p;              // EPI_NORM_MAX / EPI_NORM_OUT: rows per pair, 256 (one tile) or 128 (two per tile); 0 = 256
                              // [hi | lo | hi] with segment stride split (ops.split_bf16x3 layout)
     int store_sc1;           // bf16 output tiles of the phase kernel: sc1 stores (the lines leave
                              // the XCD's L2 instead of evicting the gathered A rows)

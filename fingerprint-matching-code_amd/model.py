@@ -486,14 +486,14 @@ class Net(nn.Module):
         if x3:
             # o1t: the split [hi | lo | hi] copy when the combine GEMM's epilogue wrote it
             o13 = o1t if o1t is not o1f else ops.split_bf16x3(o1f, C.AFAU_EMB_PAD)
-            if P_ == 256 and self.afau_fuse_norm:
+            if P_ in (128, 256) and self.afau_fuse_norm:
                 # W1 + bias + ReLU straight into split operands, then W2 with the block tail (instance
                 # norm + max over the pair's 256 positions) in its epilogue: no fp32 FFN round trip
                 h3 = ops.gemm_x3out(o13, wp[blk + "_W1"], rows, FF, 3 * C.AFAU_EMB_PAD, FF, epi=ops.EPI_RELU,
                                     bias=wp[blk + "_b1"])
                 gm = torch.empty(nb_, E, device=dev, dtype=torch.float32)
                 return ops.gemm_norm_max(h3, wp[blk + "_W2"], rows, E, 3 * FF, 3 * FF, 3 * FF, wp[blk + "_b2"], o1f,
-                                         wp[blk + "_n2w"], wp[blk + "_n2b"], gm)
+                                         wp[blk + "_n2w"], wp[blk + "_n2b"], gm, P=P_)
             hf = torch.empty(rows, FF, device=dev, dtype=torch.float32)
             ops.gemm(o13, wp[blk + "_W1"], rows, FF, 3 * C.AFAU_EMB_PAD, o13.shape[1], o13.shape[1],
                      epi=ops.EPI_RELU, bias=wp[blk + "_b1"], out_f=hf, ldc=FF)
@@ -505,12 +505,12 @@ class Net(nn.Module):
             ops.gemm(o1t, wp[blk + "_W1"], rows, FF, KE, KE, KE, epi=ops.EPI_RELU, bias=wp[blk + "_b1"],
                      out_t=hbuf if op != torch.float32 else None, out_f=hbuf if op == torch.float32 else None,
                      ldc=FF)
-            if op != torch.float32 and P_ == 256 and self.afau_fuse_norm:
+            if op != torch.float32 and P_ in (128, 256) and self.afau_fuse_norm:
                 # the second GEMM's epilogue takes the instance norm + max over the pair's 256
                 # positions (one GEMM tile): the (rows x 600) FFN output never reaches HBM
                 gm = torch.empty(nb_, E, device=dev, dtype=torch.float32)
                 return ops.gemm_norm_max(hbuf, wp[blk + "_W2"], rows, E, FF, FF, FF, wp[blk + "_b2"], o1f,
-                                         wp[blk + "_n2w"], wp[blk + "_n2b"], gm)
+                                         wp[blk + "_n2w"], wp[blk + "_n2b"], gm, P=P_)
             ops.gemm(hbuf, wp[blk + "_W2"], rows, E, FF, FF, FF, bias=wp[blk + "_b2"], out_f=ff, ldc=E)
         gm = torch.empty(nb_, E, device=dev, dtype=torch.float32)
         ops.instnorm(o1f, nb_, P_, E, wp[blk + "_n2w"], wp[blk + "_n2b"], in2=ff, gmax=gm)
@@ -566,19 +566,21 @@ class Net(nn.Module):
                           wp["row_mix2b"], att, split=split)
         # bf16s: hi*W_hi + lo*W_hi (2 terms); bf16x3: + hi*W_lo (3 terms, near-fp32)
         kc = 3 * HD if x3 else (2 * HD if split else HD)
-        if x3 and n1max == 256 and self.afau_fuse_norm:
+        # fused instance norms: a pair's positions are one 256-row GEMM tile or half of one (128)
+        fuse = self.afau_fuse_norm and n1max in (128, 256)
+        if x3 and fuse:
             # the combine projection + first instance norm in one GEMM, its output both as fp32 rows
             # (the block's residual) and as the split operand of the FFN's first product
             o1f = torch.empty(B * n1max, E, device=dev, dtype=torch.float32)
             o13 = ops.gemm_x3out(att, wp["row_Wc"], B * n1max, E, kc, C.AFAU_EMB_PAD, epi=ops.EPI_NORM_OUT,
-                                 bias=wp["row_bc"], out_f=o1f, nw=wp["row_n1w"], nb=wp["row_n1b"])
+                                 bias=wp["row_bc"], out_f=o1f, nw=wp["row_n1w"], nb=wp["row_n1b"], P=n1max)
             g_row = self._afau_block(wp, "row", B, n1max, pre=(o1f, o13))
-        elif att.dtype == torch.bfloat16 and not x3 and n1max == 256 and self.afau_fuse_norm:
+        elif att.dtype == torch.bfloat16 and not x3 and fuse:
             # the combine projection's epilogue applies the block's first instance norm (one GEMM
             # tile = one pair's 256 positions): mh never reaches HBM un-normalised
             o1f, o1t = self._afau_norm1_bufs(B * n1max, dev)
             ops.gemm_norm_out(att, wp["row_Wc"], B * n1max, E, kc, att.shape[1], att.shape[1], wp["row_bc"],
-                              wp["row_n1w"], wp["row_n1b"], o1f, out_t=None if o1t is o1f else o1t)
+                              wp["row_n1w"], wp["row_n1b"], o1f, out_t=None if o1t is o1f else o1t, P=n1max)
             g_row = self._afau_block(wp, "row", B, n1max, pre=(o1f, o1t))
         else:
             mh = torch.empty(B * n1max, E, device=dev, dtype=torch.float32)

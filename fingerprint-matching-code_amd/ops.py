@@ -378,7 +378,8 @@ def instnorm(in1, B, P, Cn, w, b, in2=None, nvalid=None, onehot_bias=None, out_f
 
 def gemm_norm_max(A, Bw, M, N, K, lda, ldb, bias, res, nw, nb, gmax, P=256, eps=1e-5):
     """AFA-U block tail fused (fpm_gemm_norm_max): gmax[b][n] = max over the pair's P rows of
-    InstanceNorm(res + A Bw^T + bias) * nw + nb; bf16 A / Bw, P = 256 rows per pair."""
+    InstanceNorm(res + A Bw^T + bias) * nw + nb; bf16 A / Bw, P = 256 or 128 rows per pair (one or
+    two pairs per 256-row tile)."""
     _dev(A, Bw, res, gmax)
     _lib.call("fpm_gemm_norm_max", _p(A), int(lda), _p(Bw), int(ldb), int(M), int(N), int(K), _p(bias), _p(res),
               int(res.stride(0)), _p(nw), _p(nb), float(eps), int(P), _p(gmax), _stream(A))
@@ -492,7 +493,7 @@ def gemm_x3out(A, Bw, M, N, K, Kp, epi=EPI_STORE, bias=None, out_t3=None, out_f=
     """C = epi(A Bw^T + bias) (bf16 A / Bw, fp32 accumulation) written as split bf16 rows
     out_t3 = [hi | lo | hi] (segment Kp, zero K padding; = split_bf16x3 of the fp32 C) and, if
     ``out_f`` is given, fp32 rows.  epi: EPI_STORE, EPI_RELU or EPI_NORM_OUT (instance norm over
-    each pair's P = 256 rows, nw / nb) -- fpm_gemm_x3out.  Returns out_t3."""
+    each pair's P = 256 or 128 rows, nw / nb) -- fpm_gemm_x3out.  Returns out_t3."""
     _dev(A, Bw, out_t3, out_f)
     for t, w in ((A, "A"), (Bw, "B")):
         if t.dtype != torch.bfloat16 or t.dim() != 2 or t.stride(1) != 1:

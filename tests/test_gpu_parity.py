@@ -980,12 +980,14 @@ def test_gnn_kernel_variants_bit_identical(sd):
             assert torch.equal(r[k], outs[0][k]), k
 
 
-def test_afau_gemm_norm_max_fused():
+@pytest.mark.parametrize("P,nb", [(256, 5), (128, 5), (128, 4)])
+def test_afau_gemm_norm_max_fused(P, nb):
     """AFA-U block tail fused into the FFN's second GEMM (fpm_gemm_norm_max): equal to the GEMM +
     separate instance norm + max (same GEMM accumulators; only the norm's reduction order differs)
-    and to a float64 torch statement of InstanceNorm1d + max over positions."""
+    and to a float64 torch statement of InstanceNorm1d + max over positions.  P = 128: two pairs
+    per 256-row tile (an odd pair count leaves the last tile half empty)."""
     g = torch.Generator().manual_seed(3)
-    nb, P, E, FF = 5, 256, 600, 256
+    E, FF = 600, 256
     rows = nb * P
     A = torch.randn(rows, FF, generator=g).to(torch.bfloat16).to(DEV)
     W = (torch.randn(E, FF, generator=g) * 0.06).to(torch.bfloat16).to(DEV)
@@ -993,7 +995,7 @@ def test_afau_gemm_norm_max_fused():
     res = torch.randn(rows, E, generator=g).to(DEV)
     nw = (torch.rand(E, generator=g) + 0.5).to(DEV)
     nbv = (torch.randn(E, generator=g) * 0.1).to(DEV)
-    gm = ops.gemm_norm_max(A, W, rows, E, FF, FF, FF, bias, res, nw, nbv, torch.empty(nb, E, device=DEV))
+    gm = ops.gemm_norm_max(A, W, rows, E, FF, FF, FF, bias, res, nw, nbv, torch.empty(nb, E, device=DEV), P=P)
     ff = torch.empty(rows, E, device=DEV)
     ops.gemm(A, W, rows, E, FF, FF, FF, bias=bias, out_f=ff, ldc=E)
     gm2 = torch.empty(nb, E, device=DEV)
@@ -1004,15 +1006,16 @@ def test_afau_gemm_norm_max_fused():
     ref = (y * nw.double() + nbv.double()).max(1).values
     assert (gm.double() - ref).abs().max() < 1e-4
     with pytest.raises(fpm._lib.FpmError):
-        ops.gemm_norm_max(A[:100], W, 100, E, FF, FF, FF, bias, res[:100], nw, nbv, gm)
+        ops.gemm_norm_max(A[:100], W, 100, E, FF, FF, FF, bias, res[:100], nw, nbv, gm, P=P)
 
 
-def test_afau_gemm_norm_out_fused():
+@pytest.mark.parametrize("P,nb", [(256, 3), (128, 3)])
+def test_afau_gemm_norm_out_fused(P, nb):
     """AFA-U block head fused into the attention-combine GEMM (fpm_gemm_norm_out): fp32 rows and the
     zero-K-padded bf16 copy equal to the GEMM + separate instance norm within reduction-order
     rounding, and to a float64 statement of InstanceNorm1d."""
     g = torch.Generator().manual_seed(4)
-    nb, P, E, K, KE = 3, 256, 600, 512, 640
+    E, K, KE = 600, 512, 640
     rows = nb * P
     A = torch.randn(rows, K, generator=g).to(torch.bfloat16).to(DEV)
     W = (torch.randn(E, K, generator=g) * 0.05).to(torch.bfloat16).to(DEV)
@@ -1021,7 +1024,7 @@ def test_afau_gemm_norm_out_fused():
     nbv = (torch.randn(E, generator=g) * 0.1).to(DEV)
     o1f = torch.empty(rows, E, device=DEV)
     o1t = torch.full((rows, KE), 7.0, device=DEV).to(torch.bfloat16)
-    ops.gemm_norm_out(A, W, rows, E, K, K, K, bias, nw, nbv, o1f, out_t=o1t)
+    ops.gemm_norm_out(A, W, rows, E, K, K, K, bias, nw, nbv, o1f, out_t=o1t, P=P)
     mh = torch.empty(rows, E, device=DEV)
     ops.gemm(A, W, rows, E, K, K, K, bias=bias, out_f=mh, ldc=E)
     r_f = torch.empty(rows, E, device=DEV)
@@ -1036,15 +1039,15 @@ def test_afau_gemm_norm_out_fused():
     assert (o1f.double() - ref).abs().max() < 1e-4
 
 
-@pytest.mark.parametrize("afau,tol", [("bf16s", 2e-4), ("bf16x3", 1e-5)])
-def test_afau_fused_forward_matches_unfused(sd, afau, tol):
+@pytest.mark.parametrize("afau,tol,n,B", [("bf16s", 2e-4, 256, 4), ("bf16x3", 1e-5, 256, 4), ("bf16x3", 1e-5, 128, 5)])
+def test_afau_fused_forward_matches_unfused(sd, afau, tol, n, B):
     """Whole bf16 forwards with the fused AFA-U block head and tail agree with the unfused path on
     a 256-keypoint batch: ss identical (computed before AFA-U); k_prob within ``tol`` -- the fused
     first norm sums in another order, which can move a bf16 rounding of its operand copy by one
     ulp (bf16s: plain bf16 FFN operands, its k_prob distance from the fp32 oracle is ~4-8e-4;
     bf16x3: split near-fp32 operands written by the GEMM epilogues, fpm_gemm_x3out); the fp32 mode
-    is not fused."""
-    pairs = synth.make_batch(41, 4, 256)
+    is not fused.  n = 128: two pairs per fused 256-row tile (five pairs: the last tile half empty)."""
+    pairs = synth.make_batch(41, B, n)
     bt = DeviceBatch.from_pairs(pairs, DEV)
     res = {}
     for fuse in (False, True):
