@@ -84,6 +84,15 @@ class _Node(nn.Module):
     pass
 
 
+class _SharedProbe:
+    """Probe x gallery: the shared side-0 graph's two SplineConv layers (fp32 rows of one graph),
+    computed once per forward in the prologue and handed to every chunk in place of its side-0
+    operand rows (chunk slicing leaves it whole)."""
+
+    def __init__(self, y):
+        self.y = y
+
+
 class _TailView:
     """Pairs [r0, r1) of a (sub-)batch ``part`` for the tail stages (AFA-U, soft top-k, Hungarian,
     selection, classifier): device views of the pair sizes, no copies; ``pair_range`` is its range in
@@ -401,7 +410,9 @@ class Net(nn.Module):
             plan = ops.spline_plan(bt.src[side], bt.dst[side], bt.pseudo[side], nn_, bt.nmax[side],
                                    bt.max_graph_edges(side))
         if side == 0 and bt.shared0 and bt.B > 1:
-            return (plan,) + self._spline_shared(wp, bt, cscale)
+            return (plan,) + self._spline_shared(wp, bt, cscale, probe=x_op if isinstance(x_op, _SharedProbe) else None)
+        if isinstance(x_op, _SharedProbe):          # a one-pair chunk of a probe x gallery batch
+            x_op = None
         x0 = bt.x[side]
         if x_op is None:
             x_op = ops.cast_bf16(x0) if op == torch.bfloat16 else x0
@@ -432,9 +443,24 @@ class Net(nn.Module):
             return 0
         return 2 if side == 0 else 1
 
-    def _spline_shared(self, wp, bt, cscale):
-        """Probe x gallery: the shared side-0 graph's two SplineConv layers once (pair 0's slice),
-        then broadcast to all pairs with the per-pair coefficient scaling (fpm_rows_bcast_scale)."""
+    def _spline_shared(self, wp, bt, cscale, probe=None):
+        """Probe x gallery: the shared side-0 graph's two SplineConv layers once (pair 0's slice; or
+        ``probe``, the forward's prologue result), then broadcast to all pairs with the per-pair
+        coefficient scaling (fpm_rows_bcast_scale)."""
+        dev = bt.device
+        y = probe.y if probe is not None else self._probe_rows(wp, bt)
+        nm = bt.nmax[0]
+        f32 = self._sc_f32(bt)
+        op = torch.float32 if f32 else torch.bfloat16
+        split = self._kp_split(0, bt)
+        out = torch.empty(bt.B * nm, 3 * C.NODE_FEATURE_DIM if split else C.NODE_FEATURE_DIM, device=dev, dtype=op)
+        outf = torch.empty(bt.B * nm, C.NODE_FEATURE_DIM, device=dev, dtype=torch.float32) if self._keep_feats else None
+        ops.rows_bcast_scale(y, bt.B, coef=cscale, out_f=outf, out_t=out, split=split)
+        return out, outf
+
+    def _probe_rows(self, wp, bt):
+        """The shared probe graph's SplineConv output rows (nmax_0, 768) fp32 (both layers, pair 0's
+        graph; the same for every chunk of a probe x gallery batch)."""
         dev = bt.device
         f32 = self._sc_f32(bt)
         op = torch.float32 if f32 else torch.bfloat16
@@ -451,11 +477,7 @@ class Net(nn.Module):
         ops.spline_conv(x_op, plan, e0, nm, nm, nv, W0, wp["bias0"], yws, 0, out_t=h)
         y = torch.empty(nm, C.NODE_FEATURE_DIM, device=dev, dtype=torch.float32)
         ops.spline_conv(h, plan, e0, nm, nm, nv, W1, wp["bias1"], yws, 1, xres=x0, out_f=y)
-        split = self._kp_split(0, bt)
-        out = torch.empty(bt.B * nm, 3 * C.NODE_FEATURE_DIM if split else C.NODE_FEATURE_DIM, device=dev, dtype=op)
-        outf = torch.empty(bt.B * nm, C.NODE_FEATURE_DIM, device=dev, dtype=torch.float32) if self._keep_feats else None
-        ops.rows_bcast_scale(y, bt.B, coef=cscale, out_f=outf, out_t=out, split=split)
-        return out, outf
+        return y
 
     def _afau_norm1_bufs(self, rows, dev):
         """The block's first-norm outputs: fp32 rows and (bf16 modes) the zero-K-padded operand copy."""
@@ -837,7 +859,7 @@ class Net(nn.Module):
         that splits the chunk's tail (AFA-U, soft top-k) into pair sub-ranges -- called with
         (tail view, b0, b1) right after each sub-range's soft top-k is queued."""
         dev = part.device
-        x_ops = tuple(None if t is None else t[b0 * part.nmax[s]:b1 * part.nmax[s]]
+        x_ops = tuple(None if t is None else t if isinstance(t, _SharedProbe) else t[b0 * part.nmax[s]:b1 * part.nmax[s]]
                       for s, t in enumerate(xop or (None, None)))
         r = self.run_gpu_stage(part, keep_feats, s_out=o["s"][b0:b1], ss_out=o["ss"][b0:b1],
                                gc=(gc[0][b0:b1], gc[1][b0:b1]), x_ops=x_ops, plans=plans,
@@ -975,6 +997,9 @@ class Net(nn.Module):
             xop_ = None
             if not self._sc_f32(bt) and cast:
                 xop_ = tuple(None if (s == 0 and bt.shared0) else ops.cast_bf16(bt.x[s]) for s in range(2))
+                if bt.shared0 and bt.B > 1:
+                    # the probe's SplineConv once per forward, not once per chunk
+                    xop_ = (_SharedProbe(self._probe_rows(self.packed(dev), bt)), xop_[1])
             self._mark("pro_cast")
             col_ = None
             if self.regression:
