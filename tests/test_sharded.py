@@ -59,6 +59,27 @@ def test_sharded_equals_single_device(dtype, devices):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", [96, 300])
+def test_sharded_equals_single_device_fp32_chain(n):
+    """Boxes above the fp64 k chain's 64 keypoints: the fp32 GNN / Sinkhorn kernels under ShardedNet's
+    HIP-graph replay equal the eager single-device forward bit for bit -- at n = 300 incl. the
+    split streaming Sinkhorn (its workspace allocated and its counters zeroed inside the captured
+    graphs) and the GNN layers' Hilbert block order."""
+    sd = params.init_params(8)
+    pairs = synth.make_batch(44, 5, [n, n - 7, n, n - 20, n], n2=[n, n, n - 11, n, n - 3])
+    net = fpm.Net(regression=True, dtype="bf16", backbone=False)
+    net.load_state_dict(sd)
+    bt = DeviceBatch.from_pairs(pairs, DEV)
+    assert (bt.ord2 is not None) == (n > 256)
+    ref = net.run(bt)
+    sh = ShardedNet(net, devices=[0, 0])
+    for _ in range(2):                              # capture, then replay
+        out = sh.run(bt)
+        for k in ("s", "ss", "ds_mat", "perm_mat", "k_prob", "cls_prob"):
+            assert torch.equal(out[k], ref[k]), (k, n)
+
+
+@pytest.mark.gpu
 def test_sharded_forward_data_dict():
     """The reference call shape: ShardedNet(net)(data_dict) -> data_dict with the reference keys,
     equal to Net(data_dict) (gt_perm_mat / label sliced per shard, losses over the whole batch)."""
