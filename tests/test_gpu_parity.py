@@ -495,10 +495,13 @@ def test_forward_data_dict_surface(sd):
     assert abs(float(out["cls_loss"]) - float(ref["cls_loss"])) < 1e-4
 
 
-def test_chunked_pipeline_bitwise(sd):
+@pytest.mark.parametrize("n", [48, 96])
+def test_chunked_pipeline_bitwise(sd, n):
     """Pipelined sub-batches (host LSA of chunk c overlapping GPU work of c+1) give bit-identical
-    outputs to the single-chunk forward; the same property makes pair-sharding across GPUs exact."""
-    pairs = synth.make_batch(9, 7, 48, n2=[48, 40, 44, 48, 30, 48, 47])
+    outputs to the single-chunk forward; the same property makes pair-sharding across GPUs exact.
+    n = 48: the fp64 k chain; n = 96: the fp32 GNN / Sinkhorn kernels."""
+    d = n - 48
+    pairs = synth.make_batch(9, 7, n, n2=[x + d for x in (48, 40, 44, 48, 30, 48, 47)])
     net = fpm.Net(regression=True, backbone=False, dtype="bf16")
     net.load_state_dict(sd)
     bt = DeviceBatch.from_pairs(pairs, DEV)
@@ -576,13 +579,14 @@ def _view_i32(ptr, n):
     return out
 
 
-@pytest.mark.parametrize("dtype,regression", [("bf16", True), ("f32", False)])
-def test_graph_replay_bitwise_equals_eager(sd, dtype, regression):
+@pytest.mark.parametrize("dtype,regression,d", [("bf16", True, 0), ("f32", False, 0), ("bf16", True, 40)])
+def test_graph_replay_bitwise_equals_eager(sd, dtype, regression, d):
     """Multi-chunk forwards replay HIP graphs captured on the batch's first forward (prologue, and
     per chunk its plans and GPU stage): bit-identical to the eager launches on a ragged batch, on
-    the capturing forward and on replays; the returned reference outputs are fresh tensors."""
-    pairs = synth.make_batch(23, 11, [48, 40, 44, 48, 30, 48, 47, 41, 48, 36, 45],
-                             n2=[48, 47, 40, 30, 48, 44, 48, 48, 39, 48, 42])
+    the capturing forward and on replays; the returned reference outputs are fresh tensors.
+    d = 40: boxes of 88 keypoints (the fp32 GNN / Sinkhorn kernels; below 64 the fp64 k chain)."""
+    pairs = synth.make_batch(23, 11, [x + d for x in (48, 40, 44, 48, 30, 48, 47, 41, 48, 36, 45)],
+                             n2=[x + d for x in (48, 47, 40, 30, 48, 44, 48, 48, 39, 48, 42)])
     bt = DeviceBatch.from_pairs(pairs, DEV)
     runs = {}
     for graphs in (False, True):
