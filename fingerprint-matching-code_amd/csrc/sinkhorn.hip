@@ -32,6 +32,7 @@ struct SinkArgs {
     // streaming kernel, pairs split over `split` workgroups along a (1 = one workgroup per pair):
     // B pairs, per-pair arrival counters (zeroed before the launch), exchange slots of xslot floats
     int B, split;
+    int xacq;      // 1: agent acquire fence after each exchange poll (default 0: sc1 loads, no fence)
     int* xcnt;
     float* xbuf;
     long xslot;
@@ -1005,15 +1006,25 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
     if (tid == 0) { ud_sh = 0.f; redo_sh = 0; xfail_sh = 0; }
     __syncthreads();
 
-    // One exchange round (cdna_hip_programming.md Guideline 16, R1 form with the acquire kept):
-    // the partial sums newC[0, limC) (and the partial maxima xmax when `two`) leave as 16-B sc1
-    // stores into this sibling's slot, every wave drains its stores, a barrier, then ONE lane adds
-    // to the pair's arrival counter (agent scope) and polls it (relaxed loads, bounded: a missing
-    // sibling sets xfail and the outputs become NaN instead of the launch hanging), ONE agent
-    // acquire, a barrier; the slots are then read with plain vector loads.  Slots alternate
-    // between two buffers: a sibling's round r + 2 store can only follow every sibling's round
-    // r + 1 arrival, which follows its reads of round r.
+    // One exchange round (cdna_hip_programming.md Guideline 16, R1 / table row 1): the partial sums
+    // newC[0, limC) (and the partial maxima xmax when `two`) leave as 16-B sc1 stores into this
+    // sibling's slot, every wave drains its stores, a barrier, then ONE lane adds to the pair's
+    // arrival counter (agent scope) and polls it (relaxed sc1 loads, bounded: a missing sibling sets
+    // xfail and the outputs become NaN instead of the launch hanging), a barrier; the slots are then
+    // read with sc1 buffer loads only (ld_slot; FPM_SK_XACQ=1 adds an agent acquire fence).  Slots
+    // alternate between two buffers: a sibling's round r + 2 store can only follow every sibling's
+    // round r + 1 arrival, which follows its reads of round r.
     auto slot_of = [&](int g, int r) { return a.xbuf + (((long)b * G + g) * 2 + (r & 1)) * a.xslot; };
+    // a slot's 16 B at float offset `off`: an sc1 buffer load (bypasses this CU's L1; the Guideline-16
+    // table's row 1 -- sc1 stores, one lane's agent-scope counter add after every storing wave's drain
+    // and a barrier, one lane's sc1 poll, every load of the bytes sc1, one workgroup per CU -- needs no
+    // acquire fence then; a.xacq = 1 keeps the fence anyway)
+    auto ld_slot = [&](int g, int r, long off) {
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)slot_of(g, r), (short)0, (int)(a.xslot * 4), 0x00020000);
+        const sk_u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off * 4), 0, 16);
+        return make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
+    };
     auto exchange = [&](bool two) {
         float* slot = slot_of(j, xr);
         const __amdgpu_buffer_rsrc_t rs =
@@ -1042,8 +1053,12 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
                 __builtin_amdgcn_s_sleep(1);
                 if (++spins > (1u << 20)) xfail_sh = 1;
             }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (a.xacq) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            } else {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: keeps the loads below
+            }
         }
         __syncthreads();
         ++xr;
@@ -1235,9 +1250,9 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
                 }
                 exchange(false);
                 for (int q = tid; q < nq; q += 1024) {
-                    float4 t = *(const float4*)(slot_of(0, xr - 1) + 4 * q);
+                    float4 t = ld_slot(0, xr - 1, 4 * q);
                     for (int g = 1; g < GP; ++g) {
-                        const float4 o = *(const float4*)(slot_of(g, xr - 1) + 4 * q);
+                        const float4 o = ld_slot(g, xr - 1, 4 * q);
                         t.x += o.x; t.y += o.y; t.z += o.z; t.w += o.w;
                     }
                     const float4 sh = *(const float4*)&potC[4 * q];
@@ -1312,15 +1327,13 @@ __global__ __launch_bounds__(1024) void sinkhorn_stream_kernel(SinkArgs a) {
             }
             exchange(true);
             for (int q = tid; q < nq; q += 1024) {
-                const float* s0 = slot_of(0, xr - 1);
-                float4 t = *(const float4*)(s0 + 4 * q), m4 = *(const float4*)(s0 + a.xslot / 2 + 4 * q);
+                float4 t = ld_slot(0, xr - 1, 4 * q), m4 = ld_slot(0, xr - 1, a.xslot / 2 + 4 * q);
                 float sv[4] = {t.x, t.y, t.z, t.w}, mv[4] = {m4.x, m4.y, m4.z, m4.w};
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
                     if (mv[k] == -INFINITY) sv[k] = 0.f;
                 for (int g = 1; g < GP; ++g) {
-                    const float* sg = slot_of(g, xr - 1);
-                    const float4 to = *(const float4*)(sg + 4 * q), mo = *(const float4*)(sg + a.xslot / 2 + 4 * q);
+                    const float4 to = ld_slot(g, xr - 1, 4 * q), mo = ld_slot(g, xr - 1, a.xslot / 2 + 4 * q);
                     const float so[4] = {to.x, to.y, to.z, to.w}, mov[4] = {mo.x, mo.y, mo.z, mo.w};
 #pragma unroll
                     for (int k = 0; k < 4; ++k) lse_combine(mv[k], sv[k], mov[k], mov[k] == -INFINITY ? 0.f : so[k]);
@@ -1624,6 +1637,15 @@ int& stream_split_flag() {
     return v;
 }
 
+// FPM_SK_XACQ=1: the split Sinkhorn's exchange keeps an agent-scope acquire fence after each poll
+int& stream_xacq_flag() {
+    static int v = [] {
+        const char* e = getenv("FPM_SK_XACQ");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
 namespace {
 long sk_cnt_bytes(int B) { return ((long)B * 4 + 15) / 16 * 16; }
 long sk_xslot(int n1max, int n2max) { return 2 * (long)((((n1max > n2max ? n1max : n2max) + 3) / 4) * 4); }
@@ -1679,6 +1701,7 @@ extern "C" int fpm_sinkhorn_log_fwd_ws(const float* s, long s_sb, long s_si, lon
         FPM_CHECK_ARG(ws_bytes >= need, "sinkhorn: workspace %ld B < %ld B (fpm_sinkhorn_ws_bytes)", ws_bytes, need);
         FPM_CHECK_ARG(((uintptr_t)ws & 15) == 0, "sinkhorn: workspace not 16-B aligned");
         a.split = stream_split_flag();
+        a.xacq = stream_xacq_flag();
         a.xcnt = (int*)ws;
         a.xbuf = (float*)((char*)ws + sk_cnt_bytes(B));
         a.xslot = sk_xslot(n1max, n2max);
